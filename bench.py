@@ -1,0 +1,283 @@
+#!/usr/bin/env python3
+"""bench.py -- validated edge-interpolants/sec of the MI355X motion-validation rake.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--edges E] [--no-cpu]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1], SURVEY.md §8(d) config 2, set B): Panda 7-DOF
+(PandaBase<0,0,0>), the 14-sphere cage of the reference's collision benchmark
+(scripts/cpp/benchmark_collision_checks.cc:33-51), E = 2^20 edges per GPU between
+collision-free endpoints with edge length capped at 1.0 rad (n_e = 4 -> 32 interpolants
+per edge).  Endpoints are synthetic (seeded uniform draws, scaled by the Panda joint
+limits), generated and filtered on the GPU before timing; inputs are resident in HBM.
+
+One step = one vgpu_validate_motions launch over the rank's whole edge batch (reference
+semantics: validate_motion per edge, 8-lane rake, early exit on the first colliding
+block).  Units = sum over edges of 8 * n_e (validate.hh:41).  Multi-GPU: each rank owns
+an independent shard of edges (weak scaling, no collective on the data path); the timed
+region is bracketed by barrier + synchronize and the max over ranks is reported.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "mr-vamp_amd"))
+
+CAGE = [(0.55, 0, 0.25), (0.35, 0.35, 0.25), (0, 0.55, 0.25), (-0.55, 0, 0.25), (-0.35, -0.35, 0.25),
+        (0, -0.55, 0.25), (0.35, -0.35, 0.25), (0.35, 0.35, 0.8), (0, 0.55, 0.8), (-0.35, 0.35, 0.8),
+        (-0.55, 0, 0.8), (-0.35, -0.35, 0.8), (0, -0.55, 0.8), (0.35, -0.35, 0.8)]
+S_M = [5.9342, 3.6652, 5.9342, 3.2289, 5.9342, 3.9095999999999997, 5.9342]
+S_A = [-2.9671, -1.8326, -2.9671, -3.1416, -2.9671, -0.0873, -2.9671]
+HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+FP32_PEAK_TFLOPS = 157.3    # MI355X_MICROARCH.md: FP32 vector (= FP32 matrix) peak
+EDGE_BYTES = 7 * 4 * 2 + 1 + 4  # start + goal in, ok + n_e out
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--edges", type=int, default=1 << 20, help="edges per GPU")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
+    ap.add_argument("--fk-leg", action="store_true", default=True)
+    return ap.parse_args()
+
+
+def make_edges(torch, vamp, env, robot, n_edges, seed, dev):
+    """Valid-endpoint edges, length capped at 1.0 (set B)."""
+    g = torch.Generator(device=dev)
+    g.manual_seed(seed)
+    sm = torch.tensor(S_M, device=dev)
+    sa = torch.tensor(S_A, device=dev)
+    pool = []
+    have = 0
+    need = 2 * n_edges
+    while have < need:
+        m = max(1 << 20, int((need - have) / 0.17 * 1.1))
+        u = torch.rand((m, 7), generator=g, device=dev, dtype=torch.float32)
+        q = torch.addcmul(sa, u, sm).contiguous()
+        ok = torch.empty(m, dtype=torch.uint8, device=dev)
+        robot.fkcc_device(q.data_ptr(), m, env, ok.data_ptr())
+        torch.cuda.synchronize(dev)
+        v = q[ok.bool()]
+        pool.append(v)
+        have += v.shape[0]
+    vq = torch.cat(pool)[:need]
+    s = vq[0::2].contiguous()
+    gl = vq[1::2].contiguous()
+    d = torch.linalg.vector_norm((gl - s).double(), dim=1)
+    scale = torch.clamp(1.0 / torch.clamp(d, min=1e-9), max=1.0).float()
+    gl = (s + (gl - s) * scale[:, None]).contiguous()
+    return s, gl
+
+
+def cpu_baseline(starts, goals, seconds):
+    """The C restatement (oracle/, kind "port") on this host's cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as op
+
+    op.build()
+    env = op.Env()
+    for c in CAGE:
+        env.add_sphere(c, np.float32(0.2))
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    # calibrate on a small slice, then run ~`seconds` worth
+    n0 = min(len(starts), 2048 * threads)
+    t = time.perf_counter()
+    op.validate_motions(env, starts[:n0], goals[:n0], (0, 0, 0), threads)
+    dt = max(time.perf_counter() - t, 1e-3)
+    n = int(min(len(starts), max(n0, n0 * seconds / dt)))
+    t = time.perf_counter()
+    ok, nb = op.validate_motions(env, starts[:n], goals[:n], (0, 0, 0), threads)
+    dt = time.perf_counter() - t
+    units = float(8 * nb.astype(np.int64).sum())
+    return {"value": units / dt, "unit": "interpolants/s", "cores": threads, "kind": "port",
+            "sample": f"{n} edges of the same workload ({int(units)} interpolants), oracle/vamp_oracle.c "
+                      f"validate_motion (rake=8, early exit), {threads} threads, {dt:.1f} s",
+            "cpu_model": cpu_model(), "ok_fraction": float(ok.mean())}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def algorithmic_flops_per_edge(starts, goals, n=256):
+    """Executed float ops per edge under reference semantics, counted by the instrumented
+    restatement (oracle/vamp_oracle.c vo_stats.flops) on a sample of the bench's edges."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
+
+    import oracle_py as op
+
+    op.build()
+    env = op.Env()
+    for c in CAGE:
+        env.add_sphere(c, np.float32(0.2))
+    ce = env.c()
+    tot = 0.0
+    for i in range(n):
+        st = op.VoStats(np.inf, np.inf, 0.0)
+        nn = C.c_int()
+        s = np.ascontiguousarray(starts[i], np.float32)
+        g = np.ascontiguousarray(goals[i], np.float32)
+        op.lib().vo_panda_validate_motion(C.byref(ce), op.fp(s), op.fp(g), 0, 0, 0, C.byref(nn), C.byref(st))
+        tot += st.flops
+    return tot / n
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    if world > 1:
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import vamp_amd as vamp
+
+    ctx = vamp.context(local)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+    env = vamp.Environment()
+    for c in CAGE:
+        env.add_sphere(vamp.Sphere(c, 0.2))
+    robot = vamp.panda_0_0
+
+    E = a.edges
+    starts, goals = make_edges(torch, vamp, env, robot, E, seed=1234 + 7919 * rank, dev=dev)
+    ok = torch.empty(E, dtype=torch.uint8, device=dev)
+    nb = torch.empty(E, dtype=torch.int32, device=dev)
+
+    def step():
+        robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, env, ok.data_ptr(), nb.data_ptr(), ctx)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    units_local = float(8 * nb.long().sum().item())
+    ok_frac = float(ok.float().mean().item())
+
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(a.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    wall = t1 - t0
+    kern_ms = ev0.elapsed_time(ev1) / a.steps  # HIP events on the launch stream
+
+    tt = torch.tensor([wall, units_local], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = tt.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = tt.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        wall_max, units_all = float(mx[0]), float(sm[1])
+    else:
+        wall_max, units_all = wall, units_local
+
+    # secondary leg (untimed for the headline): the HBM-bound sphere_fk stream, 4M configs
+    fk_leg = None
+    if a.fk_leg and rank == 0:
+        nq = 1 << 22
+        q = torch.rand((nq, 7), device=dev, dtype=torch.float32) * 6.0 - 3.0
+        out = torch.empty((3, 59, nq), device=dev, dtype=torch.float32)
+        for _ in range(2):
+            robot.sphere_fk_device(q.data_ptr(), nq, out.data_ptr(), nq, ctx)
+        f0 = torch.cuda.Event(enable_timing=True)
+        f1 = torch.cuda.Event(enable_timing=True)
+        f0.record(stream)
+        reps = 10
+        for _ in range(reps):
+            robot.sphere_fk_device(q.data_ptr(), nq, out.data_ptr(), nq, ctx)
+        f1.record(stream)
+        torch.cuda.synchronize(dev)
+        fk_ms = f0.elapsed_time(f1) / reps
+        gbs = 736.0 * nq / (fk_ms * 1e-3) / 1e9
+        fk_leg = {"kernel": "panda_sphere_fk_kernel", "bound": "hbm", "configs": nq, "ms": fk_ms,
+                  "configs_per_s": nq / (fk_ms * 1e-3), "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                  "frac": gbs / HBM_PEAK_GBS, "bytes_per_config": 736}
+        del q, out
+
+    if rank == 0:
+        s_np = starts[: 1 << 17].cpu().numpy()
+        g_np = goals[: 1 << 17].cpu().numpy()
+        flops_edge = algorithmic_flops_per_edge(s_np, g_np)
+        achieved = flops_edge * E / (kern_ms * 1e-3) / 1e12
+        cpu = None
+        if not a.no_cpu and world == 1:
+            cpu = cpu_baseline(s_np, g_np, a.cpu_seconds)
+        ms_step = wall_max / a.steps * 1e3
+        line = {
+            "metric": "validated edge-interpolants/sec (Panda 7-DOF FK+CC)",
+            "value": units_all * a.steps / wall_max,
+            "unit": "interpolants/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded uniform Panda configurations; collision-free endpoints, edges capped at 1.0)",
+            "config": {
+                "workload": "BASELINE configs[1]: Panda 7-DOF, 2^20 edges per GPU, 14-sphere cage, "
+                            "validate_motion (rake 8, resolution 32, early exit)",
+                "robot": "PandaBase<0,0,0>",
+                "edges_per_gpu": E,
+                "interpolants_per_gpu": units_local,
+                "edge_valid_fraction": ok_frac,
+                "parallelism": f"dp{world} (independent edge shards, no collective)",
+            },
+            "roofline": {
+                "kernel": "panda_validate_kernel",
+                "bound": "valu",
+                "achieved": achieved,
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP32_PEAK_TFLOPS,
+                "traffic": None,
+                "algorithmic_flops_per_edge": flops_edge,
+                "kernel_ms": kern_ms,
+                "hbm_frac": EDGE_BYTES * E / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+            },
+            "roofline_hbm_fk": fk_leg,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

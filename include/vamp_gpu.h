@@ -1,0 +1,114 @@
+/* vamp_gpu.h -- C ABI of the MI355X (gfx950) motion-validation rake.
+ *
+ * Drop-in boundary for the reference's hot path (jamesmotes/mr-vamp):
+ *   vamp::planning::validate_motion / validate_vector  (src/impl/vamp/planning/validate.hh:23-75)
+ *   Robot::fkcc<rake>                                 (src/impl/vamp/robots/panda_base.hh:53-58)
+ *   Robot::sphere_fk<rake>                            (src/impl/vamp/robots/panda_base.hh:67-71)
+ *   collision::Environment<float> + Environment.add_* (src/impl/vamp/collision/environment.hh:12-66,
+ *                                                     src/impl/vamp/bindings/environment.cc:107-146)
+ * The reference entry points take one edge / one 8-lane block per call; this ABI takes
+ * batches (see INTEGRATION.md for the cgo/ctypes/C++ bindings a maintainer would add).
+ *
+ * Conventions
+ *   - Every function returns int: VGPU_OK (0) or a negative VGPU_ERR_* code; the message
+ *     is available from vgpu_last_error(ctx).  No C++ exception crosses this boundary.
+ *   - Batch functions take DEVICE pointers and enqueue asynchronously on the context's
+ *     stream (vgpu_ctx_set_stream / vgpu_sync).  The *_host variants copy in and out and
+ *     synchronise (convenience; they measure PCIe, not the kernels).
+ *   - Configurations are row-major float32 [n][dim] (reference ConfigurationArray).
+ *   - Results use the reference's polarity: 1 = valid (collision-free), 0 = in collision.
+ *   - A context is bound to one HIP device and must be used from one host thread at a time.
+ */
+#ifndef VAMP_GPU_H
+#define VAMP_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VGPU_OK 0
+#define VGPU_ERR_INVALID_ARG (-1)
+#define VGPU_ERR_HIP (-2)
+#define VGPU_ERR_OOM (-3)
+#define VGPU_ERR_UNSUPPORTED (-4)
+#define VGPU_ERR_RSQRT (-5)
+
+typedef struct vgpu_ctx vgpu_ctx;
+typedef struct vgpu_env vgpu_env;
+
+/* Robot selection.  kind = VGPU_ROBOT_PANDA reproduces vamp::robots::PandaBase<X100, Y100, Z100>
+ * (robots/panda_base.hh:15-75); the fork's default vamp::robots::Panda is base (200, 200, 0)
+ * (robots/panda_grid.hh:39). */
+#define VGPU_ROBOT_PANDA 1
+typedef struct vgpu_robot {
+    int32_t kind;
+    int32_t base_x100, base_y100, base_z100;
+} vgpu_robot;
+
+/* ---- context -------------------------------------------------------------------------- */
+/* Creates a context on HIP device `device` and probes the host CPU's rsqrt approximation
+ * (the reference culls with v * _mm256_rsqrt_ps(v), vector/avx.hh:411-415), uploading it
+ * to the device.  Fails with VGPU_ERR_RSQRT if the host rsqrt is not table-representable. */
+int vgpu_ctx_create(int device, vgpu_ctx **out);
+void vgpu_ctx_destroy(vgpu_ctx *ctx);
+const char *vgpu_last_error(const vgpu_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL restores
+ * the context's own stream. */
+int vgpu_ctx_set_stream(vgpu_ctx *ctx, void *hip_stream);
+int vgpu_sync(vgpu_ctx *ctx);
+/* rsqrt table in use: kbits and the 2 << kbits entries (host copy).  Replacing it is for
+ * testing cross-host parity only. */
+int vgpu_rsqrt_table(const vgpu_ctx *ctx, int *kbits, const uint32_t **table);
+int vgpu_rsqrt_table_set(vgpu_ctx *ctx, const uint32_t *table, int kbits);
+
+/* ---- environment (collision::Environment<float>) ---------------------------------------- */
+int vgpu_env_create(vgpu_ctx *ctx, vgpu_env **out);
+void vgpu_env_destroy(vgpu_env *env);
+/* Shape constructors of collision/shapes.hh + factory.hh, with the routing of
+ * bindings/environment.cc:107-146 (axis_3_z == 1 -> z-aligned cuboid; xv == yv == 0 ->
+ * z-aligned capsule) and the min_distance sort of environment.hh:40-66. */
+int vgpu_env_add_sphere(vgpu_env *env, const float center[3], float radius);
+int vgpu_env_add_cuboid_axes(vgpu_env *env, const float center[3], const float axis_1[3], const float axis_2[3],
+                             const float axis_3[3], const float half_extents[3]);
+int vgpu_env_add_cuboid_euler(vgpu_env *env, const float center[3], const float euler_xyz[3],
+                              const float half_extents[3]);
+int vgpu_env_add_capsule_endpoints(vgpu_env *env, const float p1[3], const float p2[3], float radius);
+int vgpu_env_add_capsule_euler(vgpu_env *env, const float center[3], const float euler_xyz[3], float radius,
+                               float length);
+/* obstacle counts: spheres, capsules, z-capsules, cuboids, z-cuboids */
+int vgpu_env_counts(const vgpu_env *env, int32_t counts[5]);
+/* Copy the (sorted) environment to the device.  Called implicitly by the batch functions
+ * when the environment changed since the last upload. */
+int vgpu_env_upload(vgpu_env *env);
+
+/* ---- batched hot path (device pointers, asynchronous) ------------------------------------ */
+/* Robot::sphere_fk for n configurations q[n][dim] -> xyz[3][n_spheres][ld] (SoA, world frame,
+ * base offset added).  ld >= n. */
+int vgpu_sphere_fk(vgpu_ctx *ctx, const vgpu_robot *robot, const float *q, size_t n, float *xyz, size_t ld);
+/* Robot::fkcc<rake> of each configuration broadcast to the whole rake (the per-configuration
+ * mask, as used by validate(q) and the PRM sampler): valid[i] = 1 if q[i] is collision-free. */
+int vgpu_fkcc(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n, uint8_t *valid);
+/* validate_motion<Robot, 8, Robot::resolution>(starts[i], goals[i], env) for every edge:
+ * ok[i] = 1 if the whole edge is valid.  n_blocks (optional) receives n_e, the rake
+ * back-step count of validate.hh:41 (interpolants = 8 * n_e). */
+int vgpu_validate_motions(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *starts,
+                          const float *goals, size_t n_edges, uint8_t *ok, int32_t *n_blocks);
+
+/* ---- host-pointer conveniences (copy + synchronise) ---------------------------------------- */
+int vgpu_sphere_fk_host(vgpu_ctx *ctx, const vgpu_robot *robot, const float *q, size_t n, float *xyz);
+int vgpu_fkcc_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n,
+                   uint8_t *valid);
+int vgpu_validate_motions_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *starts,
+                               const float *goals, size_t n_edges, uint8_t *ok, int32_t *n_blocks);
+
+/* ---- robot metadata ------------------------------------------------------------------------ */
+/* dimension, resolution, n_spheres of a robot kind (robots/panda_base.hh:19-23) */
+int vgpu_robot_info(int32_t kind, int32_t *dimension, int32_t *resolution, int32_t *n_spheres);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

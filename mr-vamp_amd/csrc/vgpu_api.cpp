@@ -1,0 +1,594 @@
+// vgpu_api.cpp -- host runtime behind include/vamp_gpu.h.
+//
+// Owns: HIP device/stream selection, the host-rsqrt table probe + upload, the
+// collision::Environment<float> builder (shape constructors of collision/shapes.hh and
+// collision/factory.hh, the add_* routing of bindings/environment.cc:107-146 and the
+// min_distance sort of collision/environment.hh:40-66), device-resident obstacle
+// tables, argument validation and error reporting.  Kernels live in vgpu_kernels.hip.
+#include <hip/hip_runtime.h>
+#include <immintrin.h>
+
+#include <algorithm>
+#include <array>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/vamp_gpu.h"
+#include "vgpu_device.hh"
+
+extern "C" {
+hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float by, float bz, float* out,
+                                       size_t ld, hipStream_t st);
+hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, float bx, float by, float bz,
+                                  uint8_t* valid, hipStream_t st);
+hipError_t vgpu_launch_panda_validate(const float* starts, const float* goals, size_t n_edges, const EnvView* env,
+                                      float bx, float by, float bz, uint8_t* ok, int32_t* n_blocks,
+                                      hipStream_t st);
+}
+
+namespace {
+
+constexpr int kPandaDim = 7;
+constexpr int kPandaResolution = 32;  // robots/panda_base.hh:21
+constexpr int kPandaSpheres = 59;     // robots/panda/fk.hh:93
+
+inline uint32_t f2u(float f)
+{
+    uint32_t u;
+    std::memcpy(&u, &f, 4);
+    return u;
+}
+inline float u2f(uint32_t u)
+{
+    float f;
+    std::memcpy(&f, &u, 4);
+    return f;
+}
+
+// Probe the host's _mm256_rsqrt_ps as a table over (exponent parity, top K mantissa bits)
+// for inputs with biased exponent 126 + parity, plus the exact exponent-shift rule for all
+// other exponents.  K is the smallest width that reproduces every input of the two
+// reference binades (8..23; 23 = the full 2 x 2^23 table).
+__attribute__((target("avx2"))) int probe_host_rsqrt(std::vector<uint32_t>& lut, int& kbits, std::string& err)
+{
+    std::vector<uint32_t> full((size_t)2 << 23);
+    for (uint32_t p = 0; p < 2; ++p) {
+        for (uint32_t m = 0; m < (1u << 23); m += 8) {
+            alignas(32) float in[8], out[8];
+            for (int l = 0; l < 8; ++l) in[l] = u2f(((126u + p) << 23) | (m + (uint32_t)l));
+            _mm256_store_ps(out, _mm256_rsqrt_ps(_mm256_load_ps(in)));
+            for (int l = 0; l < 8; ++l) full[((size_t)p << 23) | (m + (uint32_t)l)] = f2u(out[l]);
+        }
+    }
+    int K = -1;
+    for (int k = 8; k <= 23 && K < 0; ++k) {
+        bool ok = true;
+        const uint32_t lowmask = (1u << (23 - k)) - 1u;
+        for (size_t i = 0; i < ((size_t)2 << 23) && ok; ++i) {
+            const size_t rep = i & ~(size_t)lowmask;
+            ok = full[i] == full[rep];
+        }
+        if (ok) K = k;
+    }
+    if (K < 0) {
+        err = "host rsqrt is not a function of (parity, mantissa)";
+        return VGPU_ERR_RSQRT;
+    }
+    lut.assign((size_t)2 << K, 0u);
+    for (uint32_t p = 0; p < 2; ++p)
+        for (uint32_t j = 0; j < (1u << K); ++j) lut[((size_t)p << K) | j] = full[((size_t)p << 23) | ((size_t)j << (23 - K))];
+    // exponent-shift rule over every normal exponent (sampled)
+    uint64_t s = 0x243F6A8885A308D3ull;
+    for (int e = 1; e < 255; ++e) {
+        for (int t = 0; t < 2048; ++t) {
+            s ^= s << 13;
+            s ^= s >> 7;
+            s ^= s << 17;
+            const float x = u2f(((uint32_t)e << 23) | (uint32_t)(s & 0x7FFFFF));
+            const float want = _mm_cvtss_f32(_mm_rsqrt_ss(_mm_set_ss(x)));
+            const uint32_t p = (uint32_t)e & 1u;
+            const int shift = (e - (int)(126 + p)) / 2;
+            const uint32_t tb = lut[((size_t)p << K) | ((f2u(x) & 0x7FFFFFu) >> (23 - K))];
+            const int re = (int)((tb >> 23) & 0xFF) - shift;
+            if (re <= 0 || re >= 255) continue;
+            if (u2f(tb - ((uint32_t)shift << 23)) != want) {
+                err = "host rsqrt exponent scaling is not exact";
+                return VGPU_ERR_RSQRT;
+            }
+        }
+    }
+    kbits = K;
+    return VGPU_OK;
+}
+
+}  // namespace
+
+struct vgpu_ctx {
+    int device = 0;
+    hipStream_t own = nullptr;
+    hipStream_t cur = nullptr;
+    std::string err;
+    std::vector<uint32_t> lut;
+    int kbits = 0;
+    uint32_t* lut_dev = nullptr;
+    // staging for the *_host conveniences
+    void* stage = nullptr;
+    size_t stage_bytes = 0;
+};
+
+struct vgpu_env {
+    vgpu_ctx* ctx = nullptr;
+    std::vector<std::array<float, 5>> spheres;
+    std::vector<std::array<float, 9>> capsules, zcapsules;
+    std::vector<std::array<float, 16>> cuboids, zcuboids;
+    bool dirty = true;
+    float* dev = nullptr;
+    size_t dev_floats = 0;
+    size_t off[5] = {0, 0, 0, 0, 0};
+};
+
+#define HIPCHK(ctx, expr)                                                                          \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) {                                                                    \
+            (ctx)->err = std::string(#expr) + ": " + hipGetErrorString(e_);                        \
+            return VGPU_ERR_HIP;                                                                   \
+        }                                                                                          \
+    } while (0)
+
+static int fail(vgpu_ctx* ctx, int code, const char* msg)
+{
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+// ---------------------------------------------------------------------------------------
+// context
+// ---------------------------------------------------------------------------------------
+extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
+{
+    if (!out) return VGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    auto* c = new (std::nothrow) vgpu_ctx();
+    if (!c) return VGPU_ERR_OOM;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) {
+        delete c;
+        return VGPU_ERR_HIP;
+    }
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return VGPU_ERR_HIP;
+    }
+    c->cur = c->own;
+    int rc = probe_host_rsqrt(c->lut, c->kbits, c->err);
+    if (rc != VGPU_OK) {
+        (void)hipStreamDestroy(c->own);
+        delete c;
+        return rc;
+    }
+    if (hipMalloc(&c->lut_dev, c->lut.size() * 4) != hipSuccess ||
+        hipMemcpy(c->lut_dev, c->lut.data(), c->lut.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipStreamDestroy(c->own);
+        delete c;
+        return VGPU_ERR_HIP;
+    }
+    *out = c;
+    return VGPU_OK;
+}
+
+extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
+{
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->own) (void)hipStreamSynchronize(c->own);
+    if (c->lut_dev) (void)hipFree(c->lut_dev);
+    if (c->stage) (void)hipFree(c->stage);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+extern "C" const char* vgpu_last_error(const vgpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+extern "C" int vgpu_ctx_set_stream(vgpu_ctx* c, void* s)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    c->cur = s ? (hipStream_t)s : c->own;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_sync(vgpu_ctx* c)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_rsqrt_table(const vgpu_ctx* c, int* kbits, const uint32_t** table)
+{
+    if (!c || !kbits || !table) return VGPU_ERR_INVALID_ARG;
+    *kbits = c->kbits;
+    *table = c->lut.data();
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_rsqrt_table_set(vgpu_ctx* c, const uint32_t* table, int kbits)
+{
+    if (!c || !table || kbits < 1 || kbits > 23) return fail(c, VGPU_ERR_INVALID_ARG, "bad rsqrt table");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    c->lut.assign(table, table + ((size_t)2 << kbits));
+    if (c->lut_dev) (void)hipFree(c->lut_dev);
+    c->lut_dev = nullptr;
+    HIPCHK(c, hipMalloc(&c->lut_dev, c->lut.size() * 4));
+    HIPCHK(c, hipMemcpy(c->lut_dev, c->lut.data(), c->lut.size() * 4, hipMemcpyHostToDevice));
+    c->kbits = kbits;
+    return VGPU_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// environment: shapes.hh / factory.hh restated on the host (float, no contraction)
+// ---------------------------------------------------------------------------------------
+static float clampf(float v, float lo, float hi) { return std::max(std::min(v, hi), lo); }  // math.hh:50-53
+
+static float sphere_min_distance(float x, float y, float z, float r)  // shapes.hh:238
+{
+    return std::sqrt(x * x + y * y + z * z) - r;
+}
+
+static float cuboid_min_distance(const float* c)  // shapes.hh:52-67
+{
+    const float x = c[0], y = c[1], z = c[2];
+    const float *a1 = c + 3, *a2 = c + 6, *a3 = c + 9;
+    const float d1 = -x * a1[0] + -y * a1[1] + -z * a1[2];
+    const float d2 = -x * a2[0] + -y * a2[1] + -z * a2[2];
+    const float d3 = -x * a3[0] + -y * a3[1] + -z * a3[2];
+    const float v1 = clampf(d1, -c[12], c[12]);
+    const float v2 = clampf(d2, -c[13], c[13]);
+    const float v3 = clampf(d3, -c[14], c[14]);
+    const float xn = x + a1[0] * v1 + a2[0] * v2 + a3[0] * v3;
+    const float yn = y + a1[1] * v1 + a2[1] * v2 + a3[1] * v3;
+    const float zn = z + a1[2] * v1 + a2[2] * v2 + a3[2] * v3;
+    return std::sqrt(xn * xn + yn * yn + zn * zn);
+}
+
+static float capsule_min_distance(const float* c)  // shapes.hh:165-189
+{
+    const float x1 = c[0], y1 = c[1], z1 = c[2], xv = c[3], yv = c[4], zv = c[5], r = c[6], rdv = c[7];
+    const float dot = clampf((-x1 * xv + -y1 * yv + -z1 * zv) * rdv, 0.f, 1.f);
+    const float xp = x1 + xv * dot, yp = y1 + yv * dot, zp = z1 + zv * dot;
+    float xo = -xp, yo = -yp, zo = -zp;
+    const float ol = std::sqrt(xo * xo + yo * yo + zo * zo);
+    xo = xo / ol;
+    yo = yo / ol;
+    zo = zo / ol;
+    const float ro = clampf(ol, 0.f, r);
+    const float xn = xp + ro * xo, yn = yp + ro * yo, zn = zp + ro * zo;
+    return std::sqrt(xn * xn + yn * yn + zn * zn);
+}
+
+// Eigen::AngleAxisf(phi, Z) * AngleAxisf(theta, Y) * AngleAxisf(rho, X) (factory.hh:37-39):
+// a product of AngleAxis is a quaternion; its rotation matrix columns are the cuboid axes.
+// The exact float op order of Eigen is not reproduced (parity of Euler->axes is unpinned;
+// fixtures pass resolved axes through vgpu_env_add_cuboid_axes).
+static void euler_xyz_matrix(const float e[3], float R[3][3])
+{
+    const float hr = e[0] * 0.5f, ht = e[1] * 0.5f, hp = e[2] * 0.5f;
+    const float cr = std::cos(hr), sr = std::sin(hr), ct = std::cos(ht), st = std::sin(ht), cp = std::cos(hp),
+                sp = std::sin(hp);
+    // q = qz(phi) * qy(theta) * qx(rho)
+    const float w = cp * ct * cr + sp * st * sr;
+    const float x = cp * ct * sr - sp * st * cr;
+    const float y = cp * st * cr + sp * ct * sr;
+    const float z = sp * ct * cr - cp * st * sr;
+    R[0][0] = 1 - 2 * (y * y + z * z);
+    R[0][1] = 2 * (x * y - w * z);
+    R[0][2] = 2 * (x * z + w * y);
+    R[1][0] = 2 * (x * y + w * z);
+    R[1][1] = 1 - 2 * (x * x + z * z);
+    R[1][2] = 2 * (y * z - w * x);
+    R[2][0] = 2 * (x * z - w * y);
+    R[2][1] = 2 * (y * z + w * x);
+    R[2][2] = 1 - 2 * (x * x + y * y);
+}
+
+extern "C" int vgpu_env_create(vgpu_ctx* c, vgpu_env** out)
+{
+    if (!c || !out) return VGPU_ERR_INVALID_ARG;
+    auto* e = new (std::nothrow) vgpu_env();
+    if (!e) return fail(c, VGPU_ERR_OOM, "out of host memory");
+    e->ctx = c;
+    *out = e;
+    return VGPU_OK;
+}
+
+extern "C" void vgpu_env_destroy(vgpu_env* e)
+{
+    if (!e) return;
+    if (e->dev) {
+        (void)hipSetDevice(e->ctx->device);
+        (void)hipStreamSynchronize(e->ctx->cur);
+        (void)hipFree(e->dev);
+    }
+    delete e;
+}
+
+static bool finite3(const float* v) { return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]); }
+
+extern "C" int vgpu_env_add_sphere(vgpu_env* e, const float c[3], float r)
+{
+    if (!e || !c || !finite3(c) || !std::isfinite(r)) return VGPU_ERR_INVALID_ARG;
+    e->spheres.push_back({c[0], c[1], c[2], r, sphere_min_distance(c[0], c[1], c[2], r)});
+    e->dirty = true;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_add_cuboid_axes(vgpu_env* e, const float c[3], const float a1[3], const float a2[3],
+                                        const float a3[3], const float h[3])
+{
+    if (!e || !c || !a1 || !a2 || !a3 || !h) return VGPU_ERR_INVALID_ARG;
+    std::array<float, 16> row{c[0],  c[1],  c[2],  a1[0], a1[1], a1[2], a2[0], a2[1],
+                              a2[2], a3[0], a3[1], a3[2], h[0],  h[1],  h[2],  0.0f};
+    row[15] = cuboid_min_distance(row.data());
+    if (row[11] == 1.0f)  // bindings/environment.cc:120 (axis_3_z == 1.)
+        e->zcuboids.push_back(row);
+    else
+        e->cuboids.push_back(row);
+    e->dirty = true;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_add_cuboid_euler(vgpu_env* e, const float c[3], const float euler[3], const float h[3])
+{
+    if (!e || !c || !euler || !h) return VGPU_ERR_INVALID_ARG;
+    float R[3][3];
+    euler_xyz_matrix(euler, R);
+    const float a1[3] = {R[0][0], R[1][0], R[2][0]};
+    const float a2[3] = {R[0][1], R[1][1], R[2][1]};
+    const float a3[3] = {R[0][2], R[1][2], R[2][2]};
+    return vgpu_env_add_cuboid_axes(e, c, a1, a2, a3, h);
+}
+
+extern "C" int vgpu_env_add_capsule_endpoints(vgpu_env* e, const float p1[3], const float p2[3], float r)
+{
+    if (!e || !p1 || !p2) return VGPU_ERR_INVALID_ARG;
+    const float xv = p2[0] - p1[0], yv = p2[1] - p1[1], zv = p2[2] - p1[2];  // factory.hh:113-116
+    const float dot = (xv * xv + yv * yv) + zv * zv;
+    if (!(dot > 0.0f)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "degenerate capsule");
+    std::array<float, 9> row{p1[0], p1[1], p1[2], xv, yv, zv, r, (float)(1.0 / (double)dot), 0.0f};
+    row[8] = capsule_min_distance(row.data());
+    if (xv == 0.0f && yv == 0.0f)  // bindings/environment.cc:134
+        e->zcapsules.push_back(row);
+    else
+        e->capsules.push_back(row);
+    e->dirty = true;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_add_capsule_euler(vgpu_env* e, const float c[3], const float euler[3], float r, float len)
+{
+    if (!e || !c || !euler) return VGPU_ERR_INVALID_ARG;
+    float R[3][3];
+    euler_xyz_matrix(euler, R);
+    const float h = len / 2;  // factory.hh:168-171: p = T * (0, 0, +-len/2)
+    const float p1[3] = {c[0] + R[0][2] * h, c[1] + R[1][2] * h, c[2] + R[2][2] * h};
+    const float p2[3] = {c[0] - R[0][2] * h, c[1] - R[1][2] * h, c[2] - R[2][2] * h};
+    return vgpu_env_add_capsule_endpoints(e, p1, p2, r);
+}
+
+extern "C" int vgpu_env_counts(const vgpu_env* e, int32_t counts[5])
+{
+    if (!e || !counts) return VGPU_ERR_INVALID_ARG;
+    counts[0] = (int32_t)e->spheres.size();
+    counts[1] = (int32_t)e->capsules.size();
+    counts[2] = (int32_t)e->zcapsules.size();
+    counts[3] = (int32_t)e->cuboids.size();
+    counts[4] = (int32_t)e->zcuboids.size();
+    return VGPU_OK;
+}
+
+template <size_t W>
+static void sort_md(std::vector<std::array<float, W>>& v)  // environment.hh:40-66
+{
+    std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a[W - 1] < b[W - 1]; });
+}
+
+extern "C" int vgpu_env_upload(vgpu_env* e)
+{
+    if (!e) return VGPU_ERR_INVALID_ARG;
+    vgpu_ctx* c = e->ctx;
+    if (!e->dirty && e->dev) return VGPU_OK;
+    sort_md(e->spheres);
+    sort_md(e->capsules);
+    sort_md(e->zcapsules);
+    sort_md(e->cuboids);
+    sort_md(e->zcuboids);
+    std::vector<float> blob;
+    auto put = [&](auto& v, int slot) {
+        e->off[slot] = blob.size();
+        for (auto& row : v) blob.insert(blob.end(), row.begin(), row.end());
+        while (blob.size() % 16) blob.push_back(0.0f);  // 64-B aligned sections
+    };
+    put(e->spheres, 0);
+    put(e->capsules, 1);
+    put(e->zcapsules, 2);
+    put(e->cuboids, 3);
+    put(e->zcuboids, 4);
+    if (blob.empty()) blob.assign(16, 0.0f);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (blob.size() > e->dev_floats) {
+        if (e->dev) {
+            HIPCHK(c, hipStreamSynchronize(c->cur));
+            HIPCHK(c, hipFree(e->dev));
+            e->dev = nullptr;
+        }
+        HIPCHK(c, hipMalloc(&e->dev, blob.size() * sizeof(float)));
+        e->dev_floats = blob.size();
+    }
+    HIPCHK(c, hipMemcpyAsync(e->dev, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));  // blob is a host temporary
+    e->dirty = false;
+    return VGPU_OK;
+}
+
+static EnvView make_view(const vgpu_env* e)
+{
+    EnvView v{};
+    auto p = [&](int s) { return (const VGPU_CONST float*)(e->dev + e->off[s]); };
+    v.spheres = p(0);
+    v.capsules = p(1);
+    v.zcapsules = p(2);
+    v.cuboids = p(3);
+    v.zcuboids = p(4);
+    v.n_spheres = (int)e->spheres.size();
+    v.n_capsules = (int)e->capsules.size();
+    v.n_zcapsules = (int)e->zcapsules.size();
+    v.n_cuboids = (int)e->cuboids.size();
+    v.n_zcuboids = (int)e->zcuboids.size();
+    v.lut = e->ctx->lut_dev;
+    v.kbits = e->ctx->kbits;
+    return v;
+}
+
+// ---------------------------------------------------------------------------------------
+// batch entry points
+// ---------------------------------------------------------------------------------------
+extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t* ns)
+{
+    if (kind != VGPU_ROBOT_PANDA) return VGPU_ERR_UNSUPPORTED;
+    if (dim) *dim = kPandaDim;
+    if (res) *res = kPandaResolution;
+    if (ns) *ns = kPandaSpheres;
+    return VGPU_OK;
+}
+
+static int check_robot(vgpu_ctx* c, const vgpu_robot* r, float base[3])
+{
+    if (!r) return fail(c, VGPU_ERR_INVALID_ARG, "null robot");
+    if (r->kind != VGPU_ROBOT_PANDA) return fail(c, VGPU_ERR_UNSUPPORTED, "unsupported robot kind");
+    // robots/panda/fk.hh:109-111: static_cast<float>(base_x100) / 100.0f
+    base[0] = (float)r->base_x100 / 100.0f;
+    base[1] = (float)r->base_y100 / 100.0f;
+    base[2] = (float)r->base_z100 / 100.0f;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_sphere_fk(vgpu_ctx* c, const vgpu_robot* r, const float* q, size_t n, float* xyz, size_t ld)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    float b[3];
+    int rc = check_robot(c, r, b);
+    if (rc) return rc;
+    if (n && (!q || !xyz || ld < n)) return fail(c, VGPU_ERR_INVALID_ARG, "bad sphere_fk arguments");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_panda_sphere_fk(q, n, b[0], b[1], b[2], xyz, ld, c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n, uint8_t* valid)
+{
+    if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
+    float b[3];
+    int rc = check_robot(c, r, b);
+    if (rc) return rc;
+    if (n && (!q || !valid)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if ((rc = vgpu_env_upload(e))) return rc;
+    const EnvView v = make_view(e);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_panda_fkcc(q, n, &v, b[0], b[1], b[2], valid, c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* starts,
+                                     const float* goals, size_t n_edges, uint8_t* ok, int32_t* n_blocks)
+{
+    if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
+    float b[3];
+    int rc = check_robot(c, r, b);
+    if (rc) return rc;
+    if (n_edges && (!starts || !goals || !ok)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if (n_edges > ((size_t)1 << 40)) return fail(c, VGPU_ERR_INVALID_ARG, "too many edges");
+    if ((rc = vgpu_env_upload(e))) return rc;
+    const EnvView v = make_view(e);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_panda_validate(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, c->cur));
+    return VGPU_OK;
+}
+
+// ---- host conveniences ------------------------------------------------------------------
+static int stage(vgpu_ctx* c, size_t bytes, char** p)
+{
+    if (bytes > c->stage_bytes) {
+        if (c->stage) {
+            HIPCHK(c, hipStreamSynchronize(c->cur));
+            HIPCHK(c, hipFree(c->stage));
+            c->stage = nullptr;
+        }
+        HIPCHK(c, hipMalloc(&c->stage, bytes));
+        c->stage_bytes = bytes;
+    }
+    *p = (char*)c->stage;
+    return VGPU_OK;
+}
+
+static size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
+
+extern "C" int vgpu_sphere_fk_host(vgpu_ctx* c, const vgpu_robot* r, const float* q, size_t n, float* xyz)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (n == 0) return VGPU_OK;
+    char* d;
+    const size_t qb = al(n * kPandaDim * 4), ob = (size_t)3 * kPandaSpheres * n * 4;
+    int rc = stage(c, qb + ob, &d);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(d, q, n * kPandaDim * 4, hipMemcpyHostToDevice, c->cur));
+    if ((rc = vgpu_sphere_fk(c, r, (const float*)d, n, (float*)(d + qb), n))) return rc;
+    HIPCHK(c, hipMemcpyAsync(xyz, d + qb, ob, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n,
+                              uint8_t* valid)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (n == 0) return VGPU_OK;
+    char* d;
+    const size_t qb = al(n * kPandaDim * 4);
+    int rc = stage(c, qb + n, &d);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(d, q, n * kPandaDim * 4, hipMemcpyHostToDevice, c->cur));
+    if ((rc = vgpu_fkcc(c, r, e, (const float*)d, n, (uint8_t*)(d + qb)))) return rc;
+    HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_validate_motions_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* starts,
+                                          const float* goals, size_t n, uint8_t* ok, int32_t* n_blocks)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (n == 0) return VGPU_OK;
+    char* d;
+    const size_t qb = al(n * kPandaDim * 4);
+    const size_t okb = al(n), nbb = al(n * 4);
+    int rc = stage(c, 2 * qb + okb + nbb, &d);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(d, starts, n * kPandaDim * 4, hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipMemcpyAsync(d + qb, goals, n * kPandaDim * 4, hipMemcpyHostToDevice, c->cur));
+    uint8_t* okd = (uint8_t*)(d + 2 * qb);
+    int32_t* nbd = (int32_t*)(d + 2 * qb + okb);
+    if ((rc = vgpu_validate_motions(c, r, e, (const float*)d, (const float*)(d + qb), n, okd, nbd))) return rc;
+    HIPCHK(c, hipMemcpyAsync(ok, okd, n, hipMemcpyDeviceToHost, c->cur));
+    if (n_blocks) HIPCHK(c, hipMemcpyAsync(n_blocks, nbd, n * 4, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}

@@ -1,0 +1,348 @@
+"""vamp_amd -- MI355X (gfx950) implementation of VAMP's motion-validation rake.
+
+Host-side mirror of the reference's Python surface for this path
+(``vamp.Environment``/``Sphere``/``Cuboid``/``Cylinder`` and ``vamp.<robot>.fk``/``validate``;
+reference src/impl/vamp/bindings/environment.cc:18-146 and bindings/common.hh:132-182,586-725),
+plus the batch entry points the GPU path exists for.  Every call goes through the C ABI
+(include/vamp_gpu.h) into libvampgpu.so; nothing here computes collision results on the CPU.
+
+    import vamp_amd as vamp
+    env = vamp.Environment()
+    env.add_sphere(vamp.Sphere([0.5, 0.0, 0.3], 0.2))
+    vamp.panda.validate(q, env)                      # one configuration (bindings/common.hh:172-190)
+    ok, n = vamp.panda_0_0.validate_batch(starts, goals, env)   # N edges, validate_motion each
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import VgpuError, check, load
+
+__all__ = [
+    "Context", "context", "Environment", "Sphere", "Cuboid", "Cylinder", "Robot", "PandaBase", "panda",
+    "panda_0_0", "VgpuError",
+]
+
+
+def _f3(v) -> C.Array:
+    a = (C.c_float * 3)(*[float(np.float32(x)) for x in v])
+    return a
+
+
+class Context:
+    """One HIP device + stream (vgpu_ctx).  Probes the host rsqrt approximation on creation."""
+
+    def __init__(self, device: int = 0):
+        lib = load()
+        h = C.c_void_p()
+        rc = lib.vgpu_ctx_create(int(device), C.byref(h))
+        if rc != 0:
+            raise VgpuError(f"vgpu_ctx_create(device={device}) failed: {_lib.ERRORS.get(rc, rc)}")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().vgpu_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(load().vgpu_sync(self.h), self.h)
+
+    def set_stream(self, stream_handle: Optional[int]):
+        check(load().vgpu_ctx_set_stream(self.h, C.c_void_p(stream_handle or 0)), self.h)
+
+    def rsqrt_table(self) -> Tuple[np.ndarray, int]:
+        k = C.c_int()
+        p = _lib.U32P()
+        check(load().vgpu_rsqrt_table(self.h, C.byref(k), C.byref(p)), self.h)
+        n = 2 << k.value
+        return np.ctypeslib.as_array(p, shape=(n,)).copy(), k.value
+
+    def set_rsqrt_table(self, table: np.ndarray, kbits: int):
+        t = np.ascontiguousarray(table, np.uint32)
+        check(load().vgpu_rsqrt_table_set(self.h, t.ctypes.data_as(_lib.U32P), int(kbits)), self.h)
+
+
+_contexts: Dict[int, Context] = {}
+
+
+def context(device: int = 0) -> Context:
+    if device not in _contexts:
+        _contexts[device] = Context(device)
+    return _contexts[device]
+
+
+# ---- shapes (collision/shapes.hh, factory.hh) ---------------------------------------------
+class Sphere:
+    """vamp.Sphere(center, radius) (bindings/environment.cc:20-25)."""
+
+    def __init__(self, center: Sequence[float], radius: float):
+        self.center = [float(c) for c in center]
+        self.r = float(radius)
+        self.name = ""
+
+    @property
+    def x(self):
+        return self.center[0]
+
+    @property
+    def y(self):
+        return self.center[1]
+
+    @property
+    def z(self):
+        return self.center[2]
+
+    @property
+    def position(self):
+        return list(self.center)
+
+    def __repr__(self):
+        return f"Sphere({self.center}, {self.r})"
+
+
+class Cuboid:
+    """vamp.Cuboid(center, euler_xyz, half_extents) (bindings/environment.cc:70-76); use
+    Cuboid.from_axes for resolved axes (the Euler->axes step of factory.hh:26-60 goes through
+    Eigen in the reference and is restated here without bit-parity)."""
+
+    def __init__(self, center, euler_xyz=None, half_extents=None, axes=None):
+        self.center = [float(c) for c in center]
+        self.euler = None if euler_xyz is None else [float(e) for e in euler_xyz]
+        self.half = [float(h) for h in half_extents]
+        self.axes = axes
+        self.name = ""
+
+    @classmethod
+    def from_axes(cls, center, axis_1, axis_2, axis_3, half_extents):
+        return cls(center, None, half_extents, axes=[list(axis_1), list(axis_2), list(axis_3)])
+
+
+class Cylinder:
+    """vamp.Cylinder(center, euler_xyz, radius, length) or vamp.Cylinder(endpoint1, endpoint2,
+    radius) (bindings/environment.cc:37-52); added to environments as capsules."""
+
+    def __init__(self, a, b, radius, length=None):
+        if length is None:
+            self.p1, self.p2, self.r = [float(v) for v in a], [float(v) for v in b], float(radius)
+            self.center = None
+        else:
+            self.center, self.euler, self.r, self.length = ([float(v) for v in a], [float(v) for v in b],
+                                                            float(radius), float(length))
+        self.name = ""
+
+
+class Environment:
+    """collision::Environment<float> (environment.hh:12-82) realised lazily per Context."""
+
+    def __init__(self):
+        self._ops: List[Tuple[str, object]] = []
+        self._handles: Dict[int, C.c_void_p] = {}
+
+    def _changed(self):
+        for dev, h in list(self._handles.items()):
+            load().vgpu_env_destroy(h)
+        self._handles.clear()
+
+    def add_sphere(self, s: Sphere):
+        self._ops.append(("sphere", s))
+        self._changed()
+
+    def add_cuboid(self, c: Cuboid):
+        self._ops.append(("cuboid", c))
+        self._changed()
+
+    def add_capsule(self, c: Cylinder):
+        self._ops.append(("capsule", c))
+        self._changed()
+
+    def handle(self, ctx: Context) -> C.c_void_p:
+        if ctx.device in self._handles:
+            return self._handles[ctx.device]
+        lib = load()
+        h = C.c_void_p()
+        check(lib.vgpu_env_create(ctx.h, C.byref(h)), ctx.h)
+        for kind, s in self._ops:
+            if kind == "sphere":
+                rc = lib.vgpu_env_add_sphere(h, _f3(s.center), float(np.float32(s.r)))
+            elif kind == "cuboid":
+                if s.axes is not None:
+                    rc = lib.vgpu_env_add_cuboid_axes(h, _f3(s.center), _f3(s.axes[0]), _f3(s.axes[1]),
+                                                      _f3(s.axes[2]), _f3(s.half))
+                else:
+                    rc = lib.vgpu_env_add_cuboid_euler(h, _f3(s.center), _f3(s.euler), _f3(s.half))
+            else:
+                if s.center is None:
+                    rc = lib.vgpu_env_add_capsule_endpoints(h, _f3(s.p1), _f3(s.p2), float(np.float32(s.r)))
+                else:
+                    rc = lib.vgpu_env_add_capsule_euler(h, _f3(s.center), _f3(s.euler), float(np.float32(s.r)),
+                                                        float(np.float32(s.length)))
+            check(rc, ctx.h)
+        check(lib.vgpu_env_upload(h), ctx.h)
+        self._handles[ctx.device] = h
+        return h
+
+    def counts(self, ctx: Optional[Context] = None) -> List[int]:
+        ctx = ctx or context()
+        out = (C.c_int32 * 5)()
+        check(load().vgpu_env_counts(self.handle(ctx), out), ctx.h)
+        return list(out)
+
+    def __del__(self):
+        try:
+            self._changed()
+        except Exception:
+            pass
+
+
+# ---- robots -----------------------------------------------------------------------------------
+class Robot:
+    """Python face of vamp::robots::PandaBase<X100, Y100, Z100> (robots/panda_base.hh:15-75)."""
+
+    S_M = np.array([5.9342, 3.6652, 5.9342, 3.2289, 5.9342, 3.9095999999999997, 5.9342], np.float32)
+    S_A = np.array([-2.9671, -1.8326, -2.9671, -3.1416, -2.9671, -0.0873, -2.9671], np.float32)
+    D_M = np.array([0.1685147113342995, 0.2728364072901888, 0.1685147113342995, 0.30970299482796,
+                    0.1685147113342995, 0.25578064252097404, 0.1685147113342995], np.float32)
+
+    def __init__(self, name: str, base_x100: int, base_y100: int, base_z100: int, kind: int = _lib.VGPU_ROBOT_PANDA):
+        self.name = name
+        self.c_robot = _lib.VgpuRobot(kind, base_x100, base_y100, base_z100)
+        dim, res, ns = C.c_int32(), C.c_int32(), C.c_int32()
+        self._info = None
+        self.kind = kind
+
+    def _meta(self):
+        if self._info is None:
+            dim, res, ns = C.c_int32(), C.c_int32(), C.c_int32()
+            check(load().vgpu_robot_info(self.kind, C.byref(dim), C.byref(res), C.byref(ns)))
+            self._info = (dim.value, res.value, ns.value)
+        return self._info
+
+    def dimension(self) -> int:
+        return self._meta()[0]
+
+    def resolution(self) -> int:
+        return self._meta()[1]
+
+    def n_spheres(self) -> int:
+        return self._meta()[2]
+
+    @property
+    def base(self):
+        r = self.c_robot
+        return (np.float32(r.base_x100) / np.float32(100), np.float32(r.base_y100) / np.float32(100),
+                np.float32(r.base_z100) / np.float32(100))
+
+    # --- scaling (robots/panda/fk.hh:34-62) ---
+    def scale_configuration(self, u):
+        u = np.asarray(u, np.float32)
+        return (u.astype(np.float64) * self.S_M + self.S_A).astype(np.float32)
+
+    def descale_configuration(self, q):
+        q = np.asarray(q, np.float32)
+        return ((q - self.S_A) * self.D_M).astype(np.float32)
+
+    # --- reference-named single calls ---
+    def fk(self, configuration, ctx: Optional[Context] = None) -> List[Sphere]:
+        """vamp.<robot>.fk(q) (bindings/common.hh:132-152): the collision spheres."""
+        xyz = self.sphere_fk_batch(np.asarray(configuration, np.float32)[None, :], ctx)[0]
+        radii = _PANDA_RADII
+        return [Sphere(xyz[s], float(radii[s])) for s in range(xyz.shape[0])]
+
+    def validate(self, configuration, environment: Environment, ctx: Optional[Context] = None) -> bool:
+        """vamp.<robot>.validate(q, env) (bindings/common.hh:172-190): bounds check in the
+        descaled unit box, then validate_motion(q, q) == fkcc of the broadcast block."""
+        q = np.asarray(configuration, np.float32)
+        d = self.descale_configuration(q)
+        if not ((d <= 1.0).all() and (d >= 0.0).all()):
+            return False
+        return bool(self.fkcc_batch(q[None, :], environment, ctx)[0])
+
+    def validate_motion(self, start, goal, environment: Environment, ctx: Optional[Context] = None) -> bool:
+        """planning::validate_motion<Robot, 8, resolution> (planning/validate.hh:67-75)."""
+        ok, _ = self.validate_batch(np.asarray(start, np.float32)[None], np.asarray(goal, np.float32)[None],
+                                    environment, ctx)
+        return bool(ok[0])
+
+    # --- batches (host numpy in/out) ---
+    def sphere_fk_batch(self, q, ctx: Optional[Context] = None) -> np.ndarray:
+        ctx = ctx or context()
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, self.dimension())
+        n = q.shape[0]
+        ns = self.n_spheres()
+        out = np.empty((3, ns, n), np.float32)
+        check(load().vgpu_sphere_fk_host(ctx.h, C.byref(self.c_robot), q.ctypes.data_as(_lib.F32P), n,
+                                         out.ctypes.data_as(_lib.F32P)), ctx.h)
+        return np.ascontiguousarray(out.transpose(2, 1, 0))
+
+    def fkcc_batch(self, q, environment: Environment, ctx: Optional[Context] = None) -> np.ndarray:
+        ctx = ctx or context()
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, self.dimension())
+        out = np.empty(q.shape[0], np.uint8)
+        check(load().vgpu_fkcc_host(ctx.h, C.byref(self.c_robot), environment.handle(ctx),
+                                    q.ctypes.data_as(_lib.F32P), q.shape[0], out.ctypes.data_as(_lib.U8P)), ctx.h)
+        return out.astype(bool)
+
+    def validate_batch(self, starts, goals, environment: Environment, ctx: Optional[Context] = None):
+        ctx = ctx or context()
+        s = np.ascontiguousarray(starts, np.float32).reshape(-1, self.dimension())
+        g = np.ascontiguousarray(goals, np.float32).reshape(-1, self.dimension())
+        if s.shape != g.shape:
+            raise ValueError("starts and goals differ in shape")
+        ok = np.empty(s.shape[0], np.uint8)
+        nb = np.empty(s.shape[0], np.int32)
+        check(load().vgpu_validate_motions_host(ctx.h, C.byref(self.c_robot), environment.handle(ctx),
+                                                s.ctypes.data_as(_lib.F32P), g.ctypes.data_as(_lib.F32P),
+                                                s.shape[0], ok.ctypes.data_as(_lib.U8P),
+                                                nb.ctypes.data_as(_lib.I32P)), ctx.h)
+        return ok.astype(bool), nb
+
+    # --- batches on device memory (raw pointers, e.g. torch tensor.data_ptr()) ---
+    def sphere_fk_device(self, q_ptr: int, n: int, out_ptr: int, ld: int, ctx: Optional[Context] = None):
+        ctx = ctx or context()
+        check(load().vgpu_sphere_fk(ctx.h, C.byref(self.c_robot), C.c_void_p(q_ptr), n, C.c_void_p(out_ptr), ld),
+              ctx.h)
+
+    def fkcc_device(self, q_ptr: int, n: int, environment: Environment, valid_ptr: int,
+                    ctx: Optional[Context] = None):
+        ctx = ctx or context()
+        check(load().vgpu_fkcc(ctx.h, C.byref(self.c_robot), environment.handle(ctx), C.c_void_p(q_ptr), n,
+                               C.c_void_p(valid_ptr)), ctx.h)
+
+    def validate_device(self, starts_ptr: int, goals_ptr: int, n: int, environment: Environment, ok_ptr: int,
+                        nblocks_ptr: int = 0, ctx: Optional[Context] = None):
+        ctx = ctx or context()
+        check(load().vgpu_validate_motions(ctx.h, C.byref(self.c_robot), environment.handle(ctx),
+                                           C.c_void_p(starts_ptr), C.c_void_p(goals_ptr), n, C.c_void_p(ok_ptr),
+                                           C.c_void_p(nblocks_ptr or 0)), ctx.h)
+
+
+# robots/panda/fk.hh:113-171 sphere radii (reference order)
+_PANDA_RADII = np.array(
+    [0.08] + [0.06] * 9 + [0.05, 0.055, 0.055, 0.06, 0.055, 0.055, 0.055, 0.06, 0.06, 0.06, 0.05] + [0.025] * 8 +
+    [0.05, 0.05, 0.052, 0.05, 0.025, 0.025, 0.02, 0.02] + [0.028] * 6 + [0.026] * 6 + [0.024] * 6 + [0.012] * 4,
+    np.float32)
+
+
+def PandaBase(base_x100: int, base_y100: int, base_z100: int, name: Optional[str] = None) -> Robot:
+    """vamp::robots::PandaBase<X100, Y100, Z100> (robots/panda_base.hh:15)."""
+    return Robot(name or f"panda_{base_x100}_{base_y100}_{base_z100}", base_x100, base_y100, base_z100)
+
+
+# robots/panda_grid.hh:10-41 -- including this fork's default Panda at base (2, 2, 0)
+panda = PandaBase(200, 200, 0, "panda")
+for _i in range(3):
+    for _j in range(3):
+        globals()[f"panda_{_i}_{_j}"] = PandaBase(100 * _i, 100 * _j, 0, f"panda_{_i}_{_j}")
+        __all__.append(f"panda_{_i}_{_j}")

@@ -1,0 +1,87 @@
+"""ctypes binding of the C ABI (include/vamp_gpu.h) in ``libvampgpu.so``.
+
+The library is built in-tree by ``make -C mr-vamp_amd`` (or ``__graft_entry__.build()``).
+There is deliberately no fallback: if the library is missing or no HIP device is present
+every entry point raises, so a GPU test can never pass on a silent CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvampgpu.so")
+
+VGPU_OK = 0
+VGPU_ROBOT_PANDA = 1
+ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of memory", -4: "unsupported", -5: "host rsqrt probe"}
+
+F32P = C.POINTER(C.c_float)
+U8P = C.POINTER(C.c_uint8)
+I32P = C.POINTER(C.c_int32)
+U32P = C.POINTER(C.c_uint32)
+VP = C.c_void_p
+
+
+class VgpuRobot(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("base_x100", C.c_int32), ("base_y100", C.c_int32), ("base_z100", C.c_int32)]
+
+
+# every exported symbol of include/vamp_gpu.h with its signature (restype, argtypes)
+SIGNATURES = {
+    "vgpu_ctx_create": (C.c_int, [C.c_int, C.POINTER(VP)]),
+    "vgpu_ctx_destroy": (None, [VP]),
+    "vgpu_last_error": (C.c_char_p, [VP]),
+    "vgpu_ctx_set_stream": (C.c_int, [VP, VP]),
+    "vgpu_sync": (C.c_int, [VP]),
+    "vgpu_rsqrt_table": (C.c_int, [VP, C.POINTER(C.c_int), C.POINTER(U32P)]),
+    "vgpu_rsqrt_table_set": (C.c_int, [VP, U32P, C.c_int]),
+    "vgpu_env_create": (C.c_int, [VP, C.POINTER(VP)]),
+    "vgpu_env_destroy": (None, [VP]),
+    "vgpu_env_add_sphere": (C.c_int, [VP, F32P, C.c_float]),
+    "vgpu_env_add_cuboid_axes": (C.c_int, [VP, F32P, F32P, F32P, F32P, F32P]),
+    "vgpu_env_add_cuboid_euler": (C.c_int, [VP, F32P, F32P, F32P]),
+    "vgpu_env_add_capsule_endpoints": (C.c_int, [VP, F32P, F32P, C.c_float]),
+    "vgpu_env_add_capsule_euler": (C.c_int, [VP, F32P, F32P, C.c_float, C.c_float]),
+    "vgpu_env_counts": (C.c_int, [VP, I32P]),
+    "vgpu_env_upload": (C.c_int, [VP]),
+    "vgpu_sphere_fk": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, C.c_size_t, VP, C.c_size_t]),
+    "vgpu_fkcc": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, C.c_size_t, VP]),
+    "vgpu_validate_motions": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, VP, C.c_size_t, VP, VP]),
+    "vgpu_sphere_fk_host": (C.c_int, [VP, C.POINTER(VgpuRobot), F32P, C.c_size_t, F32P]),
+    "vgpu_fkcc_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P]),
+    "vgpu_validate_motions_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P]),
+    "vgpu_robot_info": (C.c_int, [C.c_int32, I32P, I32P, I32P]),
+}
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libvampgpu.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C mr-vamp_amd` "
+                           "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+class VgpuError(RuntimeError):
+    pass
+
+
+def check(rc: int, ctx=None):
+    if rc != VGPU_OK:
+        msg = ""
+        if ctx is not None:
+            m = load().vgpu_last_error(ctx)
+            msg = m.decode() if m else ""
+        raise VgpuError(f"vamp_gpu: {ERRORS.get(rc, rc)}: {msg}")

@@ -1,0 +1,87 @@
+/* vamp_oracle.h -- CPU restatement of the reference motion-validation rake.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / the timed CPU
+ * baseline.  The product (mr-vamp_amd/, libvampgpu.so) never links or calls it.
+ *
+ * Parity pin (see DESIGN.md "Oracle and parity"):
+ *   - sin/cos, max_extent sqrt, l2_norm, rake construction, Halton: bit-exact against
+ *     oracle/_ref/ref_probe built from the reference's own vector layer + halton.hh;
+ *   - FK sphere centres and fkcc masks: against fixtures produced by evaluating the
+ *     reference's generated fk.hh expression DAG (tools/fkhh_interp.py), FK within 1e-5,
+ *     masks bit-exact on the margin-filtered set.  The reference fk.hh/validity.hh cannot
+ *     be compiled here (Eigen/pdqsort absent), so that pin is "partial" by construction.
+ */
+#ifndef VAMP_ORACLE_H
+#define VAMP_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Environment<float> (collision/environment.hh:12-82), each list sorted ascending by
+ * min_distance.  Row layouts (float32):
+ *   sphere  [5]  x y z r min_distance
+ *   capsule [9]  x1 y1 z1 xv yv zv r rdv min_distance   (also z-aligned capsules)
+ *   cuboid  [16] x y z a1x a1y a1z a2x a2y a2z a3x a3y a3z r1 r2 r3 min_distance */
+typedef struct vo_env {
+    int n_spheres, n_capsules, n_zcapsules, n_cuboids, n_zcuboids;
+    const float *spheres, *capsules, *zcapsules, *cuboids, *zcuboids;
+} vo_env;
+
+typedef struct vo_stats {
+    double test_margin;   /* min |signed test value| over evaluated primitive tests */
+    double cull_margin;   /* min |min_distance - max_extent| over evaluated cull tests */
+    double flops;         /* executed floating-point operations (fma = 2) */
+} vo_stats;
+
+/* ---- vector-layer semantics (vector/interface.hh, vector/avx.hh) ---- */
+float vo_sin(float x);                     /* interface.hh:438-456 as compiled (Horner/FMA) */
+float vo_cos(float x);                     /* interface.hh:458-469 */
+float vo_rsqrt_native(float x);            /* _mm_rsqrt_ss of this host (avx.hh:411-415) */
+float vo_max_extent(float x, float y, float z, float r); /* validity.hh:55-59 */
+float vo_l2_norm7(const float v[7]);       /* interface.hh:402-410 + avx.hh:441-452 */
+
+/* Probe this host's rsqrt approximation as a table indexed by (exponent parity, top K
+ * mantissa bits).  lut must hold 2 << 16 entries.  Returns 0 and sets *kbits on success,
+ * <0 if the host's rsqrt is not such a table function (then the GPU path refuses to run). */
+int vo_rsqrt_probe(uint32_t *lut, int *kbits);
+/* sqrt emulated from a probed table (the GPU kernels' algorithm, for testing) */
+float vo_sqrt_lut(float v, const uint32_t *lut, int kbits);
+
+/* ---- shapes (collision/shapes.hh) ---- */
+float vo_sphere_min_distance(float x, float y, float z, float r);              /* shapes.hh:238 */
+float vo_cuboid_min_distance(const float c[15]);                               /* shapes.hh:52-67 */
+float vo_capsule_min_distance(const float c[8]);                               /* shapes.hh:165-189 */
+
+/* ---- Panda (robots/panda_base.hh, robots/panda/fk.hh) ---- */
+void vo_panda_scale(float q[7]);                                               /* fk.hh:34-37 */
+void vo_panda_sphere_fk(const float q[7], int bx100, int by100, int bz100,
+                        float out_xyz[][3]);                                    /* fk.hh:104-1333 */
+/* fkcc on one block of G lanes (G = 8: a reference rake block; G = 1: a configuration
+ * broadcast to all lanes, i.e. the per-configuration mask).  q is [G][7].
+ * Returns 1 = valid (fk.hh:1335-6276 via robots/panda_base.hh:53-58). */
+int vo_panda_fkcc_block(const vo_env *env, const float *q, int G, int bx100, int by100, int bz100,
+                        vo_stats *stats);
+/* validate_motion<Panda, 8, 32> (planning/validate.hh:23-75). *n_out = back-step count n. */
+int vo_panda_validate_motion(const vo_env *env, const float start[7], const float goal[7],
+                             int bx100, int by100, int bz100, int *n_out, vo_stats *stats);
+
+/* batched, multi-threaded drivers (CPU baseline / fixture generation) */
+void vo_panda_fkcc_configs(const vo_env *env, const float *q /*[N][7]*/, size_t n, int bx100,
+                           int by100, int bz100, uint8_t *valid, int threads);
+void vo_panda_validate_motions(const vo_env *env, const float *starts, const float *goals,
+                               size_t n_edges, int bx100, int by100, int bz100, uint8_t *ok,
+                               int32_t *n_out, int threads);
+
+/* ---- Halton (random/halton.hh:73-104), closed form ---- */
+/* Sample with 1-based draw index k (k-th call to next()) of Halton<dim>, dim <= 16. */
+void vo_halton(int dim, uint64_t k, float *out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,221 @@
+"""ctypes view of the C restatement (oracle/_build/libvamp_oracle.so).
+
+TEST INFRASTRUCTURE: imported only by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, as the checker.  Never part of the product path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "_build", "libvamp_oracle.so")
+
+F32P = C.POINTER(C.c_float)
+U8P = C.POINTER(C.c_uint8)
+I32P = C.POINTER(C.c_int32)
+U32P = C.POINTER(C.c_uint32)
+
+
+class VoEnv(C.Structure):
+    _fields_ = [
+        ("n_spheres", C.c_int), ("n_capsules", C.c_int), ("n_zcapsules", C.c_int), ("n_cuboids", C.c_int),
+        ("n_zcuboids", C.c_int),
+        ("spheres", F32P), ("capsules", F32P), ("zcapsules", F32P), ("cuboids", F32P), ("zcuboids", F32P),
+    ]
+
+
+class VoStats(C.Structure):
+    _fields_ = [("test_margin", C.c_double), ("cull_margin", C.c_double), ("flops", C.c_double)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = C.CDLL(LIB)
+        L.vo_sin.restype = C.c_float
+        L.vo_sin.argtypes = [C.c_float]
+        L.vo_cos.restype = C.c_float
+        L.vo_cos.argtypes = [C.c_float]
+        L.vo_max_extent.restype = C.c_float
+        L.vo_max_extent.argtypes = [C.c_float] * 4
+        L.vo_l2_norm7.restype = C.c_float
+        L.vo_l2_norm7.argtypes = [F32P]
+        L.vo_rsqrt_probe.restype = C.c_int
+        L.vo_rsqrt_probe.argtypes = [U32P, C.POINTER(C.c_int)]
+        L.vo_sqrt_lut.restype = C.c_float
+        L.vo_sqrt_lut.argtypes = [C.c_float, U32P, C.c_int]
+        L.vo_rsqrt_native.restype = C.c_float
+        L.vo_rsqrt_native.argtypes = [C.c_float]
+        L.vo_sphere_min_distance.restype = C.c_float
+        L.vo_sphere_min_distance.argtypes = [C.c_float] * 4
+        L.vo_cuboid_min_distance.restype = C.c_float
+        L.vo_cuboid_min_distance.argtypes = [F32P]
+        L.vo_capsule_min_distance.restype = C.c_float
+        L.vo_capsule_min_distance.argtypes = [F32P]
+        L.vo_panda_sphere_fk.argtypes = [F32P, C.c_int, C.c_int, C.c_int, F32P]
+        L.vo_panda_fkcc_block.restype = C.c_int
+        L.vo_panda_fkcc_block.argtypes = [C.POINTER(VoEnv), F32P, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.POINTER(VoStats)]
+        L.vo_panda_validate_motion.restype = C.c_int
+        L.vo_panda_validate_motion.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_int, C.c_int, C.c_int,
+                                               C.POINTER(C.c_int), C.POINTER(VoStats)]
+        L.vo_panda_fkcc_configs.argtypes = [C.POINTER(VoEnv), F32P, C.c_size_t, C.c_int, C.c_int, C.c_int, U8P,
+                                            C.c_int]
+        L.vo_panda_validate_motions.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_size_t, C.c_int, C.c_int,
+                                                C.c_int, U8P, I32P, C.c_int]
+        L.vo_halton.argtypes = [C.c_int, C.c_uint64, F32P]
+        L.vo_panda_scale.argtypes = [F32P]
+        _lib = L
+    return _lib
+
+
+def fp(a):
+    return a.ctypes.data_as(F32P)
+
+
+class Env:
+    """Host environment in the oracle's layout, built like the reference's
+    Environment::add_* (bindings/environment.cc:107-146): min_distance from the shape
+    constructors, cuboids with axis_3_z == 1 and capsules with xv == yv == 0 routed to the
+    z-aligned lists, every list sorted by min_distance (environment.hh:40-66)."""
+
+    def __init__(self):
+        self.spheres, self.capsules, self.zcapsules, self.cuboids, self.zcuboids = [], [], [], [], []
+
+    def add_sphere(self, center, r):
+        x, y, z = (float(np.float32(v)) for v in center)
+        md = lib().vo_sphere_min_distance(x, y, z, float(np.float32(r)))
+        self.spheres.append([x, y, z, r, md])
+        return self
+
+    def add_cuboid_axes(self, center, a1, a2, a3, half):
+        c = np.array(list(center) + list(a1) + list(a2) + list(a3) + list(half), np.float32)
+        md = lib().vo_cuboid_min_distance(fp(c))
+        row = list(c) + [md]
+        (self.zcuboids if c[11] == 1.0 else self.cuboids).append(row)
+        return self
+
+    def add_capsule_endpoints(self, p1, p2, r):
+        p1 = np.array(p1, np.float32)
+        p2 = np.array(p2, np.float32)
+        v = (p2 - p1).astype(np.float32)
+        dot = np.float32((v[0] * v[0] + v[1] * v[1]) + v[2] * v[2])
+        rdv = np.float32(1.0 / float(dot))  # factory.hh:120-121 (double reciprocal, cast)
+        c = np.array(list(p1) + list(v) + [r, rdv], np.float32)
+        md = lib().vo_capsule_min_distance(fp(c))
+        row = list(c) + [md]
+        (self.zcapsules if (v[0] == 0 and v[1] == 0) else self.capsules).append(row)
+        return self
+
+    def arrays(self):
+        out = {}
+        for name, width in (("spheres", 5), ("capsules", 9), ("zcapsules", 9), ("cuboids", 16), ("zcuboids", 16)):
+            rows = getattr(self, name)
+            a = np.array(rows, np.float32).reshape(-1, width)
+            if len(a):
+                a = a[np.argsort(a[:, -1], kind="stable")]
+            out[name] = np.ascontiguousarray(a)
+        return out
+
+    def c(self):
+        arrs = self.arrays()
+        self._keep = arrs
+        e = VoEnv()
+        for name in arrs:
+            setattr(e, "n_" + name, len(arrs[name]))
+            setattr(e, name, fp(arrs[name]) if len(arrs[name]) else None)
+        return e
+
+
+def sphere_cage_env():
+    """The 14-sphere cage of scripts/cpp/benchmark_collision_checks.cc:33-51 (r = 0.2)."""
+    centers = [(0.55, 0, 0.25), (0.35, 0.35, 0.25), (0, 0.55, 0.25), (-0.55, 0, 0.25), (-0.35, -0.35, 0.25),
+               (0, -0.55, 0.25), (0.35, -0.35, 0.25), (0.35, 0.35, 0.8), (0, 0.55, 0.8), (-0.35, 0.35, 0.8),
+               (-0.55, 0, 0.8), (-0.35, -0.35, 0.8), (0, -0.55, 0.8), (0.35, -0.35, 0.8)]
+    e = Env()
+    for c in centers:
+        e.add_sphere(c, np.float32(0.2))
+    return e
+
+
+def sphere_fk(q, base100=(0, 0, 0)):
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, 7)
+    out = np.zeros((q.shape[0], 59, 3), np.float32)
+    L = lib()
+    for i in range(q.shape[0]):
+        L.vo_panda_sphere_fk(fp(q[i]), *base100, fp(out[i]))
+    return out
+
+
+def fkcc(env: Env, q, base100=(0, 0, 0), G=1, stats=False):
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, 7)
+    N = q.shape[0]
+    assert N % G == 0
+    ce = env.c()
+    L = lib()
+    res = np.zeros(N // G, bool)
+    tm = np.zeros(N // G)
+    cm = np.zeros(N // G)
+    fl = np.zeros(N // G)
+    for i in range(N // G):
+        st = VoStats(np.inf, np.inf, 0.0)
+        res[i] = L.vo_panda_fkcc_block(C.byref(ce), fp(q[i * G:(i + 1) * G]), G, *base100, C.byref(st))
+        tm[i], cm[i], fl[i] = st.test_margin, st.cull_margin, st.flops
+    if stats:
+        return res, tm, cm, fl
+    return res
+
+
+def fkcc_threads(env: Env, q, base100=(0, 0, 0), threads=8):
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, 7)
+    out = np.zeros(q.shape[0], np.uint8)
+    ce = env.c()
+    lib().vo_panda_fkcc_configs(C.byref(ce), fp(q), q.shape[0], *base100, out.ctypes.data_as(U8P), threads)
+    return out.astype(bool)
+
+
+def validate_motions(env: Env, starts, goals, base100=(0, 0, 0), threads=8):
+    s = np.ascontiguousarray(starts, np.float32).reshape(-1, 7)
+    g = np.ascontiguousarray(goals, np.float32).reshape(-1, 7)
+    ok = np.zeros(s.shape[0], np.uint8)
+    n = np.zeros(s.shape[0], np.int32)
+    ce = env.c()
+    lib().vo_panda_validate_motions(C.byref(ce), fp(s), fp(g), s.shape[0], *base100, ok.ctypes.data_as(U8P),
+                                    n.ctypes.data_as(I32P), threads)
+    return ok.astype(bool), n
+
+
+def rsqrt_probe():
+    lut = np.zeros(2 << 16, np.uint32)
+    k = C.c_int(0)
+    rc = lib().vo_rsqrt_probe(lut.ctypes.data_as(U32P), C.byref(k))
+    if rc != 0:
+        raise RuntimeError(f"rsqrt probe failed ({rc})")
+    return lut[: 2 << k.value].copy(), k.value
+
+
+def halton(dim, ks):
+    out = np.zeros((len(ks), dim), np.float32)
+    for i, k in enumerate(ks):
+        lib().vo_halton(dim, int(k), fp(out[i]))
+    return out
+
+
+def scale(q):
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, 7).copy()
+    for i in range(q.shape[0]):
+        lib().vo_panda_scale(fp(q[i]))
+    return q

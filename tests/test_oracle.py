@@ -1,0 +1,86 @@
+"""The C restatement against the reference's generated FK/fkcc (interpreted DAG fixtures).
+
+Fixtures: tools/make_golden.py evaluates robots/panda/fk.hh (sphere_fk and
+interleaved_sphere_fk) with tools/fkhh_interp.py.  Tolerances (north_star):
+FK sphere centres within 1e-5 absolute; collision masks bit-exact on every configuration
+whose margins clear the near-boundary band (MARGIN_*), with the flip count of the
+remainder reported.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden
+
+F = np.float32
+FK_TOL = 1e-5          # north_star: FK sphere centres within 1e-5 abs
+MARGIN_TEST = 1e-4     # |signed squared distance| (m^2) below which a test may flip under ~1e-6 FK noise
+MARGIN_CULL = 2e-3     # |min_distance - max_extent| (m) below which the rsqrt cull may differ across hosts
+
+
+def stable(test_margin, cull_margin, same_host):
+    m = test_margin > MARGIN_TEST
+    if not same_host:
+        m &= cull_margin > MARGIN_CULL
+    return m
+
+
+def same_rsqrt_host(oracle, fx):
+    lut, kb = oracle.rsqrt_probe()
+    return kb == int(fx["rsqrt_kbits"]) and np.array_equal(lut, fx["rsqrt_lut"])
+
+
+@pytest.mark.parametrize("tag,base", [("b000", (0, 0, 0)), ("b220", (200, 200, 0)), ("b105", (100, -50, 5))])
+def test_sphere_fk_vs_reference_dag(oracle, tag, base):
+    fx = golden("fk_panda.npz")
+    got = oracle.sphere_fk(fx["q"], base)
+    err = np.abs(got - fx[tag]).max()
+    assert err <= FK_TOL, err
+    assert err <= 1e-6  # observed 2.4e-7: a regression far inside the contract tolerance is still a bug
+
+
+def test_fkcc_mask_vs_reference_dag(oracle):
+    fx = golden("fkcc_panda_cage.npz")
+    env = oracle.sphere_cage_env()
+    assert np.array_equal(env.arrays()["spheres"], fx["env_spheres"])
+    same = same_rsqrt_host(oracle, fx)
+    for sfx, base in (("", (0, 0, 0)), ("_b220", (200, 200, 0))):
+        q = fx["q" + sfx]
+        got = oracle.fkcc_threads(env, q, base)
+        ref = fx["valid" + sfx]
+        m = stable(fx["test_margin" + sfx], fx["cull_margin" + sfx], same)
+        assert m.mean() > 0.97
+        assert np.array_equal(got[m], ref[m])
+        flips = int((got != ref).sum())
+        assert flips <= max(2, int(2e-4 * len(q))), flips
+
+
+def test_validate_motion_vs_reference_dag(oracle):
+    fx = golden("edges_panda_cage.npz")
+    env = oracle.sphere_cage_env()
+    ok, n = oracle.validate_motions(env, fx["starts"], fx["goals"], (0, 0, 0))
+    assert np.array_equal(n, fx["n"])
+    same = same_rsqrt_host(oracle, golden("fkcc_panda_cage.npz"))
+    m = stable(fx["test_margin"], fx["cull_margin"], same)
+    assert np.array_equal(ok[m], fx["ok"][m])
+    assert int((ok != fx["ok"]).sum()) <= 2
+
+
+def test_rake_block_equals_broadcast_single_config(oracle):
+    """validate(q) == validate_motion(q, q) == fkcc of the broadcast block
+    (bindings/common.hh:172-182): n == 1 and the block is q in every lane."""
+    fx = golden("fkcc_panda_cage.npz")
+    env = oracle.sphere_cage_env()
+    q = fx["q"][:512]
+    ok, n = oracle.validate_motions(env, q, q, (0, 0, 0))
+    assert (n == 1).all()
+    assert np.array_equal(ok, oracle.fkcc(env, q))
+
+
+def test_empty_environment_is_self_collision_only(oracle):
+    fx = golden("fkcc_panda_cage.npz")
+    q = fx["q"][:4096]
+    empty = oracle.Env()
+    v_empty = oracle.fkcc(empty, q)
+    v_cage = oracle.fkcc(oracle.sphere_cage_env(), q)
+    assert (v_cage <= v_empty).all()        # adding obstacles never validates a configuration
+    assert 0.85 < v_empty.mean() < 0.95     # ~9.5% of uniform Panda configurations self-collide

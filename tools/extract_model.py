@@ -1,0 +1,192 @@
+"""Extract ``model/panda.json`` (kinematic tree + collision hierarchy, as data).
+
+    python tools/extract_model.py [--ref /root/reference] [--out model/panda.json]
+
+Build-container tool; see tools/robot_model.py for what is extracted and from where.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import re
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(__file__))
+import fkhh_interp as fi  # noqa: E402
+import robot_model as rm  # noqa: E402
+
+
+def collect_calls(ast, Q, base100):
+    ev = fi.Evaluator(Q, base100, "exact64")
+    ev.bind_base()
+    calls = []
+
+    def walk(stmts, depth, parent):
+        for st in stmts:
+            if st[0] in ("decl", "fdecl"):
+                ev.env[st[1]] = ev.ev(st[2])
+            elif st[0] == "if":
+                args = [ev.arg(a) for a in st[1][1]]
+                calls.append(dict(depth=depth, kind=st[1][0], args=args, parent=parent))
+                walk(st[2], depth + 1, len(calls) - 1)
+
+    walk(ast, 0, -1)
+    return calls
+
+
+def extract_panda(ref):
+    urdf = f"{ref}/resources/panda/panda_spherized.urdf"
+    fkhh = f"{ref}/src/impl/vamp/robots/panda/fk.hh"
+    src = open(fkhh).read()
+    links, joints = rm.parse_urdf(urdf)
+    frames = rm.build_frames(links, joints, "panda_link0")
+    fname = [f["name"] for f in frames]
+    fk = fi.parse_function(src, r"inline void sphere_fk\(")
+    cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
+    cc_text = fi.function_body(src, r"inline bool interleaved_sphere_fk\(")
+    labels = re.findall(r"if \(/\*(.*?)\*/", cc_text)
+
+    rng = np.random.default_rng(12345)
+    K = 8
+    lo = np.array([f["lower"] for f in frames if f["dof"] >= 0])
+    hi = np.array([f["upper"] for f in frames if f["dof"] >= 0])
+    Q = lo + rng.random((K, len(lo))) * (hi - lo)
+    xyz, rad = fi.run_sphere_fk(fk, Q, (0, 0, 0), mode="exact64")
+    poses = [rm.fk_exact(frames, Q[k]) for k in range(K)]
+
+    def local_in(fidx, pts):
+        loc = np.array([rm.qmat(poses[k][0][fidx]).T @ (pts[k] - poses[k][1][fidx]) for k in range(K)])
+        return loc, np.abs(loc - loc[0]).max()
+
+    # ---- spheres: reference index -> (frame, URDF offset, radius)
+    spheres = []
+    for s in range(xyz.shape[1]):
+        pts = xyz[:, s, :].T
+        found = None
+        for fidx, f in enumerate(frames):
+            loc, spread = local_in(fidx, pts)
+            if spread > 2e-6:
+                continue
+            for j, (o, r) in enumerate(links[f["name"]]):
+                if np.abs(np.array(o) - loc[0]).max() < 2e-6 and abs(r - rad[s]) < 1e-9:
+                    found = dict(frame=fidx, offset=[float(v) for v in o], radius=float(r), link=f["name"], urdf_index=j)
+        if found is None:
+            raise RuntimeError(f"sphere {s} not matched")
+        spheres.append(found)
+
+    def sphere_at(pts, r):
+        d = np.abs(xyz - pts.T[:, None, :]).max(axis=(0, 2))
+        hits = [s for s in range(len(spheres)) if d[s] < 2e-6 and abs(rad[s] - r) < 1e-9]
+        return hits[0] if len(hits) == 1 else None
+
+    calls0 = collect_calls(cc, Q, (0, 0, 0))
+    calls1 = collect_calls(cc, Q, (200, 200, 0))
+    top = [i for i, c in enumerate(calls0) if c["depth"] == 0]
+    assert len(top) == len(labels), (len(top), len(labels))
+
+    bounding = {}  # link -> dict
+    env_checks = []
+    self_checks = []
+
+    def has_base(i, argslice):
+        a = np.stack([calls0[i]["args"][k] for k in argslice])
+        b = np.stack([calls1[i]["args"][k] for k in argslice])
+        d = b - a
+        if np.abs(d).max() < 1e-9:
+            return False
+        assert np.allclose(d[0], 2.0) and np.allclose(d[1], 2.0) and np.allclose(d[2], 0.0), d
+        return True
+
+    # pass 1: env bounding spheres (link named in the generator's comment)
+    for t, lab in zip(top, labels):
+        c = calls0[t]
+        if c["kind"] != "env":
+            continue
+        link = lab.strip()
+        fidx = fname.index(link)
+        pts = np.stack(c["args"][:3]).T
+        loc, spread = local_in(fidx, pts)
+        assert spread < 2e-6, (link, spread)
+        r = float(c["args"][3][0])
+        kids = [i for i, cc_ in enumerate(calls0) if cc_["parent"] == t]
+        children = []
+        for i in kids:
+            kp = np.stack(calls0[i]["args"][:3]).T
+            s = sphere_at(kp, float(calls0[i]["args"][3][0]))
+            assert s is not None, (link, i)
+            children.append(dict(sphere=s, base=has_base(i, range(3))))
+        b = dict(link=link, frame=fidx, offset=[float(round(v, 6)) for v in loc[0]], radius=r, base=has_base(t, range(3)))
+        bounding[link] = b
+        env_checks.append(dict(link=link, bounding_base=b["base"], children=children))
+
+    def entity(pts, r):
+        s = sphere_at(pts, r)
+        if s is not None:
+            return dict(sphere=s)
+        for link, b in bounding.items():
+            fidx = b["frame"]
+            loc, spread = local_in(fidx, pts)
+            if spread < 2e-6 and np.abs(loc[0] - np.array(b["offset"])).max() < 2e-6 and abs(r - b["radius"]) < 1e-9:
+                return dict(bound=link)
+        raise RuntimeError("unmatched self-collision entity")
+
+    order = []
+    for t, lab in zip(top, labels):
+        c = calls0[t]
+        if c["kind"] == "env":
+            order.append(dict(kind="env", index=[e["link"] for e in env_checks].index(lab.strip())))
+            continue
+        a_link, b_link = [s.strip() for s in lab.split("vs.")]
+        pa, pb = np.stack(c["args"][:3]).T, np.stack(c["args"][4:7]).T
+        ea = entity(pa, float(c["args"][3][0]))
+        eb = entity(pb, float(c["args"][7][0]))
+        kids = [i for i, cc_ in enumerate(calls0) if cc_["parent"] == t]
+        pairs = []
+        for i in kids:
+            ka = sphere_at(np.stack(calls0[i]["args"][:3]).T, float(calls0[i]["args"][3][0]))
+            kb = sphere_at(np.stack(calls0[i]["args"][4:7]).T, float(calls0[i]["args"][7][0]))
+            assert ka is not None and kb is not None
+            pairs.append([ka, kb])
+        self_checks.append(dict(links=[a_link, b_link], a=ea, b=eb, children=pairs))
+        order.append(dict(kind="self", index=len(self_checks) - 1))
+
+    dof_frames = [f for f in frames if f["dof"] >= 0]
+    model = dict(
+        robot="panda",
+        source=dict(urdf="resources/panda/panda_spherized.urdf", fk="src/impl/vamp/robots/panda/fk.hh"),
+        dimension=len(dof_frames),
+        resolution=32,  # robots/panda_base.hh:21
+        # scale_configuration: q * s_m + s_a (robots/panda/fk.hh:14-37); descale (fk.hh:39-62)
+        s_m=[5.9342, 3.6652, 5.9342, 3.2289, 5.9342, 3.9095999999999997, 5.9342],
+        s_a=[-2.9671, -1.8326, -2.9671, -3.1416, -2.9671, -0.0873, -2.9671],
+        d_m=[0.1685147113342995, 0.2728364072901888, 0.1685147113342995, 0.30970299482796, 0.1685147113342995,
+             0.25578064252097404, 0.1685147113342995],
+        space_measure=878819.1112640093,
+        frames=[dict(name=f["name"], parent=f["parent"], t=f["t"], qf=f["qf"], dof=f["dof"]) for f in frames],
+        spheres=spheres,
+        bounding=list(bounding.values()),
+        env_checks=env_checks,
+        self_checks=self_checks,
+        check_order=order,
+    )
+    return model
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "model", "panda.json"))
+    a = ap.parse_args()
+    m = extract_panda(a.ref)
+    with open(a.out, "w") as f:
+        json.dump(m, f, indent=1)
+    print(f"wrote {a.out}: {len(m['spheres'])} spheres, {len(m['env_checks'])} env checks "
+          f"({sum(len(c['children']) for c in m['env_checks'])} children), {len(m['self_checks'])} self pairs "
+          f"({sum(len(c['children']) for c in m['self_checks'])} children)")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,175 @@
+"""Generate the committed golden fixtures under tests/golden/.
+
+    python tools/make_golden.py            (build container only: needs /root/reference)
+
+Two independent sources, neither of them this project's product code:
+
+1. ``ref_pins.npz`` -- outputs of ``oracle/_ref/ref_probe``, compiled by oracle/Makefile
+   from the reference's own vector layer and halton.hh with the reference release flags
+   (sin/cos, max_extent sqrt, the validate_motion rake arithmetic, Halton<7|8>).
+2. ``fk_panda.npz``, ``fkcc_panda_cage.npz``, ``edges_panda_cage.npz``,
+   ``mbm_table_pick.npz`` -- the reference's generated ``robots/panda/fk.hh`` (sphere_fk and
+   interleaved_sphere_fk) evaluated by ``tools/fkhh_interp.py`` (ref32 mode), with the
+   collision predicates of collision/validity.hh restated in numpy.  Each mask carries the
+   margins (min |test value|, min |cull difference|) used for margin-filtered parity.
+
+Inputs are seeded numpy draws (not the reference's mt19937 stream -- the reference has no
+runnable driver here); the scenes are the reference's sphere cage
+(scripts/cpp/benchmark_collision_checks.cc:33-51) and MotionBenchMaker table_pick problems
+(resources/panda/problems.tar.bz2).
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import fkhh_interp as fi  # noqa: E402
+import oracle_py as op  # noqa: E402
+
+GOLD = os.path.join(ROOT, "tests", "golden")
+PROBE = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
+F = np.float32
+
+LO = np.array([-2.9671, -1.8326, -2.9671, -3.1416, -2.9671, -0.0873, -2.9671], F)
+HI = np.array([2.9671, 1.8326, 2.9671, 0.0873, 2.9671, 3.8223, 2.9671], F)
+
+
+def probe(mode, arr, *args):
+    with tempfile.TemporaryDirectory() as d:
+        i, o = os.path.join(d, "in.bin"), os.path.join(d, "out.bin")
+        np.asarray(arr, F).tofile(i)
+        subprocess.check_call([PROBE, mode, i, o, *map(str, args)])
+        return np.fromfile(o, F)
+
+
+def make_ref_pins(rng):
+    q = np.concatenate([rng.uniform(-3.3, 4.0, 65536 - 4096), np.linspace(-3.2, 3.9, 4096)]).astype(F)
+    sc = probe("sincos", q)
+    n = len(q)
+    ext_in = np.zeros((8192, 4), F)
+    ext_in[:, :3] = rng.uniform(-1.6, 1.6, (8192, 3)).astype(F)
+    ext_in[:8, :3] = 0.0  # zero vector: rsqrt(0) = inf -> NaN extent
+    ext_in[:, 3] = np.repeat(rng.choice(np.array([0.012, 0.06, 0.104, 0.154, 0.2], F), 1024), 8)
+    ex = probe("extent", ext_in)
+    # rake: random edges of all lengths + short ones
+    E = 1024
+    s = (LO + rng.random((E, 7), dtype=F) * (HI - LO)).astype(F)
+    g = (LO + rng.random((E, 7), dtype=F) * (HI - LO)).astype(F)
+    g[: E // 2] = (s[: E // 2] + (g[: E // 2] - s[: E // 2]) * F(0.15)).astype(F)
+    g[:4] = s[:4]  # zero-length edges (validate(q) path)
+    NB = 4
+    rk = probe("rake", np.concatenate([s, g], 1), NB).reshape(E, 2 + NB * 56)
+    h7 = np.concatenate([probe("halton", [0], 7, 2048, 0).reshape(-1, 7),
+                         probe("halton", [0], 7, 40, 999_980).reshape(-1, 7)])
+    h8 = np.concatenate([probe("halton", [0], 8, 2048, 0).reshape(-1, 8),
+                         probe("halton", [0], 8, 40, 999_980).reshape(-1, 8),
+                         probe("halton", [0], 8, 24, 2_000_990).reshape(-1, 8)])
+    k7 = np.concatenate([np.arange(1, 2049), np.arange(999_981, 1_000_021)])
+    k8 = np.concatenate([k7, np.arange(2_000_991, 2_001_015)])
+    lut, kb = op.rsqrt_probe()
+    np.savez_compressed(os.path.join(GOLD, "ref_pins.npz"), sincos_q=q, sin=sc[:n], cos=sc[n:],
+                        extent_in=ext_in, extent=ex[:8192], extent_root=ex[8192:], rsqrt_lut=lut, rsqrt_kbits=kb,
+                        rake_starts=s, rake_goals=g, rake_out=rk, rake_blocks=NB, halton7=h7, halton7_k=k7,
+                        halton8=h8, halton8_k=k8)
+
+
+def sphere_cage():
+    e = op.sphere_cage_env()
+    return e, fi.EnvNP(spheres=e.arrays()["spheres"])
+
+
+def interp_validate(cc, starts, goals, base, envnp, rs):
+    """validate_motion (planning/validate.hh:23-75) over E edges, 8-lane groups."""
+    E = starts.shape[0]
+    v = (goals - starts).astype(F)
+    sq = (v * v).astype(F)
+    dist = np.sqrt((((sq[:, 0] + sq[:, 4]) + (sq[:, 2] + sq[:, 6])) + ((sq[:, 1] + sq[:, 5]) + (sq[:, 3] + F(0))))
+                   .astype(F)).astype(F)
+    n = np.maximum(np.ceil((dist / F(8) * F(32)).astype(F)), F(1)).astype(np.int64)
+    pct = (np.arange(1, 9, dtype=F) / F(8)).astype(F)
+    block = fi.fma32(v[:, None, :], pct[None, :, None], starts[:, None, :])  # (E, 8, 7)
+    back = (v / (F(8) * n[:, None].astype(F))).astype(F)
+    ok = np.ones(E, bool)
+    tmarg = np.full(E, np.inf)
+    cmarg = np.full(E, np.inf)
+    alive = np.ones(E, bool)
+    for k in range(int(n.max())):
+        if k > 0:
+            block = (block - back[:, None, :]).astype(F)
+        idx = np.where(alive & (n > k))[0]
+        if len(idx) == 0:
+            break
+        q = block[idx].reshape(-1, 7)
+        valid, st = fi.run_fkcc(cc, q, base, envnp, rs, G=8)
+        valid = valid.reshape(-1, 8)[:, 0]
+        tmarg[idx] = np.minimum(tmarg[idx], st.test_margin.reshape(-1, 8).min(1))
+        cmarg[idx] = np.minimum(cmarg[idx], st.cull_margin.reshape(-1, 8).min(1))
+        ok[idx] &= valid
+        alive[idx] &= valid
+    return ok, n, tmarg, cmarg
+
+
+def main():
+    os.makedirs(GOLD, exist_ok=True)
+    if not os.path.exists(PROBE):
+        subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "ref"])
+    rng = np.random.default_rng(20251015)
+    make_ref_pins(rng)
+    print("ref_pins.npz")
+
+    fk, cc = fi.load_panda()
+    lut, kb = op.rsqrt_probe()
+    rs = fi.RsqrtHost(lut, kb)
+
+    # ---- FK sphere centres at both bases
+    q = op.scale(rng.random((1024, 7), dtype=F))
+    out = {}
+    for tag, base in (("b000", (0, 0, 0)), ("b220", (200, 200, 0)), ("b105", (100, -50, 5))):
+        xyz, r = fi.run_sphere_fk(fk, q, base)
+        out[tag] = np.ascontiguousarray(np.transpose(xyz, (2, 1, 0)))
+    np.savez_compressed(os.path.join(GOLD, "fk_panda.npz"), q=q, radii=r.astype(F), **out)
+    print("fk_panda.npz")
+
+    # ---- per-configuration masks (G = 1) on the sphere cage
+    env, envnp = sphere_cage()
+    q = op.scale(rng.random((32768, 7), dtype=F))
+    valid, st = fi.run_fkcc(cc, q, (0, 0, 0), envnp, rs, G=1)
+    q2 = op.scale(rng.random((8192, 7), dtype=F))
+    valid2, st2 = fi.run_fkcc(cc, q2, (200, 200, 0), envnp, rs, G=1)
+    np.savez_compressed(os.path.join(GOLD, "fkcc_panda_cage.npz"), env_spheres=env.arrays()["spheres"], q=q,
+                        valid=valid, test_margin=st.test_margin.astype(F), cull_margin=st.cull_margin.astype(F),
+                        q_b220=q2, valid_b220=valid2, test_margin_b220=st2.test_margin.astype(F),
+                        cull_margin_b220=st2.cull_margin.astype(F), rsqrt_lut=lut, rsqrt_kbits=kb)
+    print("fkcc_panda_cage.npz", valid.mean(), valid2.mean())
+
+    # ---- edges: raw pairs and valid-endpoint pairs capped at length 1.0
+    E = 4096
+    s = op.scale(rng.random((E, 7), dtype=F))
+    g = op.scale(rng.random((E, 7), dtype=F))
+    pool = op.scale(rng.random((40000, 7), dtype=F))
+    pv = op.fkcc_threads(env, pool, (0, 0, 0))
+    vq = pool[pv]
+    sb, gb = vq[0:2 * E:2][:E], vq[1:2 * E:2][:E]
+    d = np.linalg.norm((gb - sb).astype(np.float64), axis=1)
+    scale = np.minimum(1.0, 1.0 / np.maximum(d, 1e-9)).astype(F)
+    gb = (sb + (gb - sb) * scale[:, None]).astype(F)
+    starts = np.concatenate([s, sb])
+    goals = np.concatenate([g, gb])
+    starts[:8] = goals[:8]  # zero-length edges
+    ok, n, tm, cm = interp_validate(cc, starts, goals, (0, 0, 0), envnp, rs)
+    np.savez_compressed(os.path.join(GOLD, "edges_panda_cage.npz"), starts=starts, goals=goals, ok=ok,
+                        n=n.astype(np.int32), test_margin=tm.astype(F), cull_margin=cm.astype(F))
+    print("edges_panda_cage.npz", ok[:E].mean(), ok[E:].mean(), n.max())
+
+
+if __name__ == "__main__":
+    main()
