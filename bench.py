@@ -157,7 +157,10 @@ def main():
     import vamp_amd as vamp
 
     ctx = vamp.context(local)
-    stream = torch.cuda.current_stream(dev)
+    # one explicit stream for torch plumbing AND the vgpu launches, so the HIP events below
+    # bracket exactly the kernels (the legacy default stream would be handle 0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     env = vamp.Environment()
     for c in CAGE:
@@ -235,7 +238,9 @@ def main():
         achieved = flops_edge * E / (kern_ms * 1e-3) / 1e12
         cpu = None
         if not a.no_cpu and world == 1:
-            cpu = cpu_baseline(s_np, g_np, a.cpu_seconds)
+            s_cpu = starts[: 1 << 20].cpu().numpy()
+            g_cpu = goals[: 1 << 20].cpu().numpy()
+            cpu = cpu_baseline(s_cpu, g_cpu, a.cpu_seconds)
         ms_step = wall_max / a.steps * 1e3
         line = {
             "metric": "validated edge-interpolants/sec (Panda 7-DOF FK+CC)",

@@ -128,8 +128,13 @@ __device__ __forceinline__ float sphere_sphere(float ax, float ay, float az, flo
 __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 
 // sphere_environment_in_collision (collision/validity.hh:46-150), one rake group
+#ifndef VGPU_ENV_INLINE
+#define VGPU_ENV_ATTR __noinline__
+#else
+#define VGPU_ENV_ATTR __forceinline__
+#endif
 template <class Grp>
-__device__ __noinline__ bool env_collide(const EnvView& env, float x, float y, float z, float r)
+__device__ VGPU_ENV_ATTR bool env_collide(const EnvView& env, float x, float y, float z, float r)
 {
     const float d = dot3(x, y, z, x, y, z);
     const float me = sqrt_host(d, env.lut, env.kbits) + r;  // validity.hh:55-59

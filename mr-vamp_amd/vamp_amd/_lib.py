@@ -10,7 +10,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libvampgpu.so")
+# VAMP_AMD_LIB selects an alternative build of the same ABI (kernel variants for A/B timing)
+LIB_PATH = os.environ.get("VAMP_AMD_LIB") or os.path.join(HERE, "libvampgpu.so")
 
 VGPU_OK = 0
 VGPU_ROBOT_PANDA = 1
