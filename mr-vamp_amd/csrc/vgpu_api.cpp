@@ -24,9 +24,15 @@ hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float
                                        size_t ld, hipStream_t st);
 hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, float bx, float by, float bz,
                                   uint8_t* valid, hipStream_t st);
-hipError_t vgpu_launch_panda_validate(const float* starts, const float* goals, size_t n_edges, const EnvView* env,
-                                      float bx, float by, float bz, uint8_t* ok, int32_t* n_blocks,
-                                      hipStream_t st);
+size_t vgpu_validate_scan_bytes(size_t n_edges);
+hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goals, size_t n_edges,
+                                           const EnvView* env, float bx, float by, float bz, uint8_t* ok,
+                                           int32_t* n_blocks, uint32_t* cnt, uint32_t* off, void* scan_tmp,
+                                           size_t scan_bytes, hipStream_t st);
+hipError_t vgpu_launch_panda_validate_tail(const float* starts, const float* goals, size_t n_edges,
+                                           size_t n_items, const EnvView* env, float bx, float by, float bz,
+                                           uint8_t* ok, const uint32_t* cnt, const uint32_t* off,
+                                           uint32_t* item_edge, hipStream_t st);
 }
 
 namespace {
@@ -117,6 +123,12 @@ struct vgpu_ctx {
     // staging for the *_host conveniences
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    // validate workspace: cnt/off (n_edges + 1 each), scan temp, work items, pinned total
+    void* ws = nullptr;
+    size_t ws_bytes = 0;
+    uint32_t* items = nullptr;
+    size_t items_cap = 0;
+    uint32_t* total_host = nullptr;
 };
 
 struct vgpu_env {
@@ -127,7 +139,7 @@ struct vgpu_env {
     bool dirty = true;
     float* dev = nullptr;
     size_t dev_floats = 0;
-    size_t off[5] = {0, 0, 0, 0, 0};
+    int n_obs = 0;
 };
 
 #define HIPCHK(ctx, expr)                                                                          \
@@ -188,6 +200,9 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->own) (void)hipStreamSynchronize(c->own);
     if (c->lut_dev) (void)hipFree(c->lut_dev);
     if (c->stage) (void)hipFree(c->stage);
+    if (c->ws) (void)hipFree(c->ws);
+    if (c->items) (void)hipFree(c->items);
+    if (c->total_host) (void)hipHostFree(c->total_host);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -392,34 +407,36 @@ extern "C" int vgpu_env_counts(const vgpu_env* e, int32_t counts[5])
     return VGPU_OK;
 }
 
-template <size_t W>
-static void sort_md(std::vector<std::array<float, W>>& v)  // environment.hh:40-66
-{
-    std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a[W - 1] < b[W - 1]; });
-}
-
+// One list of all obstacles sorted by min_distance (see EnvView in vgpu_device.hh): per type
+// this is the reference's sort (environment.hh:40-66); merging the types is exact because
+// every type's loop evaluates exactly the obstacles with min_distance below the group's
+// largest max_extent.
 extern "C" int vgpu_env_upload(vgpu_env* e)
 {
     if (!e) return VGPU_ERR_INVALID_ARG;
     vgpu_ctx* c = e->ctx;
     if (!e->dirty && e->dev) return VGPU_OK;
-    sort_md(e->spheres);
-    sort_md(e->capsules);
-    sort_md(e->zcapsules);
-    sort_md(e->cuboids);
-    sort_md(e->zcuboids);
-    std::vector<float> blob;
-    auto put = [&](auto& v, int slot) {
-        e->off[slot] = blob.size();
-        for (auto& row : v) blob.insert(blob.end(), row.begin(), row.end());
-        while (blob.size() % 16) blob.push_back(0.0f);  // 64-B aligned sections
+    struct Rec {
+        float md;
+        std::array<float, kObsStride> r;
     };
-    put(e->spheres, 0);
-    put(e->capsules, 1);
-    put(e->zcapsules, 2);
-    put(e->cuboids, 3);
-    put(e->zcuboids, 4);
-    if (blob.empty()) blob.assign(16, 0.0f);
+    std::vector<Rec> recs;
+    auto add = [&](int type, float md, const float* p, int np) {
+        Rec rec{md, {}};
+        int t = type;
+        std::memcpy(&rec.r[0], &t, 4);
+        rec.r[1] = md;
+        for (int i = 0; i < np; ++i) rec.r[2 + i] = p[i];
+        recs.push_back(rec);
+    };
+    for (auto& o : e->spheres) add(OBS_SPHERE, o[4], o.data(), 4);
+    for (auto& o : e->capsules) add(OBS_CAPSULE, o[8], o.data(), 8);
+    for (auto& o : e->zcapsules) add(OBS_ZCAPSULE, o[8], o.data(), 8);
+    for (auto& o : e->cuboids) add(OBS_CUBOID, o[15], o.data(), 15);
+    for (auto& o : e->zcuboids) add(OBS_ZCUBOID, o[15], o.data(), 15);
+    std::stable_sort(recs.begin(), recs.end(), [](const Rec& a, const Rec& b) { return a.md < b.md; });
+    std::vector<float> blob(std::max<size_t>(recs.size(), 1) * kObsStride, 0.0f);
+    for (size_t i = 0; i < recs.size(); ++i) std::copy(recs[i].r.begin(), recs[i].r.end(), &blob[i * kObsStride]);
     HIPCHK(c, hipSetDevice(c->device));
     if (blob.size() > e->dev_floats) {
         if (e->dev) {
@@ -432,6 +449,7 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     }
     HIPCHK(c, hipMemcpyAsync(e->dev, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));  // blob is a host temporary
+    e->n_obs = (int)recs.size();
     e->dirty = false;
     return VGPU_OK;
 }
@@ -439,17 +457,8 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
 static EnvView make_view(const vgpu_env* e)
 {
     EnvView v{};
-    auto p = [&](int s) { return (const VGPU_CONST float*)(e->dev + e->off[s]); };
-    v.spheres = p(0);
-    v.capsules = p(1);
-    v.zcapsules = p(2);
-    v.cuboids = p(3);
-    v.zcuboids = p(4);
-    v.n_spheres = (int)e->spheres.size();
-    v.n_capsules = (int)e->capsules.size();
-    v.n_zcapsules = (int)e->zcapsules.size();
-    v.n_cuboids = (int)e->cuboids.size();
-    v.n_zcuboids = (int)e->zcuboids.size();
+    v.obs = (const VGPU_CONST float*)e->dev;
+    v.n_obs = e->n_obs;
     v.lut = e->ctx->lut_dev;
     v.kbits = e->ctx->kbits;
     return v;
@@ -504,6 +513,28 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     return VGPU_OK;
 }
 
+static int ensure_ws(vgpu_ctx* c, size_t n_edges, uint32_t** cnt, uint32_t** off, void** tmp, size_t* tmp_bytes)
+{
+    const size_t idx_bytes = ((n_edges + 1) * sizeof(uint32_t) + 255) & ~(size_t)255;
+    *tmp_bytes = vgpu_validate_scan_bytes(n_edges);
+    const size_t need = 2 * idx_bytes + *tmp_bytes + 256;
+    if (need > c->ws_bytes) {
+        if (c->ws) {
+            HIPCHK(c, hipStreamSynchronize(c->cur));
+            HIPCHK(c, hipFree(c->ws));
+            c->ws = nullptr;
+        }
+        HIPCHK(c, hipMalloc(&c->ws, need));
+        c->ws_bytes = need;
+    }
+    if (!c->total_host) HIPCHK(c, hipHostMalloc((void**)&c->total_host, sizeof(uint32_t), hipHostMallocDefault));
+    char* p = (char*)c->ws;
+    *cnt = (uint32_t*)p;
+    *off = (uint32_t*)(p + idx_bytes);
+    *tmp = p + 2 * idx_bytes;
+    return VGPU_OK;
+}
+
 extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* starts,
                                      const float* goals, size_t n_edges, uint8_t* ok, int32_t* n_blocks)
 {
@@ -511,12 +542,31 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     float b[3];
     int rc = check_robot(c, r, b);
     if (rc) return rc;
-    if (n_edges && (!starts || !goals || !ok)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
-    if (n_edges > ((size_t)1 << 40)) return fail(c, VGPU_ERR_INVALID_ARG, "too many edges");
+    if (n_edges == 0) return VGPU_OK;
+    if (!starts || !goals || !ok) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if (n_edges >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many edges in one call (< 2^31)");
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, vgpu_launch_panda_validate(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, c->cur));
+    uint32_t *cnt, *off;
+    void* tmp;
+    size_t tmp_bytes;
+    if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
+    HIPCHK(c, vgpu_launch_panda_validate_head(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, cnt, off,
+                                              tmp, tmp_bytes, c->cur));
+    // number of back-step work items: one D2H word (the item buffer is sized from it)
+    HIPCHK(c, hipMemcpyAsync(c->total_host, off + n_edges, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    const size_t n_items = *c->total_host;
+    if (n_items > c->items_cap) {
+        if (c->items) HIPCHK(c, hipFree(c->items));
+        c->items = nullptr;
+        const size_t cap = std::max(n_items, (size_t)1 << 20);
+        HIPCHK(c, hipMalloc(&c->items, cap * sizeof(uint32_t)));
+        c->items_cap = cap;
+    }
+    HIPCHK(c, vgpu_launch_panda_validate_tail(starts, goals, n_edges, n_items, &v, b[0], b[1], b[2], ok, cnt, off,
+                                              c->items, c->cur));
     return VGPU_OK;
 }
 

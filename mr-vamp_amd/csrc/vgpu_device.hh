@@ -11,7 +11,7 @@
 //     configuration) shares its decisions: an obstacle loop stops when ALL lanes of the
 //     group are culled, a check fires when ANY lane's test is negative
 //     (collision/validity.hh:46-150).  For G = 8 the group is 8 consecutive lanes of a
-//     wave64 and the reductions are one ballot + scalar bit-twiddling + inverse ballot.
+//     wave64 (a DPP half-row) and the reductions are three DPP shuffles.
 //
 // Compiled with -ffp-contract=off: every fmaf below is intended, nothing else fuses.
 #pragma once
@@ -22,31 +22,42 @@
 #define VGPU_CONST __attribute__((address_space(4)))
 
 // ---- group reductions -----------------------------------------------------------------
+// A rake group is G consecutive lanes of a wave64 (G = 8 -> one DPP half-row).  The
+// reductions are VALU DPP shuffles (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror), so the
+// scalar unit stays free for loop control and obstacle loads.
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v)
+{
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, false);
+}
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v)
+{
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
 struct Grp1 {
     static constexpr int G = 1;
     __device__ static __forceinline__ bool any(bool p) { return p; }
-    __device__ static __forceinline__ bool all(bool p) { return p; }
+    __device__ static __forceinline__ float max(float v) { return v; }
 };
 
 struct Grp8 {
     static constexpr int G = 8;
     __device__ static __forceinline__ bool any(bool p)
     {
-        unsigned long long t = __ballot(p);
-        t |= t >> 1;
-        t |= t >> 2;
-        t |= t >> 4;
-        t &= 0x0101010101010101ull;
-        return __builtin_amdgcn_inverse_ballot_w64(t * 0xFFull);
+        int x = p ? 1 : 0;
+        x |= dpp_i<0xB1>(x);   // quad_perm [1,0,3,2]
+        x |= dpp_i<0x4E>(x);   // quad_perm [2,3,0,1]
+        x |= dpp_i<0x141>(x);  // row_half_mirror
+        return x != 0;
     }
-    __device__ static __forceinline__ bool all(bool p)
+    __device__ static __forceinline__ float max(float v)
     {
-        unsigned long long t = __ballot(p);
-        t &= t >> 1;
-        t &= t >> 2;
-        t &= t >> 4;
-        t &= 0x0101010101010101ull;
-        return __builtin_amdgcn_inverse_ballot_w64(t * 0xFFull);
+        v = fmaxf(v, dpp_f<0xB1>(v));
+        v = fmaxf(v, dpp_f<0x4E>(v));
+        v = fmaxf(v, dpp_f<0x141>(v));
+        return v;
     }
 };
 
@@ -74,16 +85,23 @@ __device__ __forceinline__ float vamp_cos(float x)
 }
 
 // ---- environment view ----------------------------------------------------------------------
-// Obstacle rows (float32), each list sorted ascending by min_distance (last field):
-//   sphere [5] x y z r md | capsule [9] x1 y1 z1 xv yv zv r rdv md | cuboid [16] x y z a1 a2 a3 r1 r2 r3 md
+// All obstacles of collision::Environment<float> in ONE list sorted ascending by
+// min_distance, one 32-float (128 B) record each:
+//   [0] type (int bits: 0 sphere, 1 capsule, 2 z-capsule, 3 cuboid, 4 z-cuboid)  [1] min_distance
+//   sphere   [2..5]  x y z r
+//   capsule  [2..9]  x1 y1 z1 xv yv zv r rdv                     (z-capsule: same layout)
+//   cuboid   [2..16] x y z a1x a1y a1z a2x a2y a2z a3x a3y a3z r1 r2 r3   (z-cuboid: same)
+// The reference keeps one sorted list per type and stops each type's loop at its own first
+// all-lanes-culled obstacle (validity.hh:61-127); that stop is monotone in min_distance, so
+// per type it evaluates exactly {j : md_j < max_extent_max} and the union over types is the
+// same prefix of the merged list (see env_lane).
+enum : int { OBS_SPHERE = 0, OBS_CAPSULE = 1, OBS_ZCAPSULE = 2, OBS_CUBOID = 3, OBS_ZCUBOID = 4 };
+constexpr int kObsStride = 32;
+
 struct EnvView {
-    const VGPU_CONST float* spheres;
-    const VGPU_CONST float* capsules;
-    const VGPU_CONST float* zcapsules;
-    const VGPU_CONST float* cuboids;
-    const VGPU_CONST float* zcuboids;
+    const VGPU_CONST float* obs;
     const uint32_t* lut;  // host rsqrt table, 2 << kbits entries
-    int n_spheres, n_capsules, n_zcapsules, n_cuboids, n_zcuboids;
+    int n_obs;
     int kbits;
 };
 
@@ -127,83 +145,77 @@ __device__ __forceinline__ float sphere_sphere(float ax, float ay, float az, flo
 
 __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 
-// sphere_environment_in_collision (collision/validity.hh:46-150), one rake group
-#ifndef VGPU_ENV_INLINE
-#define VGPU_ENV_ATTR __noinline__
-#else
-#define VGPU_ENV_ATTR __forceinline__
-#endif
+// sphere_environment_in_collision (collision/validity.hh:46-150) for one lane of a rake group.
+//
+// Returns this lane's hit over exactly the obstacles the reference evaluates for the whole
+// group; the group result (the reference's return value) is Grp::any() of it, taken by the
+// caller.  Reference loop per type: `if (all lanes: min_distance - max_extent >= +0) break;
+// if (any lane: test < 0) return true;`.  Since the float difference of two floats is >= +0
+// exactly when min_distance >= max_extent, "all lanes culled" == min_distance >= the group
+// maximum of max_extent (a NaN/inf extent -- 0 or denormal |c|^2 -- never culls: +inf).  The
+// `return true` only ends work early: a lane stops at its own first hit, which leaves the
+// group OR unchanged.
 template <class Grp>
-__device__ VGPU_ENV_ATTR bool env_collide(const EnvView& env, float x, float y, float z, float r)
+__device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, float z, float r)
 {
     const float d = dot3(x, y, z, x, y, z);
-    const float me = sqrt_host(d, env.lut, env.kbits) + r;  // validity.hh:55-59
+    float me = sqrt_host(d, env.lut, env.kbits) + r;  // validity.hh:55-59
     const uint32_t dexp = __float_as_uint(d) & 0x7F800000u;
-    const bool nocull = dexp == 0u || dexp == 0x7F800000u;  // 0/denormal/inf/NaN: NaN extent
-
-    for (int j = 0; j < env.n_spheres; ++j) {
-        const VGPU_CONST float* o = env.spheres + 5 * j;
-        const bool cull = !nocull && !signbit_f(o[4] - me);
-        if (Grp::all(cull)) break;
-        const float v = sphere_sphere(o[0], o[1], o[2], o[3], x, y, z, r);
-        if (Grp::any(signbit_f(v))) return true;
-    }
-    for (int j = 0; j < env.n_capsules; ++j) {  // sphere_capsule.hh:9-22
-        const VGPU_CONST float* o = env.capsules + 9 * j;
-        const bool cull = !nocull && !signbit_f(o[8] - me);
-        if (Grp::all(cull)) break;
-        const float dot = dot3(x - o[0], y - o[1], z - o[2], o[3], o[4], o[5]);
-        const float cdf = fminf(fmaxf(dot * o[7], 0.0f), 1.0f);
-        const float px = __builtin_fmaf(o[3], cdf, o[0]);
-        const float py = __builtin_fmaf(o[4], cdf, o[1]);
-        const float pz = __builtin_fmaf(o[5], cdf, o[2]);
-        const float xs = x - px, ys = y - py, zs = z - pz;
-        const float rs = r + o[6];
-        const float v = __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
-        if (Grp::any(signbit_f(v))) return true;
-    }
-    for (int j = 0; j < env.n_zcapsules; ++j) {  // sphere_capsule.hh:30-43
-        const VGPU_CONST float* o = env.zcapsules + 9 * j;
-        const bool cull = !nocull && !signbit_f(o[8] - me);
-        if (Grp::all(cull)) break;
-        const float dot = (z - o[2]) * o[5];
-        const float cdf = fminf(fmaxf(dot * o[7], 0.0f), 1.0f);
-        const float pz = __builtin_fmaf(o[5], cdf, o[2]);
-        const float xs = x - o[0], ys = y - o[1], zs = z - pz;
-        const float rs = r + o[6];
-        const float v = __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
-        if (Grp::any(signbit_f(v))) return true;
-    }
+    if (dexp == 0u || dexp == 0x7F800000u || me != me) me = __builtin_inff();
+    const float emax = Grp::max(me);
     const float rsq = r * r;
-    for (int j = 0; j < env.n_cuboids; ++j) {  // sphere_cuboid.hh:9-27
-        const VGPU_CONST float* o = env.cuboids + 16 * j;
-        const bool cull = !nocull && !signbit_f(o[15] - me);
-        if (Grp::all(cull)) break;
-        const float xs = x - o[0], ys = y - o[1], zs = z - o[2];
-        const float a1 = max0(__builtin_fabsf(dot3(o[3], o[4], o[5], xs, ys, zs)) - o[12]);
-        const float a2 = max0(__builtin_fabsf(dot3(o[6], o[7], o[8], xs, ys, zs)) - o[13]);
-        const float a3 = max0(__builtin_fabsf(dot3(o[9], o[10], o[11], xs, ys, zs)) - o[14]);
-        const float v = dot3(a1, a2, a3, a1, a2, a3) - rsq;
-        if (Grp::any(signbit_f(v))) return true;
-    }
-    for (int j = 0; j < env.n_zcuboids; ++j) {  // sphere_cuboid.hh:35-52
-        const VGPU_CONST float* o = env.zcuboids + 16 * j;
-        const bool cull = !nocull && !signbit_f(o[15] - me);
-        if (Grp::all(cull)) break;
-        const float xs = x - o[0], ys = y - o[1], zs = z - o[2];
-        const float a1 = max0(__builtin_fabsf(dot2(o[3], o[4], xs, ys)) - o[12]);
-        const float a2 = max0(__builtin_fabsf(dot2(o[6], o[7], xs, ys)) - o[13]);
-        const float a3 = max0(__builtin_fabsf(zs) - o[14]);
-        const float v = dot3(a1, a2, a3, a1, a2, a3) - rsq;
-        if (Grp::any(signbit_f(v))) return true;
+
+    for (int j = 0; j < env.n_obs; ++j) {
+        const VGPU_CONST float* o = env.obs + kObsStride * j;
+        if (!(o[1] < emax)) break;  // every remaining obstacle is culled for the whole group
+        const int type = __float_as_int(o[0]);
+        float v;
+        if (type == OBS_SPHERE) {  // sphere_sphere.hh:10-22
+            v = sphere_sphere(o[2], o[3], o[4], o[5], x, y, z, r);
+        } else if (type == OBS_CAPSULE) {  // sphere_capsule.hh:9-22
+            const float dot = dot3(x - o[2], y - o[3], z - o[4], o[5], o[6], o[7]);
+            const float cdf = fminf(fmaxf(dot * o[9], 0.0f), 1.0f);
+            const float px = __builtin_fmaf(o[5], cdf, o[2]);
+            const float py = __builtin_fmaf(o[6], cdf, o[3]);
+            const float pz = __builtin_fmaf(o[7], cdf, o[4]);
+            const float xs = x - px, ys = y - py, zs = z - pz;
+            const float rs = r + o[8];
+            v = __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
+        } else if (type == OBS_ZCAPSULE) {  // sphere_capsule.hh:30-43
+            const float dot = (z - o[4]) * o[7];
+            const float cdf = fminf(fmaxf(dot * o[9], 0.0f), 1.0f);
+            const float pz = __builtin_fmaf(o[7], cdf, o[4]);
+            const float xs = x - o[2], ys = y - o[3], zs = z - pz;
+            const float rs = r + o[8];
+            v = __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
+        } else if (type == OBS_CUBOID) {  // sphere_cuboid.hh:9-27
+            const float xs = x - o[2], ys = y - o[3], zs = z - o[4];
+            const float a1 = max0(__builtin_fabsf(dot3(o[5], o[6], o[7], xs, ys, zs)) - o[14]);
+            const float a2 = max0(__builtin_fabsf(dot3(o[8], o[9], o[10], xs, ys, zs)) - o[15]);
+            const float a3 = max0(__builtin_fabsf(dot3(o[11], o[12], o[13], xs, ys, zs)) - o[16]);
+            v = dot3(a1, a2, a3, a1, a2, a3) - rsq;
+        } else {  // OBS_ZCUBOID, sphere_cuboid.hh:35-52
+            const float xs = x - o[2], ys = y - o[3], zs = z - o[4];
+            const float a1 = max0(__builtin_fabsf(dot2(o[5], o[6], xs, ys)) - o[14]);
+            const float a2 = max0(__builtin_fabsf(dot2(o[8], o[9], xs, ys)) - o[15]);
+            const float a3 = max0(__builtin_fabsf(zs) - o[16]);
+            v = dot3(a1, a2, a3, a1, a2, a3) - rsq;
+        }
+        if (signbit_f(v)) return true;  // this lane hit: the group result is already true
     }
     return false;
 }
 
 // sphere_sphere_self_collision (collision/validity.hh:13-44)
-template <class Grp>
-__device__ __forceinline__ bool self_collide(float ax, float ay, float az, float ar, float bx, float by, float bz,
-                                             float br)
+// (per lane; the group result is Grp::any of it).  self_bits returns the raw test-value
+// bits so a block of children reduces with one v_or per child (sign bit = collision).
+__device__ __forceinline__ uint32_t self_bits(float ax, float ay, float az, float ar, float bx, float by, float bz,
+                                              float br)
 {
-    return Grp::any(signbit_f(sphere_sphere(ax, ay, az, ar, bx, by, bz, br)));
+    return __float_as_uint(sphere_sphere(ax, ay, az, ar, bx, by, bz, br));
+}
+__device__ __forceinline__ bool self_lane(float ax, float ay, float az, float ar, float bx, float by, float bz,
+                                          float br)
+{
+    return signbit_f(sphere_sphere(ax, ay, az, ar, bx, by, bz, br));
 }

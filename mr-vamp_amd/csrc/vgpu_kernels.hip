@@ -1,16 +1,28 @@
 // vgpu_kernels.hip -- gfx950 kernels of the motion-validation rake.
 //
-// Three kernels per robot (Panda today):
-//   sphere_fk   one lane per configuration, SoA stores: the HBM-bound FK stream
-//               (reference robots/panda/fk.hh:104-1333 sphere_fk);
-//   fkcc        one lane per configuration (rake group G = 1 == a configuration broadcast
-//               to all 8 reference lanes): per-configuration validity mask
-//               (fk.hh:1335-6276 interleaved_sphere_fk);
-//   validate    one 8-lane group per edge (G = 8 == one reference rake block), looping over
-//               the edge's back-steps with the reference's early exit
-//               (planning/validate.hh:23-75).
-// All three are VALU code: FK is 7 chained quaternion products + sparse 3x3 transforms,
-// nothing here is a dense contraction worth MFMA (DESIGN.md "Why no MFMA").
+// Per robot (Panda today):
+//   sphere_fk      one lane per configuration, SoA stores: the HBM-bound FK stream
+//                  (reference robots/panda/fk.hh:104-1333 sphere_fk);
+//   fkcc           one lane per configuration (rake group G = 1 == a configuration broadcast
+//                  to all 8 reference lanes): per-configuration validity mask
+//                  (fk.hh:1335-6276 interleaved_sphere_fk);
+//   validate       validate_motion over a batch of edges (planning/validate.hh:23-75) in two
+//                  phases with the reference's early-exit semantics:
+//                    head  one 8-lane group per edge evaluates the first rake block
+//                          (t = 1/8 .. 8/8, validate.hh:31-44) and computes n_e;
+//                    scan  edges that survive with n_e > 1 get n_e - 1 work items;
+//                    tail  one 8-lane group per (edge, back-step k) evaluates block k,
+//                          reached by the reference's k sequential subtractions
+//                          (validate.hh:50-56), and clears the edge's flag on a hit.
+//                  On collision-heavy scenes most invalid edges die in the head block
+//                  (59.5 % of the bench edges, 0.06 % later), so the tail runs only for the
+//                  survivors, and adjacent groups of the tail are neighbouring blocks of one
+//                  edge (correlated branches).  The edge result equals the reference's
+//                  sequential loop: it is the AND of its blocks.
+// All of this is VALU code: FK is 7 chained quaternion products + sparse 3x3 transforms,
+// nothing is a dense contraction worth MFMA (DESIGN.md "Why no MFMA").
+#include <hipcub/hipcub.hpp>
+
 #include "vgpu_device.hh"
 
 #include "gen/panda_fk.inc"
@@ -39,51 +51,86 @@ __global__ __launch_bounds__(kBlock) void panda_fkcc_kernel(const float* __restr
     valid[i] = panda_fkcc<Grp1>(qi[0], qi[1], qi[2], qi[3], qi[4], qi[5], qi[6], env, bx, by, bz) ? 1 : 0;
 }
 
-// validate_vector (planning/validate.hh:23-65), rake = 8, resolution = 32 for the Panda.
-__global__ __launch_bounds__(kBlock) void panda_validate_kernel(const float* __restrict__ starts,
-                                                                const float* __restrict__ goals, size_t n_edges,
-                                                                EnvView env, float bx, float by, float bz,
-                                                                uint8_t* __restrict__ ok,
-                                                                int32_t* __restrict__ n_blocks)
+// ---- validate_vector: shared rake arithmetic (validate.hh:31-50) ----------------------------
+struct Rake {
+    float v[7];
+    int n;
+};
+
+__device__ __forceinline__ Rake rake_setup(const float* __restrict__ s, const float* __restrict__ g)
 {
-    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    const size_t e = tid >> 3;       // one 8-lane rake group per edge
-    const int lane = (int)(tid & 7);
-    if (e >= n_edges) return;        // group-uniform
-    const float* s = starts + 7 * e;
-    const float* g = goals + 7 * e;
-    float v[7], b[7];
+    Rake r;
 #pragma unroll
-    for (int j = 0; j < 7; ++j) v[j] = g[j] - s[j];  // validate.hh:72
-    // l2_norm in the AVX hsum lane order (vector/avx.hh:441-452), lane 7 padding = 0
-    const float a = (v[0] * v[0] + v[4] * v[4]) + (v[2] * v[2] + v[6] * v[6]);
-    const float c = (v[1] * v[1] + v[5] * v[5]) + (v[3] * v[3] + 0.0f);
+    for (int j = 0; j < 7; ++j) r.v[j] = g[j] - s[j];  // validate.hh:72
+    // l2_norm in the AVX hsum lane order (vector/avx.hh:441-452); lane 7 is padding 0
+    const float a = (r.v[0] * r.v[0] + r.v[4] * r.v[4]) + (r.v[2] * r.v[2] + r.v[6] * r.v[6]);
+    const float c = (r.v[1] * r.v[1] + r.v[5] * r.v[5]) + (r.v[3] * r.v[3] + 0.0f);
     const float distance = __builtin_sqrtf(a + c);
     float nf = __builtin_ceilf(distance / 8.0f * 32.0f);  // validate.hh:41
     if (!(nf > 1.0f)) nf = 1.0f;
-    const int n = (int)nf;
+    r.n = nf < 2147483520.0f ? (int)nf : 2147483520;
+    return r;
+}
+
+__global__ __launch_bounds__(kBlock) void panda_validate_head_kernel(
+    const float* __restrict__ starts, const float* __restrict__ goals, size_t n_edges, EnvView env, float bx,
+    float by, float bz, uint8_t* __restrict__ ok, int32_t* __restrict__ n_blocks, uint32_t* __restrict__ cnt)
+{
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t e = tid >> 3;  // one 8-lane rake group per edge
+    const int lane = (int)(tid & 7);
+    if (e >= n_edges) return;   // group-uniform
+    const float* s = starts + 7 * e;
+    const Rake rk = rake_setup(s, goals + 7 * e);
     const float pct = (float)(lane + 1) / 8.0f;  // validate.hh:11-21
+    float b[7];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) b[j] = __builtin_fmaf(v[j], pct, s[j]);  // validate.hh:37 (contracted)
-    const float div = (float)(8 * n);
-    float back[7];
-#pragma unroll
-    for (int j = 0; j < 7; ++j) back[j] = v[j] / div;  // validate.hh:50
-    bool valid = true;
-    for (int k = 0; k < n; ++k) {  // block 0, then n-1 back-steps (validate.hh:43-62)
-        if (k > 0) {
-#pragma unroll
-            for (int j = 0; j < 7; ++j) b[j] = b[j] - back[j];
-        }
-        if (!panda_fkcc<Grp8>(b[0], b[1], b[2], b[3], b[4], b[5], b[6], env, bx, by, bz)) {
-            valid = false;
-            break;
-        }
-    }
+    for (int j = 0; j < 7; ++j) b[j] = __builtin_fmaf(rk.v[j], pct, s[j]);  // validate.hh:37 (contracted)
+    const bool valid = panda_fkcc<Grp8>(b[0], b[1], b[2], b[3], b[4], b[5], b[6], env, bx, by, bz);
     if (lane == 0) {
         ok[e] = valid ? 1 : 0;
-        if (n_blocks) n_blocks[e] = n;
+        if (n_blocks) n_blocks[e] = rk.n;
+        cnt[e] = (valid && rk.n > 1) ? (uint32_t)(rk.n - 1) : 0u;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void scatter_items_kernel(const uint32_t* __restrict__ cnt,
+                                                               const uint32_t* __restrict__ off, size_t n_edges,
+                                                               uint32_t* __restrict__ item_edge)
+{
+    const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n_edges) return;
+    const uint32_t c = cnt[e], o = off[e];
+    for (uint32_t i = 0; i < c; ++i) item_edge[o + i] = (uint32_t)e;
+}
+
+__global__ __launch_bounds__(kBlock) void panda_validate_tail_kernel(
+    const float* __restrict__ starts, const float* __restrict__ goals, const uint32_t* __restrict__ item_edge,
+    const uint32_t* __restrict__ off, size_t n_items, EnvView env, float bx, float by, float bz,
+    uint8_t* __restrict__ ok)
+{
+    const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t it = tid >> 3;  // one 8-lane rake group per (edge, back-step)
+    const int lane = (int)(tid & 7);
+    if (it >= n_items) return;   // group-uniform
+    const uint32_t e = item_edge[it];
+    const int k = (int)(it - off[e]) + 1;  // back-step index 1 .. n_e - 1
+    const float* s = starts + 7 * (size_t)e;
+    const Rake rk = rake_setup(s, goals + 7 * (size_t)e);
+    const float pct = (float)(lane + 1) / 8.0f;
+    const float div = (float)(8 * (size_t)rk.n);
+    float b[7], back[7];
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+        b[j] = __builtin_fmaf(rk.v[j], pct, s[j]);
+        back[j] = rk.v[j] / div;  // validate.hh:50
+    }
+    for (int i = 0; i < k; ++i) {  // the reference's sequential subtraction chain, bit for bit
+#pragma unroll
+        for (int j = 0; j < 7; ++j) b[j] = b[j] - back[j];
+    }
+    const bool valid = panda_fkcc<Grp8>(b[0], b[1], b[2], b[3], b[4], b[5], b[6], env, bx, by, bz);
+    if (lane == 0 && !valid) ok[e] = 0;  // every writer stores 0: the race is benign
 }
 
 }  // namespace vgpu
@@ -110,14 +157,45 @@ hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, 
     return hipGetLastError();
 }
 
-hipError_t vgpu_launch_panda_validate(const float* starts, const float* goals, size_t n_edges, const EnvView* env,
-                                      float bx, float by, float bz, uint8_t* ok, int32_t* n_blocks, hipStream_t st)
+// Workspace for the two-phase validate: cnt[n_edges + 1], off[n_edges + 1], scan temp.
+size_t vgpu_validate_scan_bytes(size_t n_edges)
 {
-    if (n_edges == 0) return hipSuccess;
+    size_t tmp = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+                                           (int)(n_edges + 1));
+    return tmp;
+}
+
+hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goals, size_t n_edges,
+                                           const EnvView* env, float bx, float by, float bz, uint8_t* ok,
+                                           int32_t* n_blocks, uint32_t* cnt, uint32_t* off, void* scan_tmp,
+                                           size_t scan_bytes, hipStream_t st)
+{
     const size_t threads = n_edges * 8;
     const unsigned grid = (unsigned)((threads + vgpu::kBlock - 1) / vgpu::kBlock);
-    hipLaunchKernelGGL(vgpu::panda_validate_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, starts, goals, n_edges,
-                       *env, bx, by, bz, ok, n_blocks);
+    hipError_t err = hipMemsetAsync(cnt + n_edges, 0, sizeof(uint32_t), st);
+    if (err != hipSuccess) return err;
+    hipLaunchKernelGGL(vgpu::panda_validate_head_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, starts, goals,
+                       n_edges, *env, bx, by, bz, ok, n_blocks, cnt);
+    if ((err = hipGetLastError()) != hipSuccess) return err;
+    return hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, cnt, off, (int)(n_edges + 1), st);
+}
+
+hipError_t vgpu_launch_panda_validate_tail(const float* starts, const float* goals, size_t n_edges,
+                                           size_t n_items, const EnvView* env, float bx, float by, float bz,
+                                           uint8_t* ok, const uint32_t* cnt, const uint32_t* off,
+                                           uint32_t* item_edge, hipStream_t st)
+{
+    if (n_items == 0) return hipSuccess;
+    unsigned grid = (unsigned)((n_edges + vgpu::kBlock - 1) / vgpu::kBlock);
+    hipLaunchKernelGGL(vgpu::scatter_items_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, cnt, off, n_edges,
+                       item_edge);
+    hipError_t err = hipGetLastError();
+    if (err != hipSuccess) return err;
+    const size_t threads = n_items * 8;
+    grid = (unsigned)((threads + vgpu::kBlock - 1) / vgpu::kBlock);
+    hipLaunchKernelGGL(vgpu::panda_validate_tail_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, starts, goals,
+                       item_edge, off, n_items, *env, bx, by, bz, ok);
     return hipGetLastError();
 }
 

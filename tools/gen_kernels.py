@@ -213,16 +213,54 @@ class RobotGen:
         return "\n".join(hdr + E.lines + ["}", ""])
 
     def gen_fkcc(self) -> str:
+        """fkcc with lazily emitted frames (short live ranges -> fewer VGPRs) and the
+        reference's group semantics per check: a bounding test fires for the group if any
+        lane fires (Grp::any); the children's per-lane hits are OR-ed and reduced once, which
+        equals the reference's per-child `return false` (any lane, any child)."""
         E = Emitter()
         m = self.m
         dim = m["dimension"]
-        Q, P, R = self.frames_fk(E)
+        frames = m["frames"]
         spheres, bounding = m["spheres"], m["bounding"]
         links = [b["link"] for b in bounding]
+        Q, P, R = {}, {}, {}
+
+        def ensure_frame(f):
+            if f in Q:
+                return
+            fr = frames[f]
+            qf = tuple(SV.const(v) for v in fr["qf"])
+            if fr["parent"] < 0:
+                Q[f] = qf
+                P[f] = [SV.const(v) for v in fr["t"]]
+                return
+            p = fr["parent"]
+            ensure_R(p)
+            ident = list(fr["qf"]) == [1.0, 0.0, 0.0, 0.0]
+            A = Q[p] if ident else qmul(E, Q[p], qf)
+            d = fr["dof"]
+            if d >= 0:
+                h = E.tmp(f"q{d} * 0.5f")
+                c = E.tmp(f"vamp_cos({h.name})")
+                sn = E.tmp(f"vamp_sin({h.name})")
+                E.flops += 2 * 16
+                Q[f] = qmul(E, A, (c, SV.zero(), SV.zero(), sn))
+            else:
+                Q[f] = A
+            P[f] = xform(E, R[p], P[p], fr["t"])
+
+        def ensure_R(f):
+            ensure_frame(f)
+            if f not in R:
+                R[f] = qmat(E, Q[f])
+
         bc = {}
-        for b, bd in enumerate(bounding):
-            bc[b] = self.center(E, R, P, bd["frame"], bd["offset"])
-        fk_flops = E.flops
+
+        def bound_center(b):
+            if b not in bc:
+                ensure_R(bounding[b]["frame"])
+                bc[b] = self.center(E, R, P, bounding[b]["frame"], bounding[b]["offset"])
+            return bc[b]
 
         def world(c, base):
             if not base:
@@ -235,16 +273,23 @@ class RobotGen:
                 ck = m["env_checks"][o["index"]]
                 b = links.index(ck["link"])
                 bd = bounding[b]
-                w = world(bc[b], bd["base"])
-                E.raw(f"// env: {ck['link']} bounding sphere r={bd['radius']}")
-                E.raw(f"if (env_collide<Grp>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])})) {{")
-                E.indent += 1
                 for kid in ck["children"]:
-                    s = kid["sphere"]
-                    sp = spheres[s]
+                    ensure_R(spheres[kid["sphere"]]["frame"])
+                w = world(bound_center(b), bd["base"])
+                E.raw(f"// env: {ck['link']} bounding sphere r={bd['radius']} (+{len(ck['children'])} children)")
+                E.raw(f"if (Grp::any(env_lane<Grp>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])}))) {{")
+                E.indent += 1
+                E.raw("bool h = false;")
+                for kid in ck["children"]:
+                    sp = spheres[kid["sphere"]]
+                    E.raw("if (!h) {")
+                    E.indent += 1
                     c = self.center(E, R, P, sp["frame"], sp["offset"])
                     cw = world(c, kid["base"])
-                    E.raw(f"if (env_collide<Grp>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])})) return false;")
+                    E.raw(f"h = env_lane<Grp>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])});")
+                    E.indent -= 1
+                    E.raw("}")
+                E.raw("if (Grp::any(h)) return false;")
                 E.indent -= 1
                 E.raw("}")
             else:
@@ -253,35 +298,57 @@ class RobotGen:
                 def ent(e):
                     if "sphere" in e:
                         sp = spheres[e["sphere"]]
+                        ensure_R(sp["frame"])
                         return self.center(E, R, P, sp["frame"], sp["offset"]), sp["radius"]
                     bi = links.index(e["bound"])
-                    return bc[bi], bounding[bi]["radius"]
-
-                (ca, ra), (cb, rb) = ent(ck["a"]), ent(ck["b"])
-                E.raw(f"// self: {ck['links'][0]} vs {ck['links'][1]}")
-                E.raw(f"if (self_collide<Grp>({ca[0].expr()}, {ca[1].expr()}, {ca[2].expr()}, {flit(ra)}, "
-                      f"{cb[0].expr()}, {cb[1].expr()}, {cb[2].expr()}, {flit(rb)})) {{")
-                E.indent += 1
-                cache = {}
-
-                def sc(s):
-                    if s not in cache:
-                        sp = spheres[s]
-                        cache[s] = self.center(E, R, P, sp["frame"], sp["offset"])
-                    return cache[s]
+                    return bound_center(bi), bounding[bi]["radius"]
 
                 for sa, sb in ck["children"]:
-                    a, bb = sc(sa), sc(sb)
-                    E.raw(f"if (self_collide<Grp>({a[0].expr()}, {a[1].expr()}, {a[2].expr()}, "
-                          f"{flit(spheres[sa]['radius'])}, {bb[0].expr()}, {bb[1].expr()}, {bb[2].expr()}, "
-                          f"{flit(spheres[sb]['radius'])})) return false;")
+                    ensure_R(spheres[sa]["frame"])
+                    ensure_R(spheres[sb]["frame"])
+                (ca, ra), (cb, rb) = ent(ck["a"]), ent(ck["b"])
+                E.raw(f"// self: {ck['links'][0]} vs {ck['links'][1]} ({len(ck['children'])} children)")
+                E.raw(f"if (Grp::any(self_lane({ca[0].expr()}, {ca[1].expr()}, {ca[2].expr()}, {flit(ra)}, "
+                      f"{cb[0].expr()}, {cb[1].expr()}, {cb[2].expr()}, {flit(rb)}))) {{")
+                E.indent += 1
+                E.raw("uint32_t h = 0u;  // OR of the children's test-value bits: sign bit = any child fired")
+                # Evaluate the child pairs in chunks of CH distinct b-spheres: the chunk's b
+                # centres stay in registers while each a-sphere centre is recomputed per chunk,
+                # bounding the live set (the OR is order-independent).
+                CH = 6
+                pairs = ck["children"]
+                bs = sorted(set(p[1] for p in pairs))
+                nchunks = (len(bs) + CH - 1) // CH
+                for ci in range(nchunks):
+                    chunk = bs[ci * CH:(ci + 1) * CH]
+                    E.raw("{")
+                    E.indent += 1
+                    bcen = {}
+                    for sb in chunk:
+                        sp = spheres[sb]
+                        bcen[sb] = self.center(E, R, P, sp["frame"], sp["offset"])
+                    for sa in sorted(set(p[0] for p in pairs if p[1] in bcen)):
+                        sp = spheres[sa]
+                        a_ = self.center(E, R, P, sp["frame"], sp["offset"])
+                        for sb in chunk:
+                            if [sa, sb] not in pairs:
+                                continue
+                            b_ = bcen[sb]
+                            E.raw(f"h |= self_bits({a_[0].expr()}, {a_[1].expr()}, {a_[2].expr()}, "
+                                  f"{flit(spheres[sa]['radius'])}, {b_[0].expr()}, {b_[1].expr()}, {b_[2].expr()}, "
+                                  f"{flit(spheres[sb]['radius'])});")
+                    E.indent -= 1
+                    E.raw("}")
+                    if ci + 1 < nchunks:
+                        E.raw("if (Grp::any((h >> 31) != 0u)) return false;  // early exit (work only)")
+                E.raw("if (Grp::any((h >> 31) != 0u)) return false;")
                 E.indent -= 1
                 E.raw("}")
         E.raw("return true;")
         hdr = [
             f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
-            f"// FK + bounding centres: {fk_flops} float ops; checks follow the reference's",
-            "// hierarchy (link-bounding sphere first, children only on a group hit).",
+            "// FK emitted lazily in check order; checks follow the reference hierarchy",
+            "// (link-bounding sphere first, children only when the group's bounding test fires).",
             "template <class Grp>",
             f"__device__ __forceinline__ bool {self.name}_fkcc(",
             "    " + ", ".join(f"float q{i}" for i in range(dim)) + ",",
