@@ -139,7 +139,8 @@ struct vgpu_env {
     bool dirty = true;
     float* dev = nullptr;
     size_t dev_floats = 0;
-    int n_obs = 0;
+    size_t off[OBS_TYPES] = {0, 0, 0, 0, 0};
+    int cnt[OBS_TYPES] = {0, 0, 0, 0, 0};
 };
 
 #define HIPCHK(ctx, expr)                                                                          \
@@ -407,36 +408,47 @@ extern "C" int vgpu_env_counts(const vgpu_env* e, int32_t counts[5])
     return VGPU_OK;
 }
 
-// One list of all obstacles sorted by min_distance (see EnvView in vgpu_device.hh): per type
-// this is the reference's sort (environment.hh:40-66); merging the types is exact because
-// every type's loop evaluates exactly the obstacles with min_distance below the group's
-// largest max_extent.
+template <size_t W>
+static void sort_md(std::vector<std::array<float, W>>& v)  // environment.hh:40-66
+{
+    std::stable_sort(v.begin(), v.end(), [](const auto& a, const auto& b) { return a[W - 1] < b[W - 1]; });
+}
+
+// Device layout of EnvView (vgpu_device.hh): per type, records sorted by min_distance
+// (environment.hh:40-66) followed by kObsPad sentinels with min_distance = +inf.
 extern "C" int vgpu_env_upload(vgpu_env* e)
 {
     if (!e) return VGPU_ERR_INVALID_ARG;
     vgpu_ctx* c = e->ctx;
     if (!e->dirty && e->dev) return VGPU_OK;
-    struct Rec {
-        float md;
-        std::array<float, kObsStride> r;
+    sort_md(e->spheres);
+    sort_md(e->capsules);
+    sort_md(e->zcapsules);
+    sort_md(e->cuboids);
+    sort_md(e->zcuboids);
+    std::vector<float> blob;
+    auto put = [&](auto& v, int type, int np) {
+        const int S = kObsStride[type];
+        e->off[type] = blob.size();
+        e->cnt[type] = (int)v.size();
+        for (auto& row : v) {
+            const size_t base = blob.size();
+            blob.resize(base + S, 0.0f);
+            blob[base] = row[np];  // min_distance is the last field of the host row
+            for (int i = 0; i < np; ++i) blob[base + 1 + i] = row[i];
+        }
+        for (int k = 0; k < kObsPad; ++k) {
+            const size_t base = blob.size();
+            blob.resize(base + S, 0.0f);
+            blob[base] = __builtin_inff();
+        }
+        while (blob.size() % 16) blob.push_back(0.0f);
     };
-    std::vector<Rec> recs;
-    auto add = [&](int type, float md, const float* p, int np) {
-        Rec rec{md, {}};
-        int t = type;
-        std::memcpy(&rec.r[0], &t, 4);
-        rec.r[1] = md;
-        for (int i = 0; i < np; ++i) rec.r[2 + i] = p[i];
-        recs.push_back(rec);
-    };
-    for (auto& o : e->spheres) add(OBS_SPHERE, o[4], o.data(), 4);
-    for (auto& o : e->capsules) add(OBS_CAPSULE, o[8], o.data(), 8);
-    for (auto& o : e->zcapsules) add(OBS_ZCAPSULE, o[8], o.data(), 8);
-    for (auto& o : e->cuboids) add(OBS_CUBOID, o[15], o.data(), 15);
-    for (auto& o : e->zcuboids) add(OBS_ZCUBOID, o[15], o.data(), 15);
-    std::stable_sort(recs.begin(), recs.end(), [](const Rec& a, const Rec& b) { return a.md < b.md; });
-    std::vector<float> blob(std::max<size_t>(recs.size(), 1) * kObsStride, 0.0f);
-    for (size_t i = 0; i < recs.size(); ++i) std::copy(recs[i].r.begin(), recs[i].r.end(), &blob[i * kObsStride]);
+    put(e->spheres, OBS_SPHERE, 4);
+    put(e->capsules, OBS_CAPSULE, 8);
+    put(e->zcapsules, OBS_ZCAPSULE, 8);
+    put(e->cuboids, OBS_CUBOID, 15);
+    put(e->zcuboids, OBS_ZCUBOID, 15);
     HIPCHK(c, hipSetDevice(c->device));
     if (blob.size() > e->dev_floats) {
         if (e->dev) {
@@ -449,7 +461,6 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     }
     HIPCHK(c, hipMemcpyAsync(e->dev, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));  // blob is a host temporary
-    e->n_obs = (int)recs.size();
     e->dirty = false;
     return VGPU_OK;
 }
@@ -457,8 +468,10 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
 static EnvView make_view(const vgpu_env* e)
 {
     EnvView v{};
-    v.obs = (const VGPU_CONST float*)e->dev;
-    v.n_obs = e->n_obs;
+    for (int t = 0; t < OBS_TYPES; ++t) {
+        v.obs[t] = (const VGPU_CONST float*)(e->dev + e->off[t]);
+        v.n[t] = e->cnt[t];
+    }
     v.lut = e->ctx->lut_dev;
     v.kbits = e->ctx->kbits;
     return v;

@@ -85,23 +85,21 @@ __device__ __forceinline__ float vamp_cos(float x)
 }
 
 // ---- environment view ----------------------------------------------------------------------
-// All obstacles of collision::Environment<float> in ONE list sorted ascending by
-// min_distance, one 32-float (128 B) record each:
-//   [0] type (int bits: 0 sphere, 1 capsule, 2 z-capsule, 3 cuboid, 4 z-cuboid)  [1] min_distance
-//   sphere   [2..5]  x y z r
-//   capsule  [2..9]  x1 y1 z1 xv yv zv r rdv                     (z-capsule: same layout)
-//   cuboid   [2..16] x y z a1x a1y a1z a2x a2y a2z a3x a3y a3z r1 r2 r3   (z-cuboid: same)
-// The reference keeps one sorted list per type and stops each type's loop at its own first
-// all-lanes-culled obstacle (validity.hh:61-127); that stop is monotone in min_distance, so
-// per type it evaluates exactly {j : md_j < max_extent_max} and the union over types is the
-// same prefix of the merged list (see env_lane).
-enum : int { OBS_SPHERE = 0, OBS_CAPSULE = 1, OBS_ZCAPSULE = 2, OBS_CUBOID = 3, OBS_ZCUBOID = 4 };
-constexpr int kObsStride = 32;
+// collision::Environment<float> on the device: one section per obstacle type, each sorted
+// ascending by min_distance (environment.hh:40-66) and terminated by kObsPad sentinel records
+// whose min_distance is +inf (never evaluated; lets the loops prefetch past the end).
+// Records (float32, field 0 = min_distance):
+//   sphere   stride  8: md x y z r
+//   capsule  stride 16: md x1 y1 z1 xv yv zv r rdv            (z-capsule: same)
+//   cuboid   stride 16: md x y z a1x a1y a1z a2x a2y a2z a3x a3y a3z r1 r2 r3   (z-cuboid: same)
+enum : int { OBS_SPHERE = 0, OBS_CAPSULE = 1, OBS_ZCAPSULE = 2, OBS_CUBOID = 3, OBS_ZCUBOID = 4, OBS_TYPES = 5 };
+constexpr int kObsStride[OBS_TYPES] = {8, 16, 16, 16, 16};
+constexpr int kObsPad = 4;
 
 struct EnvView {
-    const VGPU_CONST float* obs;
+    const VGPU_CONST float* obs[OBS_TYPES];
     const uint32_t* lut;  // host rsqrt table, 2 << kbits entries
-    int n_obs;
+    int n[OBS_TYPES];
     int kbits;
 };
 
@@ -155,6 +153,28 @@ __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 // maximum of max_extent (a NaN/inf extent -- 0 or denormal |c|^2 -- never culls: +inf).  The
 // `return true` only ends work early: a lane stops at its own first hit, which leaves the
 // group OR unchanged.
+// One obstacle type: evaluates records while md < emax (this lane's group prefix), two per
+// iteration, the next pair's scalar loads issued before the current pair is tested.  The
+// body is branch-free per lane; the loop exits when no lane of the wave has anything left.
+template <int TYPE, class TestFn>
+__device__ __forceinline__ void scan_type(const VGPU_CONST float* o, float emax, bool& hit, TestFn test)
+{
+    constexpr int S = kObsStride[TYPE];
+    float md0 = o[0], md1 = o[S];
+    for (;;) {
+        const bool live0 = (md0 < emax) && !hit;
+        if (!__any(live0)) break;  // md is sorted: live1 implies live0
+        const float nmd0 = o[2 * S], nmd1 = o[3 * S];  // prefetch (sentinel-padded)
+        const bool live1 = (md1 < emax);
+        const float v0 = test(o);
+        const float v1 = test(o + S);
+        hit = hit || (live0 && signbit_f(v0)) || (live0 && live1 && signbit_f(v1));
+        o += 2 * S;
+        md0 = nmd0;
+        md1 = nmd1;
+    }
+}
+
 template <class Grp>
 __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, float z, float r)
 {
@@ -164,46 +184,49 @@ __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, f
     if (dexp == 0u || dexp == 0x7F800000u || me != me) me = __builtin_inff();
     const float emax = Grp::max(me);
     const float rsq = r * r;
+    bool hit = false;
 
-    for (int j = 0; j < env.n_obs; ++j) {
-        const VGPU_CONST float* o = env.obs + kObsStride * j;
-        if (!(o[1] < emax)) break;  // every remaining obstacle is culled for the whole group
-        const int type = __float_as_int(o[0]);
-        float v;
-        if (type == OBS_SPHERE) {  // sphere_sphere.hh:10-22
-            v = sphere_sphere(o[2], o[3], o[4], o[5], x, y, z, r);
-        } else if (type == OBS_CAPSULE) {  // sphere_capsule.hh:9-22
-            const float dot = dot3(x - o[2], y - o[3], z - o[4], o[5], o[6], o[7]);
-            const float cdf = fminf(fmaxf(dot * o[9], 0.0f), 1.0f);
-            const float px = __builtin_fmaf(o[5], cdf, o[2]);
-            const float py = __builtin_fmaf(o[6], cdf, o[3]);
-            const float pz = __builtin_fmaf(o[7], cdf, o[4]);
+    if (env.n[OBS_SPHERE])  // sphere_sphere.hh:10-22
+        scan_type<OBS_SPHERE>(env.obs[OBS_SPHERE], emax, hit, [&](const VGPU_CONST float* o) {
+            return sphere_sphere(o[1], o[2], o[3], o[4], x, y, z, r);
+        });
+    if (env.n[OBS_CAPSULE])  // sphere_capsule.hh:9-22
+        scan_type<OBS_CAPSULE>(env.obs[OBS_CAPSULE], emax, hit, [&](const VGPU_CONST float* o) {
+            const float dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
+            const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
+            const float px = __builtin_fmaf(o[4], cdf, o[1]);
+            const float py = __builtin_fmaf(o[5], cdf, o[2]);
+            const float pz = __builtin_fmaf(o[6], cdf, o[3]);
             const float xs = x - px, ys = y - py, zs = z - pz;
-            const float rs = r + o[8];
-            v = __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
-        } else if (type == OBS_ZCAPSULE) {  // sphere_capsule.hh:30-43
-            const float dot = (z - o[4]) * o[7];
-            const float cdf = fminf(fmaxf(dot * o[9], 0.0f), 1.0f);
-            const float pz = __builtin_fmaf(o[7], cdf, o[4]);
-            const float xs = x - o[2], ys = y - o[3], zs = z - pz;
-            const float rs = r + o[8];
-            v = __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
-        } else if (type == OBS_CUBOID) {  // sphere_cuboid.hh:9-27
-            const float xs = x - o[2], ys = y - o[3], zs = z - o[4];
-            const float a1 = max0(__builtin_fabsf(dot3(o[5], o[6], o[7], xs, ys, zs)) - o[14]);
-            const float a2 = max0(__builtin_fabsf(dot3(o[8], o[9], o[10], xs, ys, zs)) - o[15]);
-            const float a3 = max0(__builtin_fabsf(dot3(o[11], o[12], o[13], xs, ys, zs)) - o[16]);
-            v = dot3(a1, a2, a3, a1, a2, a3) - rsq;
-        } else {  // OBS_ZCUBOID, sphere_cuboid.hh:35-52
-            const float xs = x - o[2], ys = y - o[3], zs = z - o[4];
-            const float a1 = max0(__builtin_fabsf(dot2(o[5], o[6], xs, ys)) - o[14]);
-            const float a2 = max0(__builtin_fabsf(dot2(o[8], o[9], xs, ys)) - o[15]);
-            const float a3 = max0(__builtin_fabsf(zs) - o[16]);
-            v = dot3(a1, a2, a3, a1, a2, a3) - rsq;
-        }
-        if (signbit_f(v)) return true;  // this lane hit: the group result is already true
-    }
-    return false;
+            const float rs = r + o[7];
+            return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
+        });
+    if (env.n[OBS_ZCAPSULE])  // sphere_capsule.hh:30-43
+        scan_type<OBS_ZCAPSULE>(env.obs[OBS_ZCAPSULE], emax, hit, [&](const VGPU_CONST float* o) {
+            const float dot = (z - o[3]) * o[6];
+            const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
+            const float pz = __builtin_fmaf(o[6], cdf, o[3]);
+            const float xs = x - o[1], ys = y - o[2], zs = z - pz;
+            const float rs = r + o[7];
+            return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
+        });
+    if (env.n[OBS_CUBOID])  // sphere_cuboid.hh:9-27
+        scan_type<OBS_CUBOID>(env.obs[OBS_CUBOID], emax, hit, [&](const VGPU_CONST float* o) {
+            const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
+            const float a1 = max0(__builtin_fabsf(dot3(o[4], o[5], o[6], xs, ys, zs)) - o[13]);
+            const float a2 = max0(__builtin_fabsf(dot3(o[7], o[8], o[9], xs, ys, zs)) - o[14]);
+            const float a3 = max0(__builtin_fabsf(dot3(o[10], o[11], o[12], xs, ys, zs)) - o[15]);
+            return dot3(a1, a2, a3, a1, a2, a3) - rsq;
+        });
+    if (env.n[OBS_ZCUBOID])  // sphere_cuboid.hh:35-52
+        scan_type<OBS_ZCUBOID>(env.obs[OBS_ZCUBOID], emax, hit, [&](const VGPU_CONST float* o) {
+            const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
+            const float a1 = max0(__builtin_fabsf(dot2(o[4], o[5], xs, ys)) - o[13]);
+            const float a2 = max0(__builtin_fabsf(dot2(o[7], o[8], xs, ys)) - o[14]);
+            const float a3 = max0(__builtin_fabsf(zs) - o[15]);
+            return dot3(a1, a2, a3, a1, a2, a3) - rsq;
+        });
+    return hit;
 }
 
 // sphere_sphere_self_collision (collision/validity.hh:13-44)
