@@ -36,6 +36,8 @@ __device__ __forceinline__ float dpp_f(float v)
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
 }
 
+__device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b ? a : b; }
+
 struct Grp1 {
     static constexpr int G = 1;
     __device__ static __forceinline__ bool any(bool p) { return p; }
@@ -52,12 +54,15 @@ struct Grp8 {
         x |= dpp_i<0x141>(x);  // row_half_mirror
         return x != 0;
     }
+    // max of NON-NEGATIVE floats (max_extent = |c| + r > 0, or +inf): their bit patterns
+    // order like the values, so an unsigned max folds into one v_max_u32_dpp per step.
     __device__ static __forceinline__ float max(float v)
     {
-        v = fmaxf(v, dpp_f<0xB1>(v));
-        v = fmaxf(v, dpp_f<0x4E>(v));
-        v = fmaxf(v, dpp_f<0x141>(v));
-        return v;
+        uint32_t u = __float_as_uint(v);
+        u = umax(u, (uint32_t)dpp_i<0xB1>((int)u));
+        u = umax(u, (uint32_t)dpp_i<0x4E>((int)u));
+        u = umax(u, (uint32_t)dpp_i<0x141>((int)u));
+        return __uint_as_float(u);
     }
 };
 

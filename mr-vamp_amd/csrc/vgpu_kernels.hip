@@ -1,8 +1,6 @@
 // vgpu_kernels.hip -- gfx950 kernels of the motion-validation rake.
 //
-// Per robot (Panda today):
-//   sphere_fk      one lane per configuration, SoA stores: the HBM-bound FK stream
-//                  (reference robots/panda/fk.hh:104-1333 sphere_fk);
+// Per robot (Panda today; sphere_fk lives in vgpu_fk.hip):
 //   fkcc           one lane per configuration (rake group G = 1 == a configuration broadcast
 //                  to all 8 reference lanes): per-configuration validity mask
 //                  (fk.hh:1335-6276 interleaved_sphere_fk);
@@ -29,19 +27,12 @@
 
 namespace vgpu {
 
+#ifndef VGPU_WAVES_PER_EU
+#define VGPU_WAVES_PER_EU 7  // A/B on MI355X: 4 -> 6.84 ms, 6 -> 5.96, 7 -> 5.84, 8 -> 5.96 (validate, 1M edges)
+#endif
 constexpr int kBlock = 256;
 
-__global__ __launch_bounds__(kBlock) void panda_sphere_fk_kernel(const float* __restrict__ q, size_t n, float bx,
-                                                                 float by, float bz, float* __restrict__ out,
-                                                                 size_t ld)
-{
-    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const float* qi = q + 7 * i;
-    panda_sphere_fk_store(qi[0], qi[1], qi[2], qi[3], qi[4], qi[5], qi[6], bx, by, bz, out + i, ld);
-}
-
-__global__ __launch_bounds__(kBlock) void panda_fkcc_kernel(const float* __restrict__ q, size_t n, EnvView env,
+__global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_fkcc_kernel(const float* __restrict__ q, size_t n, EnvView env,
                                                             float bx, float by, float bz,
                                                             uint8_t* __restrict__ valid)
 {
@@ -72,7 +63,7 @@ __device__ __forceinline__ Rake rake_setup(const float* __restrict__ s, const fl
     return r;
 }
 
-__global__ __launch_bounds__(kBlock) void panda_validate_head_kernel(
+__global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_validate_head_kernel(
     const float* __restrict__ starts, const float* __restrict__ goals, size_t n_edges, EnvView env, float bx,
     float by, float bz, uint8_t* __restrict__ ok, int32_t* __restrict__ n_blocks, uint32_t* __restrict__ cnt)
 {
@@ -104,7 +95,7 @@ __global__ __launch_bounds__(kBlock) void scatter_items_kernel(const uint32_t* _
     for (uint32_t i = 0; i < c; ++i) item_edge[o + i] = (uint32_t)e;
 }
 
-__global__ __launch_bounds__(kBlock) void panda_validate_tail_kernel(
+__global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_validate_tail_kernel(
     const float* __restrict__ starts, const float* __restrict__ goals, const uint32_t* __restrict__ item_edge,
     const uint32_t* __restrict__ off, size_t n_items, EnvView env, float bx, float by, float bz,
     uint8_t* __restrict__ ok)
@@ -136,16 +127,6 @@ __global__ __launch_bounds__(kBlock) void panda_validate_tail_kernel(
 }  // namespace vgpu
 
 extern "C" {
-
-hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float by, float bz, float* out,
-                                       size_t ld, hipStream_t st)
-{
-    if (n == 0) return hipSuccess;
-    const unsigned grid = (unsigned)((n + vgpu::kBlock - 1) / vgpu::kBlock);
-    hipLaunchKernelGGL(vgpu::panda_sphere_fk_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, q, n, bx, by, bz, out,
-                       ld);
-    return hipGetLastError();
-}
 
 hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, float bx, float by, float bz,
                                   uint8_t* valid, hipStream_t st)
