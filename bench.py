@@ -49,7 +49,8 @@ def parse():
     ap.add_argument("--edges", type=int, default=1 << 20, help="edges per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
-    ap.add_argument("--fk-leg", action="store_true", default=True)
+    ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
 
 
@@ -117,28 +118,30 @@ def cpu_model():
     return "unknown"
 
 
-def algorithmic_flops_per_edge(starts, goals, n=256):
-    """Executed float ops per edge under reference semantics, counted by the instrumented
-    restatement (oracle/vamp_oracle.c vo_stats.flops) on a sample of the bench's edges."""
+def algorithmic_flops(starts, goals, n=512):
+    """Executed float ops per edge under reference semantics (validate_motion with early
+    exit), counted by the instrumented restatement (oracle/vamp_oracle.c vo_stats.flops) on a
+    sample of the bench's own edges; split into the first rake block (head kernel) and the
+    back-steps (tail kernel).  Returns (head_per_edge, tail_per_edge)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import ctypes as C
-
     import oracle_py as op
 
     op.build()
     env = op.Env()
     for c in CAGE:
         env.add_sphere(c, np.float32(0.2))
-    ce = env.c()
-    tot = 0.0
-    for i in range(n):
-        st = op.VoStats(np.inf, np.inf, 0.0)
-        nn = C.c_int()
-        s = np.ascontiguousarray(starts[i], np.float32)
-        g = np.ascontiguousarray(goals[i], np.float32)
-        op.lib().vo_panda_validate_motion(C.byref(ce), op.fp(s), op.fp(g), 0, 0, 0, C.byref(nn), C.byref(st))
-        tot += st.flops
-    return tot / n
+    h, t = op.validate_flops(env, starts[:n], goals[:n])
+    return float(h.mean()), float(t.mean())
+
+
+def traffic_record(path):
+    """HBM bytes per head-kernel launch from a rocprofv3 --pmc pass of this code (written by
+    tools/profile_round.sh); None when that file is absent."""
+    try:
+        with open(path) as f:
+            return json.load(f)
+    except (OSError, ValueError):
+        return None
 
 
 def main():
@@ -231,11 +234,25 @@ def main():
                   "frac": gbs / HBM_PEAK_GBS, "bytes_per_config": 736}
         del q, out
 
+    # per-phase kernel time (HIP events inside the library, separate untimed pass)
+    ctx.set_profiling(True)
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    phases = ctx.phase_times()
+    ctx.set_profiling(False)
+    calls = max(1, phases["calls"])
+    head_ms = phases["head_ms"] / calls
+    tail_ms = phases["tail_ms"] / calls
+    scan_ms = phases["scan_ms"] / calls
+
     if rank == 0:
         s_np = starts[: 1 << 17].cpu().numpy()
         g_np = goals[: 1 << 17].cpu().numpy()
-        flops_edge = algorithmic_flops_per_edge(s_np, g_np)
-        achieved = flops_edge * E / (kern_ms * 1e-3) / 1e12
+        f_head, f_tail = algorithmic_flops(s_np, g_np)
+        achieved = f_head * E / (head_ms * 1e-3) / 1e12
+        achieved_step = (f_head + f_tail) * E / (kern_ms * 1e-3) / 1e12
+        tr = traffic_record(a.traffic_json)
         cpu = None
         if not a.no_cpu and world == 1:
             s_cpu = starts[: 1 << 20].cpu().numpy()
@@ -265,16 +282,30 @@ def main():
                 "parallelism": f"dp{world} (independent edge shards, no collective)",
             },
             "roofline": {
-                "kernel": "panda_validate_kernel",
+                "kernel": "panda_validate_head_kernel",
                 "bound": "valu",
                 "achieved": achieved,
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved / FP32_PEAK_TFLOPS,
-                "traffic": None,
-                "algorithmic_flops_per_edge": flops_edge,
-                "kernel_ms": kern_ms,
-                "hbm_frac": EDGE_BYTES * E / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "traffic": (tr or {}).get("head_bytes_per_launch"),
+                "algorithmic_flops_per_launch": f_head * E,
+                "algorithmic_flops_per_edge": f_head,
+                "kernel_ms": head_ms,
+                "algorithmic_bytes_per_launch": EDGE_BYTES * E,
+                "hbm_frac": EDGE_BYTES * E / (head_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "traffic_source": (tr or {}).get("source"),
+            },
+            "roofline_step": {
+                "kernels": "head + scan + scatter + tail (one vgpu_validate_motions call)",
+                "bound": "valu",
+                "achieved": achieved_step,
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved_step / FP32_PEAK_TFLOPS,
+                "step_kernel_ms": kern_ms,
+                "phase_ms": {"head": head_ms, "scan_and_count": scan_ms, "tail": tail_ms},
+                "algorithmic_flops_per_edge": f_head + f_tail,
             },
             "roofline_hbm_fk": fk_leg,
             "cpu_baseline": cpu,

@@ -59,6 +59,12 @@ const char *vgpu_last_error(const vgpu_ctx *ctx);
  * the context's own stream. */
 int vgpu_ctx_set_stream(vgpu_ctx *ctx, void *hip_stream);
 int vgpu_sync(vgpu_ctx *ctx);
+/* Per-phase kernel timing of vgpu_validate_motions (HIP events on the context stream; adds
+ * one event synchronisation per call while enabled).  vgpu_phase_times returns and resets the
+ * accumulated milliseconds: [0] head (first rake block), [1] scan + item count read-back,
+ * [2] scatter + tail (back-step blocks), [3] number of calls. */
+int vgpu_ctx_set_profiling(vgpu_ctx *ctx, int enable);
+int vgpu_phase_times(vgpu_ctx *ctx, float ms[4]);
 /* rsqrt table in use: kbits and the 2 << kbits entries (host copy).  Replacing it is for
  * testing cross-host parity only. */
 int vgpu_rsqrt_table(const vgpu_ctx *ctx, int *kbits, const uint32_t **table);

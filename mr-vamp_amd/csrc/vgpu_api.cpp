@@ -25,10 +25,11 @@ hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float
 hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, float bx, float by, float bz,
                                   uint8_t* valid, hipStream_t st);
 size_t vgpu_validate_scan_bytes(size_t n_edges);
+hipError_t vgpu_launch_scan(const uint32_t* cnt, uint32_t* off, size_t n_edges, void* scan_tmp, size_t scan_bytes,
+                            hipStream_t st);
 hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goals, size_t n_edges,
                                            const EnvView* env, float bx, float by, float bz, uint8_t* ok,
-                                           int32_t* n_blocks, uint32_t* cnt, uint32_t* off, void* scan_tmp,
-                                           size_t scan_bytes, hipStream_t st);
+                                           int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
 hipError_t vgpu_launch_panda_validate_tail(const float* starts, const float* goals, size_t n_edges,
                                            size_t n_items, const EnvView* env, float bx, float by, float bz,
                                            uint8_t* ok, const uint32_t* cnt, const uint32_t* off,
@@ -129,6 +130,10 @@ struct vgpu_ctx {
     uint32_t* items = nullptr;
     size_t items_cap = 0;
     uint32_t* total_host = nullptr;
+    // optional phase timing
+    bool prof = false;
+    hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    float acc[4] = {0, 0, 0, 0};
 };
 
 struct vgpu_env {
@@ -204,6 +209,8 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->ws) (void)hipFree(c->ws);
     if (c->items) (void)hipFree(c->items);
     if (c->total_host) (void)hipHostFree(c->total_host);
+    for (auto& ev : c->ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -222,6 +229,27 @@ extern "C" int vgpu_sync(vgpu_ctx* c)
     if (!c) return VGPU_ERR_INVALID_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_ctx_set_profiling(vgpu_ctx* c, int enable)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    for (auto& ev : c->ev)
+        if (!ev) HIPCHK(c, hipEventCreate(&ev));
+    c->prof = enable != 0;
+    for (float& a : c->acc) a = 0.0f;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_phase_times(vgpu_ctx* c, float ms[4])
+{
+    if (!c || !ms) return VGPU_ERR_INVALID_ARG;
+    for (int i = 0; i < 4; ++i) {
+        ms[i] = c->acc[i];
+        c->acc[i] = 0.0f;
+    }
     return VGPU_OK;
 }
 
@@ -565,8 +593,11 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     void* tmp;
     size_t tmp_bytes;
     if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
-    HIPCHK(c, vgpu_launch_panda_validate_head(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, cnt, off,
-                                              tmp, tmp_bytes, c->cur));
+    if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
+    HIPCHK(c, vgpu_launch_panda_validate_head(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, cnt,
+                                              c->cur));
+    if (c->prof) HIPCHK(c, hipEventRecord(c->ev[1], c->cur));
+    HIPCHK(c, vgpu_launch_scan(cnt, off, n_edges, tmp, tmp_bytes, c->cur));
     // number of back-step work items: one D2H word (the item buffer is sized from it)
     HIPCHK(c, hipMemcpyAsync(c->total_host, off + n_edges, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
@@ -578,8 +609,21 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
         HIPCHK(c, hipMalloc(&c->items, cap * sizeof(uint32_t)));
         c->items_cap = cap;
     }
+    if (c->prof) HIPCHK(c, hipEventRecord(c->ev[2], c->cur));
     HIPCHK(c, vgpu_launch_panda_validate_tail(starts, goals, n_edges, n_items, &v, b[0], b[1], b[2], ok, cnt, off,
                                               c->items, c->cur));
+    if (c->prof) {
+        HIPCHK(c, hipEventRecord(c->ev[3], c->cur));
+        HIPCHK(c, hipEventSynchronize(c->ev[3]));
+        float t0 = 0, t1 = 0, t2 = 0;
+        HIPCHK(c, hipEventElapsedTime(&t0, c->ev[0], c->ev[1]));
+        HIPCHK(c, hipEventElapsedTime(&t1, c->ev[1], c->ev[2]));
+        HIPCHK(c, hipEventElapsedTime(&t2, c->ev[2], c->ev[3]));
+        c->acc[0] += t0;  // head kernel (one memset + panda_validate_head_kernel)
+        c->acc[1] += t1;  // scan + the 4-byte D2H of the item count
+        c->acc[2] += t2;  // scatter + panda_validate_tail_kernel
+        c->acc[3] += 1.0f;
+    }
     return VGPU_OK;
 }
 

@@ -147,10 +147,15 @@ size_t vgpu_validate_scan_bytes(size_t n_edges)
     return tmp;
 }
 
+hipError_t vgpu_launch_scan(const uint32_t* cnt, uint32_t* off, size_t n_edges, void* scan_tmp, size_t scan_bytes,
+                            hipStream_t st)
+{
+    return hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, cnt, off, (int)(n_edges + 1), st);
+}
+
 hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goals, size_t n_edges,
                                            const EnvView* env, float bx, float by, float bz, uint8_t* ok,
-                                           int32_t* n_blocks, uint32_t* cnt, uint32_t* off, void* scan_tmp,
-                                           size_t scan_bytes, hipStream_t st)
+                                           int32_t* n_blocks, uint32_t* cnt, hipStream_t st)
 {
     const size_t threads = n_edges * 8;
     const unsigned grid = (unsigned)((threads + vgpu::kBlock - 1) / vgpu::kBlock);
@@ -158,8 +163,7 @@ hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goa
     if (err != hipSuccess) return err;
     hipLaunchKernelGGL(vgpu::panda_validate_head_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, starts, goals,
                        n_edges, *env, bx, by, bz, ok, n_blocks, cnt);
-    if ((err = hipGetLastError()) != hipSuccess) return err;
-    return hipcub::DeviceScan::ExclusiveSum(scan_tmp, scan_bytes, cnt, off, (int)(n_edges + 1), st);
+    return hipGetLastError();
 }
 
 hipError_t vgpu_launch_panda_validate_tail(const float* starts, const float* goals, size_t n_edges,

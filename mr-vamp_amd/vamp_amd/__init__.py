@@ -62,6 +62,15 @@ class Context:
     def set_stream(self, stream_handle: Optional[int]):
         check(load().vgpu_ctx_set_stream(self.h, C.c_void_p(stream_handle or 0)), self.h)
 
+    def set_profiling(self, enable: bool):
+        check(load().vgpu_ctx_set_profiling(self.h, int(bool(enable))), self.h)
+
+    def phase_times(self) -> dict:
+        """Accumulated ms of vgpu_validate_motions phases since the last call (then reset)."""
+        out = (C.c_float * 4)()
+        check(load().vgpu_phase_times(self.h, out), self.h)
+        return {"head_ms": out[0], "scan_ms": out[1], "tail_ms": out[2], "calls": int(out[3])}
+
     def rsqrt_table(self) -> Tuple[np.ndarray, int]:
         k = C.c_int()
         p = _lib.U32P()

@@ -35,6 +35,8 @@ SIGNATURES = {
     "vgpu_last_error": (C.c_char_p, [VP]),
     "vgpu_ctx_set_stream": (C.c_int, [VP, VP]),
     "vgpu_sync": (C.c_int, [VP]),
+    "vgpu_ctx_set_profiling": (C.c_int, [VP, C.c_int]),
+    "vgpu_phase_times": (C.c_int, [VP, F32P]),
     "vgpu_rsqrt_table": (C.c_int, [VP, C.POINTER(C.c_int), C.POINTER(U32P)]),
     "vgpu_rsqrt_table_set": (C.c_int, [VP, U32P, C.c_int]),
     "vgpu_env_create": (C.c_int, [VP, C.POINTER(VP)]),

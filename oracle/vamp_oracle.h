@@ -70,6 +70,10 @@ int vo_panda_fkcc_block(const vo_env *env, const float *q, int G, int bx100, int
 int vo_panda_validate_motion(const vo_env *env, const float start[7], const float goal[7],
                              int bx100, int by100, int bz100, int *n_out, vo_stats *stats);
 
+/* the same, with the first rake block's work counted in *head and the back-steps in *tail */
+int vo_panda_validate_motion_split(const vo_env *env, const float start[7], const float goal[7], int bx100,
+                                   int by100, int bz100, int *n_out, vo_stats *head, vo_stats *tail);
+
 /* batched, multi-threaded drivers (CPU baseline / fixture generation) */
 void vo_panda_fkcc_configs(const vo_env *env, const float *q /*[N][7]*/, size_t n, int bx100,
                            int by100, int bz100, uint8_t *valid, int threads);

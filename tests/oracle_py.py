@@ -72,6 +72,9 @@ def lib():
         L.vo_panda_validate_motion.restype = C.c_int
         L.vo_panda_validate_motion.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_int, C.c_int, C.c_int,
                                                C.POINTER(C.c_int), C.POINTER(VoStats)]
+        L.vo_panda_validate_motion_split.restype = C.c_int
+        L.vo_panda_validate_motion_split.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_int, C.c_int, C.c_int,
+                                                     C.POINTER(C.c_int), C.POINTER(VoStats), C.POINTER(VoStats)]
         L.vo_panda_fkcc_configs.argtypes = [C.POINTER(VoEnv), F32P, C.c_size_t, C.c_int, C.c_int, C.c_int, U8P,
                                             C.c_int]
         L.vo_panda_validate_motions.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_size_t, C.c_int, C.c_int,
@@ -219,3 +222,21 @@ def scale(q):
     for i in range(q.shape[0]):
         lib().vo_panda_scale(fp(q[i]))
     return q
+
+
+def validate_flops(env: Env, starts, goals, base100=(0, 0, 0)):
+    """Executed float ops of validate_motion per edge (reference semantics, early exit),
+    split into the first rake block and the back-steps."""
+    ce = env.c()
+    L = lib()
+    head = np.zeros(len(starts))
+    tail = np.zeros(len(starts))
+    for i in range(len(starts)):
+        h = VoStats(np.inf, np.inf, 0.0)
+        t = VoStats(np.inf, np.inf, 0.0)
+        n = C.c_int()
+        s = np.ascontiguousarray(starts[i], np.float32)
+        g = np.ascontiguousarray(goals[i], np.float32)
+        L.vo_panda_validate_motion_split(C.byref(ce), fp(s), fp(g), *base100, C.byref(n), C.byref(h), C.byref(t))
+        head[i], tail[i] = h.flops, t.flops
+    return head, tail
