@@ -1,0 +1,215 @@
+// vamp_gpu.hpp -- C++ host mirror of the reference's hot-path API over the C ABI (vamp_gpu.h).
+//
+// Mirrors the names and argument meaning of the reference (jamesmotes/mr-vamp):
+//   vamp::collision::Environment<float> + add_* routing     collision/environment.hh:12-66,
+//                                                          bindings/environment.cc:107-146
+//   vamp::robots::PandaBase<X100,Y100,Z100>, Panda          robots/panda_base.hh:15-75,
+//                                                          robots/panda_grid.hh:10-41
+//   vamp::planning::validate_motion<Robot, rake, res>       planning/validate.hh:67-75
+// so a planner written against the reference can swap its batch edge checks to the GPU.  As in
+// the reference, collision results are plain bools (true = valid); infrastructure failures
+// (no device, HIP error, bad arguments) throw vamp_gpu::Error, since the C ABI reports them
+// as status codes.
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "vamp_gpu.h"
+
+namespace vamp_gpu
+{
+    struct Error : std::runtime_error
+    {
+        int code;
+        Error(int c, const std::string &m) : std::runtime_error(m), code(c) {}
+    };
+
+    inline void check(int rc, const vgpu_ctx *ctx, const char *what)
+    {
+        if (rc != VGPU_OK)
+        {
+            throw Error(rc, std::string(what) + ": " + (ctx ? vgpu_last_error(ctx) : "no context"));
+        }
+    }
+
+    // One HIP device + stream; probes the host CPU's rsqrt approximation on creation.
+    class Context
+    {
+    public:
+        explicit Context(int device = 0)
+        {
+            const int rc = vgpu_ctx_create(device, &h_);
+            if (rc != VGPU_OK)
+            {
+                throw Error(rc, "vgpu_ctx_create failed");
+            }
+        }
+        ~Context() { vgpu_ctx_destroy(h_); }
+        Context(const Context &) = delete;
+        Context &operator=(const Context &) = delete;
+        auto handle() const noexcept -> vgpu_ctx * { return h_; }
+        void sync() { check(vgpu_sync(h_), h_, "vgpu_sync"); }
+        void set_stream(void *hip_stream) { check(vgpu_ctx_set_stream(h_, hip_stream), h_, "set_stream"); }
+
+    private:
+        vgpu_ctx *h_ = nullptr;
+    };
+
+    namespace collision
+    {
+        using Point = std::array<float, 3>;
+
+        // vamp::collision::Environment<float>: obstacles are routed and sorted exactly like the
+        // reference (axis_3_z == 1 -> z-aligned cuboid, xv == yv == 0 -> z-aligned capsule,
+        // each list by min_distance); the device copy is made lazily on first use.
+        class Environment
+        {
+        public:
+            explicit Environment(Context &ctx) : ctx_(ctx)
+            {
+                check(vgpu_env_create(ctx.handle(), &h_), ctx.handle(), "vgpu_env_create");
+            }
+            ~Environment() { vgpu_env_destroy(h_); }
+            Environment(const Environment &) = delete;
+            Environment &operator=(const Environment &) = delete;
+
+            void add_sphere(const Point &center, float radius)
+            {
+                check(vgpu_env_add_sphere(h_, center.data(), radius), ctx_.handle(), "add_sphere");
+            }
+            // factory::cuboid::array(center, euler_xyz, half_extents) (factory.hh:26-95)
+            void add_cuboid(const Point &center, const Point &euler_xyz, const Point &half_extents)
+            {
+                check(vgpu_env_add_cuboid_euler(h_, center.data(), euler_xyz.data(), half_extents.data()),
+                      ctx_.handle(), "add_cuboid");
+            }
+            // Cuboid<float> field constructor (shapes.hh:71-105)
+            void add_cuboid(const Point &center, const Point &a1, const Point &a2, const Point &a3,
+                            const Point &half_extents)
+            {
+                check(vgpu_env_add_cuboid_axes(h_, center.data(), a1.data(), a2.data(), a3.data(),
+                                               half_extents.data()),
+                      ctx_.handle(), "add_cuboid");
+            }
+            // factory::cylinder::endpoints (factory.hh:104-121)
+            void add_capsule(const Point &p1, const Point &p2, float radius)
+            {
+                check(vgpu_env_add_capsule_endpoints(h_, p1.data(), p2.data(), radius), ctx_.handle(),
+                      "add_capsule");
+            }
+            // factory::cylinder::center (factory.hh:149-173)
+            void add_capsule(const Point &center, const Point &euler_xyz, float radius, float length)
+            {
+                check(vgpu_env_add_capsule_euler(h_, center.data(), euler_xyz.data(), radius, length),
+                      ctx_.handle(), "add_capsule");
+            }
+            auto handle() const noexcept -> vgpu_env * { return h_; }
+            auto context() const noexcept -> Context & { return ctx_; }
+
+        private:
+            Context &ctx_;
+            vgpu_env *h_ = nullptr;
+        };
+    }  // namespace collision
+
+    namespace robots
+    {
+        // vamp::robots::PandaBase<X100, Y100, Z100> (robots/panda_base.hh:15-75)
+        template <int BaseX100, int BaseY100, int BaseZ100>
+        struct PandaBase
+        {
+            static constexpr auto name = "panda";
+            static constexpr std::size_t dimension = 7;
+            static constexpr std::size_t resolution = 32;
+            static constexpr std::size_t n_spheres = 59;
+            static constexpr float base_x = static_cast<float>(BaseX100) / 100.0f;
+            static constexpr float base_y = static_cast<float>(BaseY100) / 100.0f;
+            static constexpr float base_z = static_cast<float>(BaseZ100) / 100.0f;
+
+            using Configuration = std::array<float, dimension>;
+            using Spheres = std::array<std::array<float, 3>, n_spheres>;  // centres; radii are constants
+
+            static auto c_robot() noexcept -> vgpu_robot
+            {
+                return vgpu_robot{VGPU_ROBOT_PANDA, BaseX100, BaseY100, BaseZ100};
+            }
+
+            // fkcc<rake> of one configuration broadcast to the rake == validate(q) without the
+            // joint-limit check (bindings/common.hh:172-182)
+            static auto fkcc(collision::Environment &env, const Configuration &q) -> bool
+            {
+                return fkcc(env, std::vector<Configuration>{q})[0] != 0;
+            }
+
+            static auto fkcc(collision::Environment &env, const std::vector<Configuration> &q)
+                -> std::vector<uint8_t>
+            {
+                std::vector<uint8_t> out(q.size());
+                const vgpu_robot r = c_robot();
+                vgpu_ctx *c = env.context().handle();
+                check(vgpu_fkcc_host(c, &r, env.handle(), q.empty() ? nullptr : q[0].data(), q.size(),
+                                     out.data()),
+                      c, "vgpu_fkcc_host");
+                return out;
+            }
+
+            // sphere_fk<1> (fk.hh:104-1333): world-frame centres of the 59 collision spheres
+            static auto sphere_fk(Context &ctx, const Configuration &q) -> Spheres
+            {
+                std::vector<float> soa(3 * n_spheres);
+                const vgpu_robot r = c_robot();
+                check(vgpu_sphere_fk_host(ctx.handle(), &r, q.data(), 1, soa.data()), ctx.handle(),
+                      "vgpu_sphere_fk_host");
+                Spheres out{};
+                for (std::size_t s = 0; s < n_spheres; ++s)
+                    for (int c = 0; c < 3; ++c) out[s][c] = soa[c * n_spheres + s];
+                return out;
+            }
+        };
+
+        // robots/panda_grid.hh:10-41 -- this fork's default Panda stands at (2, 2, 0)
+        struct Panda : PandaBase<200, 200, 0> {};
+        struct Panda_0_0 : PandaBase<0, 0, 0> { static constexpr auto name = "panda_0_0"; };
+        struct Panda_1_0 : PandaBase<100, 0, 0> { static constexpr auto name = "panda_1_0"; };
+        struct Panda_2_2 : PandaBase<200, 200, 0> { static constexpr auto name = "panda_2_2"; };
+    }  // namespace robots
+
+    namespace planning
+    {
+        // validate_motion<Robot, 8, Robot::resolution> for a batch of edges (validate.hh:67-75);
+        // n_blocks receives n_e (interpolants = 8 * n_e) when given.
+        template <typename Robot>
+        inline auto validate_motions(collision::Environment &env,
+                                     const std::vector<typename Robot::Configuration> &starts,
+                                     const std::vector<typename Robot::Configuration> &goals,
+                                     std::vector<int32_t> *n_blocks = nullptr) -> std::vector<uint8_t>
+        {
+            if (starts.size() != goals.size())
+            {
+                throw Error(VGPU_ERR_INVALID_ARG, "validate_motions: starts/goals differ in size");
+            }
+            std::vector<uint8_t> ok(starts.size());
+            std::vector<int32_t> n(starts.size());
+            const vgpu_robot r = Robot::c_robot();
+            vgpu_ctx *c = env.context().handle();
+            check(vgpu_validate_motions_host(c, &r, env.handle(), starts.empty() ? nullptr : starts[0].data(),
+                                             goals.empty() ? nullptr : goals[0].data(), starts.size(), ok.data(),
+                                             n.data()),
+                  c, "vgpu_validate_motions_host");
+            if (n_blocks) *n_blocks = std::move(n);
+            return ok;
+        }
+
+        // validate_motion<Robot, 8, res>(start, goal, env): one edge (prefer the batch form)
+        template <typename Robot>
+        inline auto validate_motion(collision::Environment &env, const typename Robot::Configuration &start,
+                                    const typename Robot::Configuration &goal) -> bool
+        {
+            return validate_motions<Robot>(env, {start}, {goal})[0] != 0;
+        }
+    }  // namespace planning
+}  // namespace vamp_gpu
