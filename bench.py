@@ -144,6 +144,25 @@ def traffic_record(path):
         return None
 
 
+def shard_seed(rank):
+    """Each rank draws its own independent edge shard (weak scaling: E edges per GPU)."""
+    return 1234 + 7919 * rank
+
+
+def reduce_over_ranks(dist, torch, wall, units, dev, world):
+    """(max wall time over ranks, sum of units over ranks): the job finishes when the
+    slowest rank does, and value = every rank's interpolants / that time.  The reduction
+    tensor lives on `dev` (RCCL) or on the CPU (gloo)."""
+    if world <= 1:
+        return float(wall), float(units)
+    on = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+    mx = torch.tensor([wall], dtype=torch.float64, device=on)
+    sm = torch.tensor([units], dtype=torch.float64, device=on)
+    dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+    dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+    return float(mx[0]), float(sm[0])
+
+
 def main():
     a = parse()
     import torch
@@ -171,7 +190,7 @@ def main():
     robot = vamp.panda_0_0
 
     E = a.edges
-    starts, goals = make_edges(torch, vamp, env, robot, E, seed=1234 + 7919 * rank, dev=dev)
+    starts, goals = make_edges(torch, vamp, env, robot, E, seed=shard_seed(rank), dev=dev)
     ok = torch.empty(E, dtype=torch.uint8, device=dev)
     nb = torch.empty(E, dtype=torch.int32, device=dev)
 
@@ -201,15 +220,7 @@ def main():
     wall = t1 - t0
     kern_ms = ev0.elapsed_time(ev1) / a.steps  # HIP events on the launch stream
 
-    tt = torch.tensor([wall, units_local], dtype=torch.float64, device=dev)
-    if world > 1:
-        mx = tt.clone()
-        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
-        sm = tt.clone()
-        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
-        wall_max, units_all = float(mx[0]), float(sm[1])
-    else:
-        wall_max, units_all = wall, units_local
+    wall_max, units_all = reduce_over_ranks(dist, torch, wall, units_local, dev, world)
 
     # secondary leg (untimed for the headline): the HBM-bound sphere_fk stream, 4M configs
     fk_leg = None
