@@ -71,6 +71,7 @@ int vgpu_rsqrt_table(const vgpu_ctx *ctx, int *kbits, const uint32_t **table);
 int vgpu_rsqrt_table_set(vgpu_ctx *ctx, const uint32_t *table, int kbits);
 
 /* ---- environment (collision::Environment<float>) ---------------------------------------- */
+/* ctx may be NULL for a host-only environment (built and inspected, never uploaded). */
 int vgpu_env_create(vgpu_ctx *ctx, vgpu_env **out);
 void vgpu_env_destroy(vgpu_env *env);
 /* Shape constructors of collision/shapes.hh + factory.hh, with the routing of
@@ -86,6 +87,23 @@ int vgpu_env_add_capsule_euler(vgpu_env *env, const float center[3], const float
                                float length);
 /* obstacle counts: spheres, capsules, z-capsules, cuboids, z-cuboids */
 int vgpu_env_counts(const vgpu_env *env, int32_t counts[5]);
+
+/* Environment::add_heightfield(factory::heightfield::array(center, scale, {xd, yd}, data))
+ * (bindings/environment.cc:96,144-147; factory.hh:365-423): data row-major xd*yd floats. */
+int vgpu_env_add_heightfield(vgpu_env *env, const float center[3], const float scale[3], size_t xd, size_t yd,
+                             const float *data);
+/* Environment::add_pointcloud(points, r_min, r_max, r_point) (bindings/environment.cc:148-158):
+ * builds a CAPT (collision/capt.hh:327-398) on the host; *build_ns (optional) = build time. */
+int vgpu_env_add_pointcloud(vgpu_env *env, const float *points, size_t n, float r_min, float r_max,
+                            float r_point, int64_t *build_ns);
+/* counts[0] = heightfields, counts[1] = point clouds */
+int vgpu_env_ext_counts(const vgpu_env *env, int32_t counts[2]);
+/* the built CAPT of point cloud `index`: 2^nlog2 leaves, n_aff affordance vectors, top box */
+int vgpu_env_pointcloud_info(const vgpu_env *env, int index, int32_t *nlog2, size_t *n_aff, float top[6]);
+/* copies of its arrays: tests[2^nlog2-1], aabbs[2^nlog2][6], aff_starts[2^nlog2+1],
+ * aff[n_aff][3][8] (any pointer may be NULL) */
+int vgpu_env_pointcloud_arrays(const vgpu_env *env, int index, float *tests, float *aabbs, uint32_t *aff_starts,
+                               float *aff);
 /* Copy the (sorted) environment to the device.  Called implicitly by the batch functions
  * when the environment changed since the last upload. */
 int vgpu_env_upload(vgpu_env *env);
@@ -104,6 +122,12 @@ int vgpu_validate_motions(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env,
                           const float *goals, size_t n_edges, uint8_t *ok, int32_t *n_blocks);
 
 /* ---- host-pointer conveniences (copy + synchronise) ---------------------------------------- */
+/* Raw sphere queries against point cloud `index`: simd = 0 -> CAPT::collides(center, r)
+ * (capt.hh:403-443); simd = 1 -> one lane of CAPT::collides_simd (capt.hh:457-541).
+ * centers[n][3], radii[n] -> out[n] (1 = collision). */
+int vgpu_pointcloud_collides(vgpu_ctx *ctx, vgpu_env *env, int index, const float *centers, const float *radii,
+                             size_t n, int simd, uint8_t *out);
+
 int vgpu_sphere_fk_host(vgpu_ctx *ctx, const vgpu_robot *robot, const float *q, size_t n, float *xyz);
 int vgpu_fkcc_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n,
                    uint8_t *valid);
@@ -112,6 +136,8 @@ int vgpu_validate_motions_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env 
 
 /* ---- robot metadata ------------------------------------------------------------------------ */
 /* dimension, resolution, n_spheres of a robot kind (robots/panda_base.hh:19-23) */
+int vgpu_pointcloud_collides_host(vgpu_ctx *ctx, vgpu_env *env, int index, const float *centers,
+                                  const float *radii, size_t n, int simd, uint8_t *out);
 int vgpu_robot_info(int32_t kind, int32_t *dimension, int32_t *resolution, int32_t *n_spheres);
 
 #ifdef __cplusplus

@@ -17,9 +17,12 @@
 #include <vector>
 
 #include "../../include/vamp_gpu.h"
+#include "vgpu_capt.hh"
 #include "vgpu_device.hh"
 
 extern "C" {
+hipError_t vgpu_launch_capt_query(const float* centers, const float* radii, size_t n, const EnvView* env, int index,
+                                  int simd, uint8_t* out, hipStream_t st);
 hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float by, float bz, float* out,
                                        size_t ld, hipStream_t st);
 hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, float bx, float by, float bz,
@@ -141,6 +144,9 @@ struct vgpu_env {
     std::vector<std::array<float, 5>> spheres;
     std::vector<std::array<float, 9>> capsules, zcapsules;
     std::vector<std::array<float, 16>> cuboids, zcuboids;
+    std::vector<vgpu::Heightfield> heightfields;
+    std::vector<vgpu::CaptTree> pointclouds;
+    size_t hf_off = 0, pc_off = 0;
     bool dirty = true;
     float* dev = nullptr;
     size_t dev_floats = 0;
@@ -341,9 +347,10 @@ static void euler_xyz_matrix(const float e[3], float R[3][3])
     R[2][2] = 1 - 2 * (x * x + y * y);
 }
 
+// c may be NULL: a host-only environment (build and inspect; it cannot be uploaded or used)
 extern "C" int vgpu_env_create(vgpu_ctx* c, vgpu_env** out)
 {
-    if (!c || !out) return VGPU_ERR_INVALID_ARG;
+    if (!out) return VGPU_ERR_INVALID_ARG;
     auto* e = new (std::nothrow) vgpu_env();
     if (!e) return fail(c, VGPU_ERR_OOM, "out of host memory");
     e->ctx = c;
@@ -436,6 +443,72 @@ extern "C" int vgpu_env_counts(const vgpu_env* e, int32_t counts[5])
     return VGPU_OK;
 }
 
+// HeightField via factory::heightfield::array / flat (factory.hh:365-423): reciprocal scales
+extern "C" int vgpu_env_add_heightfield(vgpu_env* e, const float center[3], const float scale[3], size_t xd,
+                                        size_t yd, const float* data)
+{
+    if (!e || !center || !scale || (xd * yd && !data)) return VGPU_ERR_INVALID_ARG;
+    if (xd == 0 || yd == 0 || xd * yd >= (1u << 24)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "heightfield size");
+    vgpu::Heightfield h;
+    h.x = center[0];
+    h.y = center[1];
+    h.z = center[2];
+    h.xs = 1.0f / scale[0];
+    h.ys = 1.0f / scale[1];
+    h.zs = 1.0f / scale[2];
+    h.xd = xd;
+    h.yd = yd;
+    h.data.assign(data, data + xd * yd);
+    e->heightfields.push_back(std::move(h));
+    e->dirty = true;
+    return VGPU_OK;
+}
+
+// Environment::add_pointcloud (bindings/environment.cc:148-158): builds the CAPT on the host
+extern "C" int vgpu_env_add_pointcloud(vgpu_env* e, const float* points, size_t n, float r_min, float r_max,
+                                       float r_point, int64_t* build_ns)
+{
+    if (!e || (n && !points)) return VGPU_ERR_INVALID_ARG;
+    if (n == 0 || n > ((size_t)1 << 26)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "point cloud size");
+    for (size_t i = 0; i < 3 * n; ++i)
+        if (!std::isfinite(points[i])) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "non-finite point");
+    e->pointclouds.emplace_back();
+    vgpu::capt_build(points, n, r_min, r_max, r_point, e->pointclouds.back());
+    if (build_ns) *build_ns = e->pointclouds.back().build_ns;
+    e->dirty = true;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_ext_counts(const vgpu_env* e, int32_t counts[2])
+{
+    if (!e || !counts) return VGPU_ERR_INVALID_ARG;
+    counts[0] = (int32_t)e->heightfields.size();
+    counts[1] = (int32_t)e->pointclouds.size();
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_pointcloud_info(const vgpu_env* e, int index, int32_t* nlog2, size_t* n_aff, float top[6])
+{
+    if (!e || index < 0 || (size_t)index >= e->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
+    const auto& t = e->pointclouds[index];
+    if (nlog2) *nlog2 = t.nlog2;
+    if (n_aff) *n_aff = t.n_aff();
+    if (top) std::copy(t.top, t.top + 6, top);
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_pointcloud_arrays(const vgpu_env* e, int index, float* tests, float* aabbs,
+                                          uint32_t* aff_starts, float* aff)
+{
+    if (!e || index < 0 || (size_t)index >= e->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
+    const auto& t = e->pointclouds[index];
+    if (tests) std::copy(t.tests.begin(), t.tests.end(), tests);
+    if (aabbs) std::copy(t.aabbs.begin(), t.aabbs.end(), aabbs);
+    if (aff_starts) std::copy(t.aff_starts.begin(), t.aff_starts.end(), aff_starts);
+    if (aff) std::copy(t.aff.begin(), t.aff.end(), aff);
+    return VGPU_OK;
+}
+
 template <size_t W>
 static void sort_md(std::vector<std::array<float, W>>& v)  // environment.hh:40-66
 {
@@ -448,6 +521,7 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
 {
     if (!e) return VGPU_ERR_INVALID_ARG;
     vgpu_ctx* c = e->ctx;
+    if (!c) return VGPU_ERR_INVALID_ARG;  // host-only environment
     if (!e->dirty && e->dev) return VGPU_OK;
     sort_md(e->spheres);
     sort_md(e->capsules);
@@ -477,6 +551,49 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     put(e->zcapsules, OBS_ZCAPSULE, 8);
     put(e->cuboids, OBS_CUBOID, 15);
     put(e->zcuboids, OBS_ZCUBOID, 15);
+    // heightfields and point clouds: kExtHdr-float headers, then their arrays (16-B aligned)
+    auto hdr_u = [](uint32_t u) { return u2f(u); };
+    auto align16 = [&]() { while (blob.size() % 4) blob.push_back(0.0f); };
+    e->hf_off = blob.size();
+    blob.resize(blob.size() + (size_t)kExtHdr * e->heightfields.size(), 0.0f);
+    e->pc_off = blob.size();
+    blob.resize(blob.size() + (size_t)kExtHdr * e->pointclouds.size(), 0.0f);
+    for (size_t i = 0; i < e->heightfields.size(); ++i) {
+        const auto& h = e->heightfields[i];
+        align16();
+        const size_t data_off = blob.size();
+        blob.insert(blob.end(), h.data.begin(), h.data.end());
+        float* hd = &blob[e->hf_off + kExtHdr * i];
+        const float v[HF_OFF] = {h.x, h.y, h.z, h.xs, h.ys, h.zs, (float)h.xd, (float)h.yd, (float)(h.xd / 2),
+                                 (float)(h.yd / 2)};
+        std::copy(v, v + HF_OFF, hd);
+        hd[HF_OFF] = hdr_u((uint32_t)data_off);
+        hd[HF_CELLS] = hdr_u((uint32_t)(h.xd * h.yd));
+    }
+    for (size_t i = 0; i < e->pointclouds.size(); ++i) {
+        const auto& t = e->pointclouds[i];
+        align16();
+        const size_t o_tests = blob.size();
+        blob.insert(blob.end(), t.tests.begin(), t.tests.end());
+        align16();
+        const size_t o_aabbs = blob.size();
+        blob.insert(blob.end(), t.aabbs.begin(), t.aabbs.end());
+        align16();
+        const size_t o_starts = blob.size();
+        for (uint32_t v : t.aff_starts) blob.push_back(u2f(v));
+        align16();
+        const size_t o_aff = blob.size();
+        blob.insert(blob.end(), t.aff.begin(), t.aff.end());
+        float* hd = &blob[e->pc_off + kExtHdr * i];
+        std::copy(t.top, t.top + 6, hd);
+        hd[PC_RPOINT] = t.r_point;
+        hd[PC_NLOG2] = hdr_u((uint32_t)t.nlog2);
+        hd[PC_TESTS] = hdr_u((uint32_t)o_tests);
+        hd[PC_AABBS] = hdr_u((uint32_t)o_aabbs);
+        hd[PC_STARTS] = hdr_u((uint32_t)o_starts);
+        hd[PC_AFF] = hdr_u((uint32_t)o_aff);
+    }
+    if (blob.size() >= ((size_t)1 << 32)) return fail(c, VGPU_ERR_INVALID_ARG, "environment larger than 16 GiB");
     HIPCHK(c, hipSetDevice(c->device));
     if (blob.size() > e->dev_floats) {
         if (e->dev) {
@@ -502,6 +619,11 @@ static EnvView make_view(const vgpu_env* e)
     }
     v.lut = e->ctx->lut_dev;
     v.kbits = e->ctx->kbits;
+    v.hf = (const VGPU_CONST float*)(e->dev + e->hf_off);
+    v.pc = (const VGPU_CONST float*)(e->dev + e->pc_off);
+    v.base = e->dev;
+    v.n_hf = (int)e->heightfields.size();
+    v.n_pc = (int)e->pointclouds.size();
     return v;
 }
 
@@ -627,6 +749,23 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     return VGPU_OK;
 }
 
+// CAPT::collides (simd = 0, capt.hh:403-443) or one lane of CAPT::collides_simd (simd = 1,
+// capt.hh:457-541) for n raw spheres against point cloud `index` of the environment.
+extern "C" int vgpu_pointcloud_collides(vgpu_ctx* c, vgpu_env* e, int index, const float* centers,
+                                        const float* radii, size_t n, int simd, uint8_t* out)
+{
+    if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
+    if (index < 0 || (size_t)index >= e->pointclouds.size()) return fail(c, VGPU_ERR_INVALID_ARG, "bad index");
+    if (n == 0) return VGPU_OK;
+    if (!centers || !radii || !out) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
+    int rc = vgpu_env_upload(e);
+    if (rc) return rc;
+    const EnvView v = make_view(e);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_capt_query(centers, radii, n, &v, index, simd, out, c->cur));
+    return VGPU_OK;
+}
+
 // ---- host conveniences ------------------------------------------------------------------
 static int stage(vgpu_ctx* c, size_t bytes, char** p)
 {
@@ -696,6 +835,26 @@ extern "C" int vgpu_validate_motions_host(vgpu_ctx* c, const vgpu_robot* r, vgpu
     if ((rc = vgpu_validate_motions(c, r, e, (const float*)d, (const float*)(d + qb), n, okd, nbd))) return rc;
     HIPCHK(c, hipMemcpyAsync(ok, okd, n, hipMemcpyDeviceToHost, c->cur));
     if (n_blocks) HIPCHK(c, hipMemcpyAsync(n_blocks, nbd, n * 4, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_pointcloud_collides_host(vgpu_ctx* c, vgpu_env* e, int index, const float* centers,
+                                             const float* radii, size_t n, int simd, uint8_t* out)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (n == 0) return VGPU_OK;
+    char* d;
+    const size_t cb = al(n * 12), rb = al(n * 4);
+    int rc = stage(c, cb + rb + n, &d);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(d, centers, n * 12, hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipMemcpyAsync(d + cb, radii, n * 4, hipMemcpyHostToDevice, c->cur));
+    if ((rc = vgpu_pointcloud_collides(c, e, index, (const float*)d, (const float*)(d + cb), n, simd,
+                                       (uint8_t*)(d + cb + rb))))
+        return rc;
+    HIPCHK(c, hipMemcpyAsync(out, d + cb + rb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
 }

@@ -106,7 +106,20 @@ struct EnvView {
     const uint32_t* lut;  // host rsqrt table, 2 << kbits entries
     int n[OBS_TYPES];
     int kbits;
+    // heightfields and point clouds (no cull; evaluated after the five primitive types,
+    // validity.hh:133-148).  Headers are kExtHdr floats each (layouts below); data / tree
+    // arrays are addressed as float offsets from `base` (the environment's device buffer).
+    const VGPU_CONST float* hf;
+    const VGPU_CONST float* pc;
+    const float* base;
+    int n_hf, n_pc;
 };
+constexpr int kExtHdr = 16;
+// heightfield header: x y z xs ys zs xd yd xd2 yd2 (floats) | data_off cells (uint32 bits)
+enum : int { HF_X = 0, HF_Y, HF_Z, HF_XS, HF_YS, HF_ZS, HF_XD, HF_YD, HF_XD2, HF_YD2, HF_OFF, HF_CELLS };
+// point-cloud (CAPT) header: top lower xyz, top upper xyz, r_point | nlog2, tests_off, aabbs_off,
+// starts_off, aff_off (uint32 bits).  aff = [n_aff][3][8] floats (x8 y8 z8), 16-B aligned.
+enum : int { PC_TOP = 0, PC_RPOINT = 6, PC_NLOG2 = 7, PC_TESTS, PC_AABBS, PC_STARTS, PC_AFF };
 
 __device__ __forceinline__ bool signbit_f(float v) { return (__float_as_uint(v) >> 31) != 0u; }
 
@@ -180,7 +193,80 @@ __device__ __forceinline__ void scan_type(const VGPU_CONST float* o, float emax,
     }
 }
 
-template <class Grp>
+// _mm256_max_ps / _mm256_min_ps operand semantics (a NaN first operand yields the second)
+__device__ __forceinline__ float mm_max(float a, float b) { return a > b ? a : b; }
+__device__ __forceinline__ float mm_min(float a, float b) { return a < b ? a : b; }
+__device__ __forceinline__ uint32_t hdr_u(const VGPU_CONST float* h, int i) { return __float_as_uint(h[i]); }
+
+// sphere_heightfield (sphere_heightfield.hh:9-30) in the release build's form (ref_probe "hf"):
+// xs = floor(clamp(fma(xs, hx - x, xd2), 0, xd)), index = fma(ys, xd, xs), value = (z - r) -
+// fma(zs, data[index], hz).  An index outside the data (undefined in the reference, whose
+// gather reads past the array) is reported as a collision.
+__device__ __forceinline__ bool hf_lane(const VGPU_CONST float* h, const float* __restrict__ base, float x, float y,
+                                        float z, float r)
+{
+    const float xo = h[HF_X] - x, yo = h[HF_Y] - y;
+    const float xs = __builtin_floorf(mm_min(mm_max(__builtin_fmaf(h[HF_XS], xo, h[HF_XD2]), 0.0f), h[HF_XD]));
+    const float ys = __builtin_floorf(mm_min(mm_max(__builtin_fmaf(h[HF_YS], yo, h[HF_YD2]), 0.0f), h[HF_YD]));
+    const float fi = __builtin_fmaf(ys, h[HF_XD], xs);
+    const uint32_t cells = hdr_u(h, HF_CELLS);
+    if (!(fi >= 0.0f && fi < (float)cells)) return true;
+    const uint32_t idx = (uint32_t)__builtin_rintf(fi);
+    if (idx >= cells) return true;
+    const float zh = base[hdr_u(h, HF_OFF) + idx];
+    return signbit_f((z - r) - __builtin_fmaf(h[HF_ZS], zh, h[HF_Z]));
+}
+
+// one lane of CAPT::collides_simd (capt.hh:457-541): top-box test inflated by r, descent of
+// the implicit split tree (axis cycles x, y, z), leaf point-volume box test with
+// (r + r_point)^2, then the leaf's affordance vectors, inclusive distance test.  Sums of
+// squares in the FloatVector form fma(d0, d0, fma(d2, d2, d1 * d1)) (ref_probe "sql2").
+__device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float* __restrict__ base, float x, float y,
+                                          float z, float r)
+{
+    if (!((x + r >= h[0]) && (x - r <= h[3]) && (y + r >= h[1]) && (y - r <= h[4]) && (z + r >= h[2]) &&
+          (z - r <= h[5])))
+        return false;
+    const int nlog2 = (int)hdr_u(h, PC_NLOG2);
+    const float* __restrict__ tests = base + hdr_u(h, PC_TESTS);
+    uint32_t idx = 0;
+    float a = x, b = y, c = z;  // the axis of level i is i % 3
+    for (int i = 0; i < nlog2; ++i) {
+        idx = 2u * idx + 1u + ((a >= tests[idx]) ? 1u : 0u);
+        const float t = a;
+        a = b;
+        b = c;
+        c = t;
+    }
+    const uint32_t leaf = nlog2 ? idx - ((1u << nlog2) - 1u) : 0u;
+    const float* __restrict__ box = base + hdr_u(h, PC_AABBS) + 6u * leaf;
+    const float rr = r + h[PC_RPOINT];
+    const float rc = rr * rr;
+    const float d0 = x - mm_min(mm_max(x, box[0]), box[3]);
+    const float d1 = y - mm_min(mm_max(y, box[1]), box[4]);
+    const float d2 = z - mm_min(mm_max(z, box[2]), box[5]);
+    if (!(__builtin_fmaf(d0, d0, __builtin_fmaf(d2, d2, d1 * d1)) <= rc)) return false;
+    const uint32_t* __restrict__ starts = (const uint32_t*)(base + hdr_u(h, PC_STARTS));
+    const uint32_t s = starts[leaf], e = starts[leaf + 1];
+    const float4* __restrict__ aff = (const float4*)(base + hdr_u(h, PC_AFF));
+    for (uint32_t i = s; i < e; ++i) {
+        const float4* v = aff + 6u * i;
+        const float4 x0 = v[0], x1 = v[1], y0 = v[2], y1 = v[3], z0 = v[4], z1 = v[5];
+        const float px[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const float py[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+        const float pz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+        bool any = false;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const float dx = px[l] - x, dy = py[l] - y, dz = pz[l] - z;
+            any |= __builtin_fmaf(dx, dx, __builtin_fmaf(dz, dz, dy * dy)) <= rc;
+        }
+        if (any) return true;
+    }
+    return false;
+}
+
+template <class Grp, bool EXT = false>
 __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, float z, float r)
 {
     const float d = dot3(x, y, z, x, y, z);
@@ -231,6 +317,12 @@ __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, f
             const float a3 = max0(__builtin_fabsf(zs) - o[15]);
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
         });
+    if constexpr (EXT) {
+        for (int i = 0; i < env.n_hf; ++i)
+            if (!hit) hit = hf_lane(env.hf + kExtHdr * i, env.base, x, y, z, r);
+        for (int i = 0; i < env.n_pc; ++i)
+            if (!hit) hit = capt_lane(env.pc + kExtHdr * i, env.base, x, y, z, r);
+    }
     return hit;
 }
 

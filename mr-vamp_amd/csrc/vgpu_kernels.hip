@@ -32,6 +32,7 @@ namespace vgpu {
 #endif
 constexpr int kBlock = 256;
 
+template <bool EXT>
 __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_fkcc_kernel(const float* __restrict__ q, size_t n, EnvView env,
                                                             float bx, float by, float bz,
                                                             uint8_t* __restrict__ valid)
@@ -39,7 +40,7 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_fkcc_kernel(c
     const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const float* qi = q + 7 * i;
-    valid[i] = panda_fkcc<Grp1>(qi[0], qi[1], qi[2], qi[3], qi[4], qi[5], qi[6], env, bx, by, bz) ? 1 : 0;
+    valid[i] = panda_fkcc<Grp1, EXT>(qi[0], qi[1], qi[2], qi[3], qi[4], qi[5], qi[6], env, bx, by, bz) ? 1 : 0;
 }
 
 // ---- validate_vector: shared rake arithmetic (validate.hh:31-50) ----------------------------
@@ -63,6 +64,7 @@ __device__ __forceinline__ Rake rake_setup(const float* __restrict__ s, const fl
     return r;
 }
 
+template <bool EXT>
 __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_validate_head_kernel(
     const float* __restrict__ starts, const float* __restrict__ goals, size_t n_edges, EnvView env, float bx,
     float by, float bz, uint8_t* __restrict__ ok, int32_t* __restrict__ n_blocks, uint32_t* __restrict__ cnt)
@@ -77,7 +79,7 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_validate_head
     float b[7];
 #pragma unroll
     for (int j = 0; j < 7; ++j) b[j] = __builtin_fmaf(rk.v[j], pct, s[j]);  // validate.hh:37 (contracted)
-    const bool valid = panda_fkcc<Grp8>(b[0], b[1], b[2], b[3], b[4], b[5], b[6], env, bx, by, bz);
+    const bool valid = panda_fkcc<Grp8, EXT>(b[0], b[1], b[2], b[3], b[4], b[5], b[6], env, bx, by, bz);
     if (lane == 0) {
         ok[e] = valid ? 1 : 0;
         if (n_blocks) n_blocks[e] = rk.n;
@@ -95,6 +97,7 @@ __global__ __launch_bounds__(kBlock) void scatter_items_kernel(const uint32_t* _
     for (uint32_t i = 0; i < c; ++i) item_edge[o + i] = (uint32_t)e;
 }
 
+template <bool EXT>
 __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_validate_tail_kernel(
     const float* __restrict__ starts, const float* __restrict__ goals, const uint32_t* __restrict__ item_edge,
     const uint32_t* __restrict__ off, size_t n_items, EnvView env, float bx, float by, float bz,
@@ -120,11 +123,13 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_validate_tail
 #pragma unroll
         for (int j = 0; j < 7; ++j) b[j] = b[j] - back[j];
     }
-    const bool valid = panda_fkcc<Grp8>(b[0], b[1], b[2], b[3], b[4], b[5], b[6], env, bx, by, bz);
+    const bool valid = panda_fkcc<Grp8, EXT>(b[0], b[1], b[2], b[3], b[4], b[5], b[6], env, bx, by, bz);
     if (lane == 0 && !valid) ok[e] = 0;  // every writer stores 0: the race is benign
 }
 
 }  // namespace vgpu
+
+static bool has_ext(const EnvView* env) { return env->n_hf > 0 || env->n_pc > 0; }
 
 extern "C" {
 
@@ -133,8 +138,12 @@ hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, 
 {
     if (n == 0) return hipSuccess;
     const unsigned grid = (unsigned)((n + vgpu::kBlock - 1) / vgpu::kBlock);
-    hipLaunchKernelGGL(vgpu::panda_fkcc_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, q, n, *env, bx, by, bz,
-                       valid);
+    if (has_ext(env))
+        hipLaunchKernelGGL(vgpu::panda_fkcc_kernel<true>, dim3(grid), dim3(vgpu::kBlock), 0, st, q, n, *env, bx, by,
+                           bz, valid);
+    else
+        hipLaunchKernelGGL(vgpu::panda_fkcc_kernel<false>, dim3(grid), dim3(vgpu::kBlock), 0, st, q, n, *env, bx, by,
+                           bz, valid);
     return hipGetLastError();
 }
 
@@ -161,8 +170,12 @@ hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goa
     const unsigned grid = (unsigned)((threads + vgpu::kBlock - 1) / vgpu::kBlock);
     hipError_t err = hipMemsetAsync(cnt + n_edges, 0, sizeof(uint32_t), st);
     if (err != hipSuccess) return err;
-    hipLaunchKernelGGL(vgpu::panda_validate_head_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, starts, goals,
-                       n_edges, *env, bx, by, bz, ok, n_blocks, cnt);
+    if (has_ext(env))
+        hipLaunchKernelGGL(vgpu::panda_validate_head_kernel<true>, dim3(grid), dim3(vgpu::kBlock), 0, st, starts,
+                           goals, n_edges, *env, bx, by, bz, ok, n_blocks, cnt);
+    else
+        hipLaunchKernelGGL(vgpu::panda_validate_head_kernel<false>, dim3(grid), dim3(vgpu::kBlock), 0, st, starts,
+                           goals, n_edges, *env, bx, by, bz, ok, n_blocks, cnt);
     return hipGetLastError();
 }
 
@@ -179,8 +192,12 @@ hipError_t vgpu_launch_panda_validate_tail(const float* starts, const float* goa
     if (err != hipSuccess) return err;
     const size_t threads = n_items * 8;
     grid = (unsigned)((threads + vgpu::kBlock - 1) / vgpu::kBlock);
-    hipLaunchKernelGGL(vgpu::panda_validate_tail_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, starts, goals,
-                       item_edge, off, n_items, *env, bx, by, bz, ok);
+    if (has_ext(env))
+        hipLaunchKernelGGL(vgpu::panda_validate_tail_kernel<true>, dim3(grid), dim3(vgpu::kBlock), 0, st, starts,
+                           goals, item_edge, off, n_items, *env, bx, by, bz, ok);
+    else
+        hipLaunchKernelGGL(vgpu::panda_validate_tail_kernel<false>, dim3(grid), dim3(vgpu::kBlock), 0, st, starts,
+                           goals, item_edge, off, n_items, *env, bx, by, bz, ok);
     return hipGetLastError();
 }
 

@@ -1,0 +1,81 @@
+// vgpu_query.hip -- raw point-cloud queries: one lane per sphere against one CAPT of the
+// environment ("raw sphere queries").
+//   simd = 0: CAPT::collides(center, r) (collision/capt.hh:403-443): top-box distance test
+//             against r^2, descent, leaf box against (r + r_point)^2 in the scalar Volume form
+//             (fma(d2, d2, fma(d0, d0, d1*d1)), std::clamp), affordance scan;
+//   simd = 1: one lane of CAPT::collides_simd (capt.hh:457-541), the form the fkcc path uses.
+#include "vgpu_device.hh"
+
+namespace vgpu {
+
+__device__ __forceinline__ float std_clamp(float v, float lo, float hi) { return (v < lo) ? lo : (hi < v) ? hi : v; }
+
+__device__ __forceinline__ float box_dist2_scalar(const float* b, float x, float y, float z)
+{
+    const float d0 = x - std_clamp(x, b[0], b[3]);
+    const float d1 = y - std_clamp(y, b[1], b[4]);
+    const float d2 = z - std_clamp(z, b[2], b[5]);
+    return __builtin_fmaf(d2, d2, __builtin_fmaf(d0, d0, d1 * d1));
+}
+
+__device__ bool capt_scalar(const VGPU_CONST float* h, const float* __restrict__ base, float x, float y, float z,
+                            float r)
+{
+    const float top[6] = {h[0], h[1], h[2], h[3], h[4], h[5]};
+    if (box_dist2_scalar(top, x, y, z) > r * r) return false;
+    const int nlog2 = (int)hdr_u(h, PC_NLOG2);
+    const float* __restrict__ tests = base + hdr_u(h, PC_TESTS);
+    uint32_t idx = 0;
+    float a = x, b = y, c = z;
+    for (int i = 0; i < nlog2; ++i) {
+        idx = 2u * idx + 1u + ((a >= tests[idx]) ? 1u : 0u);
+        const float t = a;
+        a = b;
+        b = c;
+        c = t;
+    }
+    const uint32_t leaf = nlog2 ? idx - ((1u << nlog2) - 1u) : 0u;
+    const float rr = r + h[PC_RPOINT];
+    const float rsq = rr * rr;
+    if (box_dist2_scalar(base + hdr_u(h, PC_AABBS) + 6u * leaf, x, y, z) > rsq) return false;
+    const uint32_t* __restrict__ starts = (const uint32_t*)(base + hdr_u(h, PC_STARTS));
+    const float4* __restrict__ aff = (const float4*)(base + hdr_u(h, PC_AFF));
+    for (uint32_t i = starts[leaf], e = starts[leaf + 1]; i < e; ++i) {
+        const float4* v = aff + 6u * i;
+        const float4 x0 = v[0], x1 = v[1], y0 = v[2], y1 = v[3], z0 = v[4], z1 = v[5];
+        const float px[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+        const float py[8] = {y0.x, y0.y, y0.z, y0.w, y1.x, y1.y, y1.z, y1.w};
+        const float pz[8] = {z0.x, z0.y, z0.z, z0.w, z1.x, z1.y, z1.z, z1.w};
+        bool any = false;
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const float dx = px[l] - x, dy = py[l] - y, dz = pz[l] - z;
+            any |= __builtin_fmaf(dx, dx, __builtin_fmaf(dz, dz, dy * dy)) <= rsq;
+        }
+        if (any) return true;
+    }
+    return false;
+}
+
+__global__ __launch_bounds__(256) void capt_query_kernel(const float* __restrict__ centers,
+                                                         const float* __restrict__ radii, size_t n, EnvView env,
+                                                         int index, int simd, uint8_t* __restrict__ out)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float x = centers[3 * i], y = centers[3 * i + 1], z = centers[3 * i + 2], r = radii[i];
+    const VGPU_CONST float* h = env.pc + kExtHdr * index;
+    out[i] = (simd ? capt_lane(h, env.base, x, y, z, r) : capt_scalar(h, env.base, x, y, z, r)) ? 1 : 0;
+}
+
+}  // namespace vgpu
+
+extern "C" hipError_t vgpu_launch_capt_query(const float* centers, const float* radii, size_t n, const EnvView* env,
+                                             int index, int simd, uint8_t* out, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    hipLaunchKernelGGL(vgpu::capt_query_kernel, dim3(grid), dim3(256), 0, st, centers, radii, n, *env, index, simd,
+                       out);
+    return hipGetLastError();
+}

@@ -23,8 +23,8 @@ from . import _lib
 from ._lib import VgpuError, check, load
 
 __all__ = [
-    "Context", "context", "Environment", "Sphere", "Cuboid", "Cylinder", "Robot", "PandaBase", "panda",
-    "panda_0_0", "VgpuError",
+    "Context", "context", "Environment", "Sphere", "Cuboid", "Cylinder", "HeightField", "make_heightfield", "Robot",
+    "PandaBase", "panda", "panda_0_0", "VgpuError",
 ]
 
 
@@ -152,12 +152,39 @@ class Cylinder:
         self.name = ""
 
 
+class HeightField:
+    """collision::HeightField<float> as made by vamp.make_heightfield(center, scale,
+    dimensions, data) (bindings/environment.cc:96-105, factory.hh:365-423): reciprocal scales
+    xs/ys/zs = 1/scale, data row-major with dimensions (xd, yd)."""
+
+    def __init__(self, center, scale, dimensions, data):
+        self.center = [float(v) for v in center]
+        self.scale = [float(v) for v in scale]
+        self.xd, self.yd = int(dimensions[0]), int(dimensions[1])
+        self.data = np.ascontiguousarray(data, np.float32).ravel()
+        if self.data.size != self.xd * self.yd:
+            raise ValueError("heightfield data must hold dimensions[0] * dimensions[1] values")
+        self.x, self.y, self.z = (np.float32(v) for v in self.center)
+        self.xs, self.ys, self.zs = (np.float32(1.0) / np.float32(v) for v in self.scale)
+
+
+def make_heightfield(center, scale, dimensions, data) -> HeightField:
+    return HeightField(center, scale, dimensions, data)
+
+
+class _PointCloud:
+    def __init__(self, points, r_min, r_max, r_point):
+        self.points = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+        self.r_min, self.r_max, self.r_point = float(r_min), float(r_max), float(r_point)
+
+
 class Environment:
     """collision::Environment<float> (environment.hh:12-82) realised lazily per Context."""
 
     def __init__(self):
         self._ops: List[Tuple[str, object]] = []
         self._handles: Dict[int, C.c_void_p] = {}
+        self._host: Optional[C.c_void_p] = None  # host-only twin holding the built CAPTs
 
     def _changed(self):
         for dev, h in list(self._handles.items()):
@@ -176,6 +203,63 @@ class Environment:
         self._ops.append(("capsule", c))
         self._changed()
 
+    def add_heightfield(self, h: HeightField):
+        self._ops.append(("heightfield", h))
+        self._changed()
+
+    def add_pointcloud(self, points, r_min: float, r_max: float, r_point: float) -> int:
+        """Environment::add_pointcloud (bindings/environment.cc:148-158): builds a CAPT and
+        returns the build time in nanoseconds."""
+        pc = _PointCloud(points, r_min, r_max, r_point)
+        lib = load()
+        if self._host is None:
+            h = C.c_void_p()
+            check(lib.vgpu_env_create(None, C.byref(h)))
+            self._host = h
+        ns = C.c_int64()
+        check(lib.vgpu_env_add_pointcloud(self._host, pc.points.ctypes.data_as(_lib.F32P), pc.points.shape[0],
+                                          pc.r_min, pc.r_max, pc.r_point, C.byref(ns)))
+        self._ops.append(("pointcloud", pc))
+        self._changed()
+        return int(ns.value)
+
+    def pointcloud_arrays(self, index: int = 0) -> dict:
+        """The built CAPT's arrays (tests, aabbs, aff_starts, affordances [n][3][8], top box)."""
+        lib = load()
+        n2, na, top = C.c_int32(), C.c_size_t(), (C.c_float * 6)()
+        check(lib.vgpu_env_pointcloud_info(self._host, index, C.byref(n2), C.byref(na), top))
+        m = 1 << n2.value
+        tests = np.zeros(max(m - 1, 0), np.float32)
+        aabbs = np.zeros((m, 6), np.float32)
+        starts = np.zeros(m + 1, np.uint32)
+        aff = np.zeros((na.value, 3, 8), np.float32)
+        check(lib.vgpu_env_pointcloud_arrays(self._host, index, tests.ctypes.data_as(_lib.F32P),
+                                             aabbs.ctypes.data_as(_lib.F32P), starts.ctypes.data_as(_lib.U32P),
+                                             aff.ctypes.data_as(_lib.F32P)))
+        return {"nlog2": n2.value, "tests": tests, "aabbs": aabbs, "aff_starts": starts, "aff": aff,
+                "aabb_top": np.array(top[:], np.float32)}
+
+    def pointcloud_collides(self, centers, radii, index: int = 0, simd: bool = False,
+                            ctx: Optional[Context] = None) -> np.ndarray:
+        """Raw sphere queries on the GPU: CAPT::collides (capt.hh:403-443), or with simd=True
+        one lane of CAPT::collides_simd (capt.hh:457-541)."""
+        ctx = ctx or context()
+        c = np.ascontiguousarray(centers, np.float32).reshape(-1, 3)
+        r = np.ascontiguousarray(radii, np.float32).ravel()
+        if r.shape[0] != c.shape[0]:
+            raise ValueError("one radius per centre")
+        out = np.zeros(c.shape[0], np.uint8)
+        check(load().vgpu_pointcloud_collides_host(ctx.h, self.handle(ctx), index, c.ctypes.data_as(_lib.F32P),
+                                                   r.ctypes.data_as(_lib.F32P), c.shape[0], int(simd),
+                                                   out.ctypes.data_as(_lib.U8P)), ctx.h)
+        return out.astype(bool)
+
+    def pointcloud_collides_device(self, centers_ptr: int, radii_ptr: int, n: int, out_ptr: int, index: int = 0,
+                                   simd: bool = False, ctx: Optional[Context] = None):
+        ctx = ctx or context()
+        check(load().vgpu_pointcloud_collides(ctx.h, self.handle(ctx), index, centers_ptr, radii_ptr, n, int(simd),
+                                              out_ptr), ctx.h)
+
     def handle(self, ctx: Context) -> C.c_void_p:
         if ctx.device in self._handles:
             return self._handles[ctx.device]
@@ -191,6 +275,12 @@ class Environment:
                                                       _f3(s.axes[2]), _f3(s.half))
                 else:
                     rc = lib.vgpu_env_add_cuboid_euler(h, _f3(s.center), _f3(s.euler), _f3(s.half))
+            elif kind == "heightfield":
+                rc = lib.vgpu_env_add_heightfield(h, _f3(s.center), _f3(s.scale), s.xd, s.yd,
+                                                  s.data.ctypes.data_as(_lib.F32P))
+            elif kind == "pointcloud":
+                rc = lib.vgpu_env_add_pointcloud(h, s.points.ctypes.data_as(_lib.F32P), s.points.shape[0], s.r_min,
+                                                 s.r_max, s.r_point, None)
             else:
                 if s.center is None:
                     rc = lib.vgpu_env_add_capsule_endpoints(h, _f3(s.p1), _f3(s.p2), float(np.float32(s.r)))
@@ -211,6 +301,9 @@ class Environment:
     def __del__(self):
         try:
             self._changed()
+            if self._host is not None:
+                load().vgpu_env_destroy(self._host)
+                self._host = None
         except Exception:
             pass
 

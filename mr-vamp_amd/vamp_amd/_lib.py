@@ -47,6 +47,14 @@ SIGNATURES = {
     "vgpu_env_add_capsule_endpoints": (C.c_int, [VP, F32P, F32P, C.c_float]),
     "vgpu_env_add_capsule_euler": (C.c_int, [VP, F32P, F32P, C.c_float, C.c_float]),
     "vgpu_env_counts": (C.c_int, [VP, I32P]),
+    "vgpu_env_add_heightfield": (C.c_int, [VP, F32P, F32P, C.c_size_t, C.c_size_t, F32P]),
+    "vgpu_env_add_pointcloud": (C.c_int, [VP, F32P, C.c_size_t, C.c_float, C.c_float, C.c_float,
+                                          C.POINTER(C.c_int64)]),
+    "vgpu_env_ext_counts": (C.c_int, [VP, I32P]),
+    "vgpu_env_pointcloud_info": (C.c_int, [VP, C.c_int, I32P, C.POINTER(C.c_size_t), F32P]),
+    "vgpu_env_pointcloud_arrays": (C.c_int, [VP, C.c_int, F32P, F32P, U32P, F32P]),
+    "vgpu_pointcloud_collides": (C.c_int, [VP, VP, C.c_int, VP, VP, C.c_size_t, C.c_int, VP]),
+    "vgpu_pointcloud_collides_host": (C.c_int, [VP, VP, C.c_int, F32P, F32P, C.c_size_t, C.c_int, U8P]),
     "vgpu_env_upload": (C.c_int, [VP]),
     "vgpu_sphere_fk": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, C.c_size_t, VP, C.c_size_t]),
     "vgpu_fkcc": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, C.c_size_t, VP]),

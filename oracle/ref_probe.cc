@@ -19,6 +19,13 @@
 //     are restated below with the reference's own FloatVector types because
 //     validate.hh itself includes environment.hh -> Eigen)
 //   * rng::Halton<dim>::next                                (random/halton.hh:73-104)
+//   * collision::sql2_3 on FloatVector (collision/math.hh:29-42), the CAPT affordance test
+//   * expression probes for code whose header cannot be compiled here (capt.hh needs
+//     <pdqsort.h>, sphere_heightfield.hh needs shapes.hh -> Eigen): the CAPT leaf-box test
+//     (capt.hh:505-521), Volume::distsq_to / contained_by_internal_ball (capt.hh:70-89) and
+//     sphere_heightfield (sphere_heightfield.hh:9-30) are restated below with the reference's
+//     own FloatVector/IntVector types and compiled with its flags, so the contraction and
+//     association the release compiler picks for those expression shapes is observed.
 //
 // Usage: ref_probe <mode> <in.bin> <out.bin> [args]   (raw little-endian float32)
 #include <cstdio>
@@ -29,6 +36,7 @@
 
 #include <vamp/vector.hh>
 #include <vamp/random/halton.hh>
+#include <vamp/collision/math.hh>   // <algorithm>/<cmath> only: compiled as is
 
 using namespace vamp;
 
@@ -80,6 +88,68 @@ probe_extent(const float *x, const float *y, const float *z, float r, float *ext
     auto me = rt + sr;
     me.to_array(ext);
     rt.to_array(root);
+}
+
+// collision::sql2_3 with a broadcast centre (capt.hh:528-534 affordance scan)
+__attribute__((noinline)) static void
+probe_sql2(const float *ax, const float *ay, const float *az, float bx, float by, float bz, float *out)
+{
+    FloatVector<8> X(ax), Y(ay), Z(az);
+    const auto xc = FloatVector<8>::fill(bx), yc = FloatVector<8>::fill(by), zc = FloatVector<8>::fill(bz);
+    collision::sql2_3(X, Y, Z, xc, yc, zc).to_array(out);
+}
+
+// leaf-box distance of collides_simd (capt.hh:505-521): c - clamp(c, lo, up), summed squares,
+// and rc_sq = (r + r_point)^2
+__attribute__((noinline)) static void probe_capt_box(const float *c, const float *lo, const float *up,
+                                                     const float *r, float rp, float *out, float *rc)
+{
+    FloatVector<8> c0(c), c1(c + 8), c2(c + 16), rr(r);
+    FloatVector<8> l0(lo), l1(lo + 8), l2(lo + 16), u0(up), u1(up + 8), u2(up + 16);
+    auto d0 = c0 - c0.clamp(l0, u0);
+    auto d1 = c1 - c1.clamp(l1, u1);
+    auto d2 = c2 - c2.clamp(l2, u2);
+    auto dist = d0 * d0 + d1 * d1 + d2 * d2;
+    rr = rr + rp;
+    auto rcs = rr * rr;
+    dist.to_array(out);
+    rcs.to_array(rc);
+}
+
+// Volume::distsq_to (capt.hh:79-86) and contained_by_internal_ball's sum (capt.hh:70-77), scalar
+__attribute__((noinline)) static float probe_vol_distsq(const float *p, const float *lo, const float *up)
+{
+    const float d0 = p[0] - std::clamp(p[0], lo[0], up[0]);
+    const float d1 = p[1] - std::clamp(p[1], lo[1], up[1]);
+    const float d2 = p[2] - std::clamp(p[2], lo[2], up[2]);
+    return d0 * d0 + d1 * d1 + d2 * d2;
+}
+__attribute__((noinline)) static float probe_vol_ball(const float *p, const float *lo, const float *up)
+{
+    const float d0 = std::max(p[0] - lo[0], up[0] - p[0]);
+    const float d1 = std::max(p[1] - lo[1], up[1] - p[1]);
+    const float d2 = std::max(p[2] - lo[2], up[2] - p[2]);
+    return d0 * d0 + d1 * d1 + d2 * d2;
+}
+
+// sphere_heightfield (sphere_heightfield.hh:9-30); hf = {x, y, z, xs, ys, zs, xd, yd}
+__attribute__((noinline)) static void probe_hf(const float *x, const float *y, const float *z, float r,
+                                               const float *hf, const float *data, float *out)
+{
+    using IndexT = IntVector<8>;
+    const std::size_t xd = (std::size_t)hf[6], yd = (std::size_t)hf[7];
+    const std::size_t xd2 = xd / 2, yd2 = yd / 2;
+    FloatVector<8> X(x), Y(y), Z(z), R(r);
+    FloatVector<8> hx(hf[0]), hy(hf[1]), hz(hf[2]), hxs(hf[3]), hys(hf[4]), hzs(hf[5]);
+    auto xo = hx - X;
+    auto yo = hy - Y;
+    auto xs = (hxs * xo + xd2).clamp(0.F, static_cast<float>(xd)).floor();
+    auto ys = (hys * yo + yd2).clamp(0.F, static_cast<float>(yd)).floor();
+    auto index = ys * xd + xs;
+    IndexT indices = index.template to<IndexT>();
+    auto zh = FloatVector<8>::gather(data, indices);
+    auto zhs = hzs * zh + hz;
+    (Z - R - zhs).to_array(out);
 }
 
 int main(int argc, char **argv)
@@ -203,6 +273,79 @@ int main(int argc, char **argv)
         {
             std::fprintf(stderr, "dim must be 7 or 8\n");
             return 2;
+        }
+        write_f32(argv[3], out);
+    }
+    else if (mode == "sql2")
+    {
+        // in: N x 6 (ax ay az bx by bz), b constant per group of 8.  out: N sql2_3
+        auto in = read_f32(argv[2]);
+        const size_t n = in.size() / 6;
+        std::vector<float> out(n);
+        alignas(32) float ax[8], ay[8], az[8], o[8];
+        for (size_t i = 0; i < n; i += 8)
+        {
+            for (int l = 0; l < 8; ++l)
+            {
+                ax[l] = in[6 * (i + l) + 0];
+                ay[l] = in[6 * (i + l) + 1];
+                az[l] = in[6 * (i + l) + 2];
+            }
+            probe_sql2(launder(ax), ay, az, in[6 * i + 3], in[6 * i + 4], in[6 * i + 5], o);
+            std::memcpy(&out[i], o, 32);
+        }
+        write_f32(argv[3], out);
+    }
+    else if (mode == "capt_box")
+    {
+        // in: N x 11 (c[3] lo[3] up[3] r rp), rp constant per group of 8.
+        // out: N simd leaf distsq, N rc_sq, N scalar distsq_to, N scalar ball sum
+        auto in = read_f32(argv[2]);
+        const size_t n = in.size() / 11;
+        std::vector<float> out(4 * n);
+        alignas(32) float c[24], lo[24], up[24], r[8], o[8], rc[8];
+        for (size_t i = 0; i < n; i += 8)
+        {
+            for (int l = 0; l < 8; ++l)
+            {
+                const float *row = &in[11 * (i + l)];
+                for (int k = 0; k < 3; ++k)
+                {
+                    c[8 * k + l] = row[k];
+                    lo[8 * k + l] = row[3 + k];
+                    up[8 * k + l] = row[6 + k];
+                }
+                r[l] = row[9];
+                out[2 * n + i + l] = probe_vol_distsq(launder(row), row + 3, row + 6);
+                out[3 * n + i + l] = probe_vol_ball(launder(row), row + 3, row + 6);
+            }
+            probe_capt_box(launder(c), lo, up, r, in[11 * i + 10], o, rc);
+            std::memcpy(&out[i], o, 32);
+            std::memcpy(&out[n + i], rc, 32);
+        }
+        write_f32(argv[3], out);
+    }
+    else if (mode == "hf")
+    {
+        // in: header [8] (x y z xs ys zs xd yd), data[xd*yd], then N x 4 (x y z r), r constant
+        // per group of 8.  out: N test values (z - r - zh_scaled)
+        auto in = read_f32(argv[2]);
+        const size_t cells = (size_t)in[6] * (size_t)in[7];
+        const float *data = &in[8];
+        const float *q = &in[8 + cells];
+        const size_t n = (in.size() - 8 - cells) / 4;
+        std::vector<float> out(n);
+        alignas(32) float x[8], y[8], z[8], o[8];
+        for (size_t i = 0; i < n; i += 8)
+        {
+            for (int l = 0; l < 8; ++l)
+            {
+                x[l] = q[4 * (i + l)];
+                y[l] = q[4 * (i + l) + 1];
+                z[l] = q[4 * (i + l) + 2];
+            }
+            probe_hf(launder(x), y, z, q[4 * i + 3], in.data(), data, o);
+            std::memcpy(&out[i], o, 32);
         }
         write_f32(argv[3], out);
     }

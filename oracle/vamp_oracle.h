@@ -27,9 +27,36 @@ extern "C" {
  *   sphere  [5]  x y z r min_distance
  *   capsule [9]  x1 y1 z1 xv yv zv r rdv min_distance   (also z-aligned capsules)
  *   cuboid  [16] x y z a1x a1y a1z a2x a2y a2z a3x a3y a3z r1 r2 r3 min_distance */
+/* HeightField<float> (collision/shapes.hh:250-312) as made by factory::heightfield::flat
+ * (factory.hh:365-386): xs/ys/zs are the reciprocal scales; data row-major, xd*yd floats. */
+typedef struct vo_heightfield {
+    float x, y, z, xs, ys, zs;
+    int xd, yd;
+    const float *data;
+} vo_heightfield;
+
+/* CAPT (collision/capt.hh:91-398): the four arrays of the built tree.
+ *   tests      [2^nlog2 - 1]      split values, implicit binary tree
+ *   aabbs      [2^nlog2][6]       leaf Volume {lower xyz, upper xyz}
+ *   aff_starts [2^nlog2 + 1]      affordance vector range per leaf
+ *   aff        [n_aff][3][8]      affordance vectors (x8, y8, z8), +inf padded */
+typedef struct vo_capt {
+    int nlog2;
+    float r_min, r_max, r_point;
+    float aabb_top[6];
+    float *tests;
+    float *aabbs;
+    uint32_t *aff_starts;
+    float *aff;
+    size_t n_aff;
+} vo_capt;
+
 typedef struct vo_env {
     int n_spheres, n_capsules, n_zcapsules, n_cuboids, n_zcuboids;
     const float *spheres, *capsules, *zcapsules, *cuboids, *zcuboids;
+    int n_heightfields, n_pointclouds;
+    const vo_heightfield *heightfields;
+    const vo_capt *pointclouds;
 } vo_env;
 
 typedef struct vo_stats {
@@ -56,6 +83,35 @@ float vo_sqrt_lut(float v, const uint32_t *lut, int kbits);
 float vo_sphere_min_distance(float x, float y, float z, float r);              /* shapes.hh:238 */
 float vo_cuboid_min_distance(const float c[15]);                               /* shapes.hh:52-67 */
 float vo_capsule_min_distance(const float c[8]);                               /* shapes.hh:165-189 */
+
+/* sphere_heightfield (sphere_heightfield.hh:9-30): signed test value, collision = sign bit.
+ * *oob is set when the reference's gather index falls outside the data (undefined in the
+ * reference; the GPU path reports a collision there). */
+float vo_sphere_heightfield(const vo_heightfield *h, float x, float y, float z, float r, int *oob);
+
+/* ---- CAPT (collision/capt.hh) ---- */
+/* CAPT::CAPT(points, r_min, r_max, r_point) (capt.hh:327-398, subdivide :156-325).  points: n x 3.  Ties in a
+ * split coordinate are ordered by point index (the reference's pdqsort_branchless leaves
+ * their order unspecified).  Returns 0 on success; free with vo_capt_free. */
+int vo_capt_build(const float *points, size_t n, float r_min, float r_max, float r_point, vo_capt *out);
+void vo_capt_free(vo_capt *t);
+/* CAPT::collides(center, r) (capt.hh:403-443) */
+int vo_capt_collides(const vo_capt *t, const float c[3], float r, vo_stats *st);
+/* one lane of CAPT::collides_simd (capt.hh:457-541): the result of the SIMD call is the OR
+ * of this over the lanes */
+int vo_capt_collides_lane(const vo_capt *t, const float c[3], float r, vo_stats *st);
+/* batch of raw queries (centres n x 3, radii n); simd != 0 selects the per-lane collides_simd
+ * semantics.  margin (optional, n) receives each query's smallest |comparison difference|. */
+void vo_capt_collides_batch(const vo_capt *t, const float *centers, const float *radii, size_t n, int simd,
+                            uint8_t *out, double *margin);
+
+/* expression-level pins (ref_probe "sql2" / "capt_box"): collision::sql2_3 on FloatVector,
+ * the collides_simd leaf-box distance (FloatVector clamp), Volume::distsq_to and the
+ * contained_by_internal_ball sum (scalar) */
+float vo_sql2_3(float ax, float ay, float az, float bx, float by, float bz);
+float vo_capt_box_vec(const float c[3], const float lo[3], const float up[3]);
+float vo_capt_vol_distsq(const float p[3], const float lo[3], const float up[3]);
+float vo_capt_vol_ball(const float p[3], const float lo[3], const float up[3]);
 
 /* ---- Panda (robots/panda_base.hh, robots/panda/fk.hh) ---- */
 void vo_panda_scale(float q[7]);                                               /* fk.hh:34-37 */

@@ -20,11 +20,24 @@ I32P = C.POINTER(C.c_int32)
 U32P = C.POINTER(C.c_uint32)
 
 
+class VoHeightfield(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float), ("xs", C.c_float), ("ys", C.c_float),
+                ("zs", C.c_float), ("xd", C.c_int), ("yd", C.c_int), ("data", F32P)]
+
+
+class VoCapt(C.Structure):
+    _fields_ = [("nlog2", C.c_int), ("r_min", C.c_float), ("r_max", C.c_float), ("r_point", C.c_float),
+                ("aabb_top", C.c_float * 6), ("tests", F32P), ("aabbs", F32P), ("aff_starts", U32P),
+                ("aff", F32P), ("n_aff", C.c_size_t)]
+
+
 class VoEnv(C.Structure):
     _fields_ = [
         ("n_spheres", C.c_int), ("n_capsules", C.c_int), ("n_zcapsules", C.c_int), ("n_cuboids", C.c_int),
         ("n_zcuboids", C.c_int),
         ("spheres", F32P), ("capsules", F32P), ("zcapsules", F32P), ("cuboids", F32P), ("zcuboids", F32P),
+        ("n_heightfields", C.c_int), ("n_pointclouds", C.c_int),
+        ("heightfields", C.POINTER(VoHeightfield)), ("pointclouds", C.POINTER(VoCapt)),
     ]
 
 
@@ -80,6 +93,19 @@ def lib():
         L.vo_panda_validate_motions.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_size_t, C.c_int, C.c_int,
                                                 C.c_int, U8P, I32P, C.c_int]
         L.vo_halton.argtypes = [C.c_int, C.c_uint64, F32P]
+        L.vo_sphere_heightfield.restype = C.c_float
+        L.vo_sphere_heightfield.argtypes = [C.POINTER(VoHeightfield), C.c_float, C.c_float, C.c_float, C.c_float,
+                                            C.POINTER(C.c_int)]
+        L.vo_sql2_3.restype = C.c_float
+        L.vo_sql2_3.argtypes = [C.c_float] * 6
+        for fn in ("vo_capt_box_vec", "vo_capt_vol_distsq", "vo_capt_vol_ball"):
+            getattr(L, fn).restype = C.c_float
+            getattr(L, fn).argtypes = [F32P, F32P, F32P]
+        L.vo_capt_build.restype = C.c_int
+        L.vo_capt_build.argtypes = [F32P, C.c_size_t, C.c_float, C.c_float, C.c_float, C.POINTER(VoCapt)]
+        L.vo_capt_free.argtypes = [C.POINTER(VoCapt)]
+        L.vo_capt_collides_batch.argtypes = [C.POINTER(VoCapt), F32P, F32P, C.c_size_t, C.c_int, U8P,
+                                             C.POINTER(C.c_double)]
         L.vo_panda_scale.argtypes = [F32P]
         _lib = L
     return _lib
@@ -97,6 +123,7 @@ class Env:
 
     def __init__(self):
         self.spheres, self.capsules, self.zcapsules, self.cuboids, self.zcuboids = [], [], [], [], []
+        self.heightfields, self.pointclouds = [], []
 
     def add_sphere(self, center, r):
         x, y, z = (float(np.float32(v)) for v in center)
@@ -123,6 +150,19 @@ class Env:
         (self.zcapsules if (v[0] == 0 and v[1] == 0) else self.capsules).append(row)
         return self
 
+    def add_heightfield(self, center, scale, xd, yd, data):
+        """factory::heightfield::flat (factory.hh:365-386): stores 1/scale."""
+        d = np.ascontiguousarray(data, np.float32).ravel()
+        assert d.size == xd * yd
+        self.heightfields.append(((np.float32(center[0]), np.float32(center[1]), np.float32(center[2]),
+                                   np.float32(1.0) / np.float32(scale[0]), np.float32(1.0) / np.float32(scale[1]),
+                                   np.float32(1.0) / np.float32(scale[2]), int(xd), int(yd)), d))
+        return self
+
+    def add_pointcloud(self, points, r_min, r_max, r_point):
+        self.pointclouds.append(Capt(points, r_min, r_max, r_point))
+        return self
+
     def arrays(self):
         out = {}
         for name, width in (("spheres", 5), ("capsules", 9), ("zcapsules", 9), ("cuboids", 16), ("zcuboids", 16)):
@@ -140,7 +180,58 @@ class Env:
         for name in arrs:
             setattr(e, "n_" + name, len(arrs[name]))
             setattr(e, name, fp(arrs[name]) if len(arrs[name]) else None)
+        if self.heightfields:
+            hf = (VoHeightfield * len(self.heightfields))()
+            for i, (h, d) in enumerate(self.heightfields):
+                hf[i] = VoHeightfield(*h, fp(d))
+            e.n_heightfields = len(self.heightfields)
+            e.heightfields = hf
+            self._keep_hf = hf
+        if self.pointclouds:
+            pc = (VoCapt * len(self.pointclouds))()
+            for i, t in enumerate(self.pointclouds):
+                pc[i] = t.t
+            e.n_pointclouds = len(self.pointclouds)
+            e.pointclouds = pc
+            self._keep_pc = pc
         return e
+
+
+class Capt:
+    """CAPT::CAPT (collision/capt.hh:327-398) built by the C restatement."""
+
+    def __init__(self, points, r_min, r_max, r_point):
+        p = np.ascontiguousarray(points, np.float32).reshape(-1, 3)
+        self.t = VoCapt()
+        lib().vo_capt_build(fp(p), p.shape[0], r_min, r_max, r_point, C.byref(self.t))
+
+    def arrays(self):
+        t = self.t
+        m = 1 << t.nlog2
+        return {
+            "nlog2": t.nlog2,
+            "tests": np.ctypeslib.as_array(t.tests, (max(m - 1, 1),))[: m - 1].copy(),
+            "aabbs": np.ctypeslib.as_array(t.aabbs, (m * 6,)).reshape(m, 6).copy(),
+            "aff_starts": np.ctypeslib.as_array(t.aff_starts, (m + 1,)).copy(),
+            "aff": (np.ctypeslib.as_array(t.aff, (t.n_aff * 24,)).reshape(-1, 3, 8).copy() if t.n_aff
+                    else np.zeros((0, 3, 8), np.float32)),
+            "aabb_top": np.array(t.aabb_top[:], np.float32),
+        }
+
+    def collides(self, centers, radii, simd=False, margin=False):
+        c = np.ascontiguousarray(centers, np.float32).reshape(-1, 3)
+        r = np.ascontiguousarray(radii, np.float32).ravel()
+        out = np.zeros(c.shape[0], np.uint8)
+        m = np.zeros(c.shape[0], np.float64)
+        lib().vo_capt_collides_batch(C.byref(self.t), fp(c), fp(r), c.shape[0], int(simd), out.ctypes.data_as(U8P),
+                                     m.ctypes.data_as(C.POINTER(C.c_double)))
+        return (out.astype(bool), m) if margin else out.astype(bool)
+
+    def __del__(self):
+        try:
+            lib().vo_capt_free(C.byref(self.t))
+        except Exception:
+            pass
 
 
 def sphere_cage_env():

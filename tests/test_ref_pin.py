@@ -90,3 +90,63 @@ def test_halton_bit_exact(oracle, pins):
         ref = pins[f"halton{dim}"]
         got = oracle.halton(dim, ks)
         assert (got.view(np.uint32) == ref.view(np.uint32)).all(), dim
+
+
+# ---- point-cloud (CAPT) and heightfield expression pins (tests/golden/ref_pins_ext.npz) ----
+@pytest.fixture(scope="module")
+def ext():
+    return golden("ref_pins_ext.npz")
+
+
+def _f3(a):
+    a = np.ascontiguousarray(a, F)
+    return a.ctypes.data_as(C.POINTER(C.c_float)), a
+
+
+def test_sql2_bit_exact(oracle, ext):
+    """collision::sql2_3 on FloatVector (math.hh:29-42), compiled from the reference header:
+    the CAPT affordance distance (capt.hh:528-534)."""
+    L = oracle.lib()
+    x = ext["sql2_in"]
+    got = np.array([L.vo_sql2_3(*map(float, row)) for row in x], F)
+    assert (got.view(np.uint32) == ext["sql2"].view(np.uint32)).all()
+
+
+def test_capt_box_forms_bit_exact(oracle, ext):
+    """collides_simd leaf-box distance (capt.hh:505-521) and Volume::distsq_to /
+    contained_by_internal_ball (capt.hh:70-86) as the reference release build evaluates them."""
+    L = oracle.lib()
+    x = ext["box_in"]
+    vec, dist, ball = [], [], []
+    for row in x:
+        c, _a = _f3(row[0:3])
+        lo, _b = _f3(row[3:6])
+        up, _c = _f3(row[6:9])
+        vec.append(L.vo_capt_box_vec(c, lo, up))
+        dist.append(L.vo_capt_vol_distsq(c, lo, up))
+        ball.append(L.vo_capt_vol_ball(c, lo, up))
+    for got, key in ((vec, "box_vec"), (dist, "vol_distsq"), (ball, "vol_ball")):
+        got = np.array(got, F)
+        ref = ext[key]
+        assert ((got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))).all(), key
+    rr = (x[:, 9] + x[:, 10]).astype(F)
+    assert ((rr * rr).astype(F) == ext["box_rc"]).all()
+
+
+def test_heightfield_bit_exact(oracle, ext):
+    """sphere_heightfield (sphere_heightfield.hh:9-30): every in-range query bit-exact; the
+    out-of-range ones (a gather past the data in the reference) are flagged, not compared."""
+    L = oracle.lib()
+    h = ext["hf_hdr"]
+    data = np.ascontiguousarray(ext["hf_data"], F)
+    hf = oracle.VoHeightfield(*map(float, h[:6]), int(h[6]), int(h[7]), data.ctypes.data_as(C.POINTER(C.c_float)))
+    q, ref = ext["hf_q"], ext["hf"]
+    oob = C.c_int(0)
+    n_in = 0
+    for row, want in zip(q, ref):
+        v = F(L.vo_sphere_heightfield(C.byref(hf), *map(float, row), C.byref(oob)))
+        if oob.value:
+            continue
+        n_in += 1
+        assert v.view(np.uint32) == want.view(np.uint32)
+    assert n_in > 0.9 * len(q)

@@ -277,7 +277,7 @@ class RobotGen:
                     ensure_R(spheres[kid["sphere"]]["frame"])
                 w = world(bound_center(b), bd["base"])
                 E.raw(f"// env: {ck['link']} bounding sphere r={bd['radius']} (+{len(ck['children'])} children)")
-                E.raw(f"if (Grp::any(env_lane<Grp>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])}))) {{")
+                E.raw(f"if (Grp::any(env_lane<Grp, EXT>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])}))) {{")
                 E.indent += 1
                 E.raw("bool h = false;")
                 for kid in ck["children"]:
@@ -286,7 +286,7 @@ class RobotGen:
                     E.indent += 1
                     c = self.center(E, R, P, sp["frame"], sp["offset"])
                     cw = world(c, kid["base"])
-                    E.raw(f"h = env_lane<Grp>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])});")
+                    E.raw(f"h = env_lane<Grp, EXT>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])});")
                     E.indent -= 1
                     E.raw("}")
                 E.raw("if (Grp::any(h)) return false;")
@@ -349,7 +349,7 @@ class RobotGen:
             f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
             "// FK emitted lazily in check order; checks follow the reference hierarchy",
             "// (link-bounding sphere first, children only when the group's bounding test fires).",
-            "template <class Grp>",
+            "template <class Grp, bool EXT>",
             f"__device__ __forceinline__ bool {self.name}_fkcc(",
             "    " + ", ".join(f"float q{i}" for i in range(dim)) + ",",
             "    const EnvView& env, float bx, float by, float bz)",

@@ -82,6 +82,38 @@ def make_ref_pins(rng):
                         halton8=h8, halton8_k=k8)
 
 
+def make_ext_pins(rng):
+    """Expression pins for the point-cloud and heightfield paths (ref_probe modes sql2,
+    capt_box, hf): collision::sql2_3 compiled from the reference's math.hh, and restated
+    capt.hh / sphere_heightfield.hh expressions compiled with the reference's types and flags."""
+    N = 8 * 1024
+    a = rng.normal(size=(N, 3)).astype(F)
+    b = np.repeat(rng.normal(size=(N // 8, 3)).astype(F), 8, axis=0)
+    sql2_in = np.concatenate([a, b], 1).astype(F)
+    sql2 = probe("sql2", sql2_in)
+    c = rng.normal(size=(N, 3)).astype(F)
+    lo = (rng.normal(size=(N, 3)) * 0.5 - 0.3).astype(F)
+    up = (lo + rng.random((N, 3)).astype(F)).astype(F)
+    lo[:64] = -np.inf  # unbounded cells (the root volume)
+    up[64:128] = np.inf
+    r = (rng.random(N) * 0.06).astype(F)
+    rp = np.repeat((rng.random(N // 8) * 0.01).astype(F), 8)
+    box_in = np.concatenate([c, lo, up, r[:, None], rp[:, None]], 1).astype(F)
+    box = probe("capt_box", box_in).reshape(4, N)
+    xd, yd = 37, 29
+    hdr = np.array([0.3, -0.2, 0.1, 1 / 0.05, 1 / 0.04, 1 / 0.5, xd, yd], F)
+    data = rng.random(xd * yd).astype(F)
+    q = np.zeros((N, 4), F)
+    q[:, 0] = rng.uniform(-0.9, 0.9, N)
+    q[:, 1] = rng.uniform(-0.9, 0.9, N)
+    q[:, 2] = rng.uniform(0, 1, N)
+    q[:, 3] = np.repeat(rng.uniform(0.01, 0.1, N // 8), 8)
+    hf = probe("hf", np.concatenate([hdr, data, q.ravel()]))
+    np.savez_compressed(os.path.join(GOLD, "ref_pins_ext.npz"), sql2_in=sql2_in, sql2=sql2, box_in=box_in,
+                        box_vec=box[0], box_rc=box[1], vol_distsq=box[2], vol_ball=box[3], hf_hdr=hdr,
+                        hf_data=data, hf_q=q, hf=hf)
+
+
 def sphere_cage():
     e = op.sphere_cage_env()
     return e, fi.EnvNP(spheres=e.arrays()["spheres"])
@@ -125,6 +157,8 @@ def main():
     rng = np.random.default_rng(20251015)
     make_ref_pins(rng)
     print("ref_pins.npz")
+    make_ext_pins(np.random.default_rng(20261015))
+    print("ref_pins_ext.npz")
 
     fk, cc = fi.load_panda()
     lut, kb = op.rsqrt_probe()
