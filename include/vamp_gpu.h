@@ -128,6 +128,20 @@ int vgpu_validate_motions(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env,
 int vgpu_pointcloud_collides(vgpu_ctx *ctx, vgpu_env *env, int index, const float *centers, const float *radii,
                              size_t n, int simd, uint8_t *out);
 
+/* ---- sampling (PRM vertex stage) ---------------------------------------- */
+/* rng::Halton<dim>::next (random/halton.hh:73-104): draws first .. first+n-1 of a fresh sampler
+ * (first >= 1; the reference resets every 1e6 draws and rotates the bases), out[n][dim]. */
+int vgpu_halton(vgpu_ctx *ctx, int dim, uint64_t first, size_t n, float *out);
+/* Halton<dimension> draws scaled by Robot::scale_configuration (panda/fk.hh:34-37): q[n][dim] */
+int vgpu_sample_configurations(vgpu_ctx *ctx, const vgpu_robot *robot, uint64_t first, size_t n, float *q);
+/* the same fused with the per-configuration fkcc (prm.hh:236-251); q may be NULL */
+int vgpu_sample_fkcc(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, uint64_t first, size_t n, float *q,
+                     uint8_t *valid);
+/* stream compaction of the rows whose flag is set: index_out[*count] ascending, rows_out (if not
+ * NULL) = the selected rows[dim].  Synchronises to return *count (host). */
+int vgpu_compact(vgpu_ctx *ctx, const float *rows, const uint8_t *valid, size_t n, int dim, float *rows_out,
+                 uint32_t *index_out, size_t *count);
+
 int vgpu_sphere_fk_host(vgpu_ctx *ctx, const vgpu_robot *robot, const float *q, size_t n, float *xyz);
 int vgpu_fkcc_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n,
                    uint8_t *valid);
@@ -138,6 +152,9 @@ int vgpu_validate_motions_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env 
 /* dimension, resolution, n_spheres of a robot kind (robots/panda_base.hh:19-23) */
 int vgpu_pointcloud_collides_host(vgpu_ctx *ctx, vgpu_env *env, int index, const float *centers,
                                   const float *radii, size_t n, int simd, uint8_t *out);
+int vgpu_halton_host(vgpu_ctx *ctx, int dim, uint64_t first, size_t n, float *out);
+int vgpu_sample_fkcc_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, uint64_t first, size_t n, float *q,
+                          uint8_t *valid);
 int vgpu_robot_info(int32_t kind, int32_t *dimension, int32_t *resolution, int32_t *n_spheres);
 
 #ifdef __cplusplus

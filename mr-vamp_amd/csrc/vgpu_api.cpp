@@ -21,6 +21,15 @@
 #include "vgpu_device.hh"
 
 extern "C" {
+hipError_t vgpu_launch_panda_sample(uint64_t first, size_t n, float* q, hipStream_t st);
+hipError_t vgpu_launch_panda_sample_fkcc(uint64_t first, size_t n, const EnvView* env, float bx, float by, float bz,
+                                         float* q, uint8_t* valid, hipStream_t st);
+hipError_t vgpu_launch_halton(int dim, uint64_t first, size_t n, float* out, hipStream_t st);
+size_t vgpu_compact_bytes(size_t n);
+hipError_t vgpu_launch_compact(const uint8_t* valid, size_t n, uint32_t* idx_out, uint32_t* count, void* tmp,
+                               size_t tmp_bytes, hipStream_t st);
+hipError_t vgpu_launch_gather_rows(const float* q, const uint32_t* idx, const uint32_t* count, size_t max_rows,
+                                   int dim, float* out, hipStream_t st);
 hipError_t vgpu_launch_capt_query(const float* centers, const float* radii, size_t n, const EnvView* env, int index,
                                   int simd, uint8_t* out, hipStream_t st);
 hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float by, float bz, float* out,
@@ -133,6 +142,9 @@ struct vgpu_ctx {
     uint32_t* items = nullptr;
     size_t items_cap = 0;
     uint32_t* total_host = nullptr;
+    // compaction workspace (selected indices' count word + hipcub temp)
+    void* aux = nullptr;
+    size_t aux_bytes = 0;
     // optional phase timing
     bool prof = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -214,6 +226,7 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->stage) (void)hipFree(c->stage);
     if (c->ws) (void)hipFree(c->ws);
     if (c->items) (void)hipFree(c->items);
+    if (c->aux) (void)hipFree(c->aux);
     if (c->total_host) (void)hipHostFree(c->total_host);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -766,6 +779,78 @@ extern "C" int vgpu_pointcloud_collides(vgpu_ctx* c, vgpu_env* e, int index, con
     return VGPU_OK;
 }
 
+// ---- sampling (rng::Halton, Robot::scale_configuration) and compaction --------------------------
+extern "C" int vgpu_halton(vgpu_ctx* c, int dim, uint64_t first, size_t n, float* out)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (dim < 1 || dim > 16 || first == 0) return fail(c, VGPU_ERR_INVALID_ARG, "dim must be 1..16, first >= 1");
+    if (n == 0) return VGPU_OK;
+    if (!out) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_halton(dim, first, n, out, c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_sample_configurations(vgpu_ctx* c, const vgpu_robot* r, uint64_t first, size_t n, float* q)
+{
+    float b[3];
+    int rc = check_robot(c, r, b);
+    if (rc) return rc;
+    if (first == 0) return fail(c, VGPU_ERR_INVALID_ARG, "draw indices start at 1");
+    if (n == 0) return VGPU_OK;
+    if (!q) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_panda_sample(first, n, q, c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, uint64_t first, size_t n, float* q,
+                                uint8_t* valid)
+{
+    if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
+    float b[3];
+    int rc = check_robot(c, r, b);
+    if (rc) return rc;
+    if (first == 0) return fail(c, VGPU_ERR_INVALID_ARG, "draw indices start at 1");
+    if (n == 0) return VGPU_OK;
+    if (!valid) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
+    if ((rc = vgpu_env_upload(e))) return rc;
+    const EnvView v = make_view(e);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_panda_sample_fkcc(first, n, &v, b[0], b[1], b[2], q, valid, c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_compact(vgpu_ctx* c, const float* rows, const uint8_t* valid, size_t n, int dim, float* rows_out,
+                            uint32_t* index_out, size_t* count)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (dim < 1 || !count || n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "bad compaction args");
+    *count = 0;
+    if (n == 0) return VGPU_OK;
+    if (!valid || !index_out || (rows_out && !rows)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
+    const size_t tmp = vgpu_compact_bytes(n);
+    const size_t need = 256 + tmp;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (need > c->aux_bytes) {
+        if (c->aux) {
+            HIPCHK(c, hipStreamSynchronize(c->cur));
+            HIPCHK(c, hipFree(c->aux));
+            c->aux = nullptr;
+        }
+        HIPCHK(c, hipMalloc(&c->aux, need));
+        c->aux_bytes = need;
+    }
+    if (!c->total_host) HIPCHK(c, hipHostMalloc((void**)&c->total_host, sizeof(uint32_t), hipHostMallocDefault));
+    uint32_t* cnt = (uint32_t*)c->aux;
+    HIPCHK(c, vgpu_launch_compact(valid, n, index_out, cnt, (char*)c->aux + 256, tmp, c->cur));
+    if (rows_out) HIPCHK(c, vgpu_launch_gather_rows(rows, index_out, cnt, n, dim, rows_out, c->cur));
+    HIPCHK(c, hipMemcpyAsync(c->total_host, cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    *count = *c->total_host;
+    return VGPU_OK;
+}
+
 // ---- host conveniences ------------------------------------------------------------------
 static int stage(vgpu_ctx* c, size_t bytes, char** p)
 {
@@ -855,6 +940,35 @@ extern "C" int vgpu_pointcloud_collides_host(vgpu_ctx* c, vgpu_env* e, int index
                                        (uint8_t*)(d + cb + rb))))
         return rc;
     HIPCHK(c, hipMemcpyAsync(out, d + cb + rb, n, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_halton_host(vgpu_ctx* c, int dim, uint64_t first, size_t n, float* out)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (n == 0) return VGPU_OK;
+    char* d;
+    int rc = stage(c, n * (size_t)dim * 4, &d);
+    if (rc) return rc;
+    if ((rc = vgpu_halton(c, dim, first, n, (float*)d))) return rc;
+    HIPCHK(c, hipMemcpyAsync(out, d, n * (size_t)dim * 4, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_sample_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, uint64_t first, size_t n,
+                                     float* q, uint8_t* valid)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (n == 0) return VGPU_OK;
+    char* d;
+    const size_t qb = al(n * kPandaDim * 4);
+    int rc = stage(c, qb + n, &d);
+    if (rc) return rc;
+    if ((rc = vgpu_sample_fkcc(c, r, e, first, n, q ? (float*)d : nullptr, (uint8_t*)(d + qb)))) return rc;
+    if (q) HIPCHK(c, hipMemcpyAsync(q, d, n * kPandaDim * 4, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
 }

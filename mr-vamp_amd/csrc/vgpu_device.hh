@@ -89,6 +89,39 @@ __device__ __forceinline__ float vamp_cos(float x)
     return vamp_sin(v);
 }
 
+// ---- rng::Halton<dim>::next (random/halton.hh:73-104), closed form ------------------------------
+// Draw k (1-based: the k-th next() of a fresh sampler).  The reference restarts its numerators
+// every 1,000,000 draws and rotates the bases left; since the reset sets iterations = 0 after
+// the increment, every cycle after the first is 1,000,001 draws long.  Within a cycle, draw i
+// has coordinate d = radical inverse of i in base primes[(d + cycle) % dim], and the
+// reference's n / d are exact float integers, so one float division reproduces it.
+constexpr uint32_t kHaltonPrimes[16] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53, 59};
+constexpr uint64_t kHaltonCycle = 1000000u;
+
+__device__ __forceinline__ void halton_index(uint64_t k, uint32_t& idx, uint32_t& cycle)
+{
+    if (k <= kHaltonCycle) {
+        idx = (uint32_t)k;
+        cycle = 0;
+    } else {
+        const uint64_t kk = k - kHaltonCycle - 1;
+        cycle = (uint32_t)(1 + kk / (kHaltonCycle + 1));
+        idx = (uint32_t)(kk % (kHaltonCycle + 1)) + 1u;
+    }
+}
+
+__device__ __forceinline__ float halton_coord(uint32_t idx, uint32_t b)
+{
+    uint32_t num = 0, den = 1;
+    while (idx) {
+        const uint32_t q = idx / b;
+        num = num * b + (idx - q * b);
+        den *= b;
+        idx = q;
+    }
+    return (float)num / (float)den;
+}
+
 // ---- environment view ----------------------------------------------------------------------
 // collision::Environment<float> on the device: one section per obstacle type, each sorted
 // ascending by min_distance (environment.hh:40-66) and terminated by kObsPad sentinel records

@@ -43,6 +43,42 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_fkcc_kernel(c
     valid[i] = panda_fkcc<Grp1, EXT>(qi[0], qi[1], qi[2], qi[3], qi[4], qi[5], qi[6], env, bx, by, bz) ? 1 : 0;
 }
 
+// ---- sampling: Halton<7> draw -> scale_configuration -> fkcc (prm.hh:236-251) ----
+__device__ __forceinline__ void panda_sample(uint64_t k, float q[7])
+{
+    uint32_t idx, cyc;
+    halton_index(k, idx, cyc);
+#pragma unroll
+    for (int d = 0; d < 7; ++d)
+        q[d] = __builtin_fmaf(halton_coord(idx, kHaltonPrimes[(d + cyc) % 7u]), panda_s_m[d], panda_s_a[d]);
+}
+
+__global__ __launch_bounds__(kBlock) void panda_sample_kernel(uint64_t first, size_t n, float* __restrict__ q)
+{
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    float v[7];
+    panda_sample(first + i, v);
+#pragma unroll
+    for (int d = 0; d < 7; ++d) q[7 * i + d] = v[d];
+}
+
+template <bool EXT>
+__global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_sample_fkcc_kernel(
+    uint64_t first, size_t n, EnvView env, float bx, float by, float bz, float* __restrict__ q,
+    uint8_t* __restrict__ valid)
+{
+    const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    float v[7];
+    panda_sample(first + i, v);
+    if (q) {
+#pragma unroll
+        for (int d = 0; d < 7; ++d) q[7 * i + d] = v[d];
+    }
+    valid[i] = panda_fkcc<Grp1, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, bx, by, bz) ? 1 : 0;
+}
+
 // ---- validate_vector: shared rake arithmetic (validate.hh:31-50) ----------------------------
 struct Rake {
     float v[7];
@@ -85,6 +121,17 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_validate_head
         if (n_blocks) n_blocks[e] = rk.n;
         cnt[e] = (valid && rk.n > 1) ? (uint32_t)(rk.n - 1) : 0u;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void gather_rows_kernel(const float* __restrict__ q, const uint32_t* __restrict__ idx,
+                                                             const uint32_t* __restrict__ count, int dim,
+                                                             float* __restrict__ out)
+{
+    const size_t t = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    const size_t j = t / (size_t)dim;
+    if (j >= *count) return;
+    const int d = (int)(t - j * (size_t)dim);
+    out[t] = q[(size_t)idx[j] * dim + d];
 }
 
 __global__ __launch_bounds__(kBlock) void scatter_items_kernel(const uint32_t* __restrict__ cnt,
@@ -145,6 +192,54 @@ hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, 
         hipLaunchKernelGGL(vgpu::panda_fkcc_kernel<false>, dim3(grid), dim3(vgpu::kBlock), 0, st, q, n, *env, bx, by,
                            bz, valid);
     return hipGetLastError();
+}
+
+hipError_t vgpu_launch_panda_sample(uint64_t first, size_t n, float* q, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n + vgpu::kBlock - 1) / vgpu::kBlock);
+    hipLaunchKernelGGL(vgpu::panda_sample_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, first, n, q);
+    return hipGetLastError();
+}
+
+hipError_t vgpu_launch_panda_sample_fkcc(uint64_t first, size_t n, const EnvView* env, float bx, float by, float bz,
+                                         float* q, uint8_t* valid, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n + vgpu::kBlock - 1) / vgpu::kBlock);
+    if (has_ext(env))
+        hipLaunchKernelGGL(vgpu::panda_sample_fkcc_kernel<true>, dim3(grid), dim3(vgpu::kBlock), 0, st, first, n,
+                           *env, bx, by, bz, q, valid);
+    else
+        hipLaunchKernelGGL(vgpu::panda_sample_fkcc_kernel<false>, dim3(grid), dim3(vgpu::kBlock), 0, st, first, n,
+                           *env, bx, by, bz, q, valid);
+    return hipGetLastError();
+}
+
+// Compaction of valid samples (the PRM vertex stage): out_q[j] = q[idx[j]], idx ascending.
+size_t vgpu_compact_bytes(size_t n)
+{
+    size_t tmp = 0;
+    (void)hipcub::DeviceSelect::Flagged(nullptr, tmp, hipcub::CountingInputIterator<uint32_t>(0),
+                                        (const uint8_t*)nullptr, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+    return tmp;
+}
+
+hipError_t vgpu_launch_gather_rows(const float* q, const uint32_t* idx, const uint32_t* count, size_t max_rows,
+                                   int dim, float* out, hipStream_t st)
+{
+    if (max_rows == 0) return hipSuccess;
+    const size_t threads = max_rows * (size_t)dim;
+    const unsigned grid = (unsigned)((threads + vgpu::kBlock - 1) / vgpu::kBlock);
+    hipLaunchKernelGGL(vgpu::gather_rows_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, q, idx, count, dim, out);
+    return hipGetLastError();
+}
+
+hipError_t vgpu_launch_compact(const uint8_t* valid, size_t n, uint32_t* idx_out, uint32_t* count, void* tmp,
+                               size_t tmp_bytes, hipStream_t st)
+{
+    return hipcub::DeviceSelect::Flagged(tmp, tmp_bytes, hipcub::CountingInputIterator<uint32_t>(0), valid, idx_out,
+                                         count, (int)n, st);
 }
 
 // Workspace for the two-phase validate: cnt[n_edges + 1], off[n_edges + 1], scan temp.

@@ -68,7 +68,24 @@ __global__ __launch_bounds__(256) void capt_query_kernel(const float* __restrict
     out[i] = (simd ? capt_lane(h, env.base, x, y, z, r) : capt_scalar(h, env.base, x, y, z, r)) ? 1 : 0;
 }
 
+// rng::Halton<dim>::next draws first .. first + n - 1, one lane per draw (random/halton.hh:73-104)
+__global__ __launch_bounds__(256) void halton_kernel(int dim, uint64_t first, size_t n, float* __restrict__ out)
+{
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint32_t idx, cyc;
+    halton_index(first + i, idx, cyc);
+    for (int d = 0; d < dim; ++d) out[(size_t)dim * i + d] = halton_coord(idx, kHaltonPrimes[(d + cyc) % (uint32_t)dim]);
+}
+
 }  // namespace vgpu
+
+extern "C" hipError_t vgpu_launch_halton(int dim, uint64_t first, size_t n, float* out, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(vgpu::halton_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, dim, first, n, out);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t vgpu_launch_capt_query(const float* centers, const float* radii, size_t n, const EnvView* env,
                                              int index, int simd, uint8_t* out, hipStream_t st)

@@ -23,7 +23,7 @@ from . import _lib
 from ._lib import VgpuError, check, load
 
 __all__ = [
-    "Context", "context", "Environment", "Sphere", "Cuboid", "Cylinder", "HeightField", "make_heightfield", "Robot",
+    "Context", "context", "Environment", "Sphere", "Cuboid", "Cylinder", "HeightField", "make_heightfield", "Robot", "halton", "compact_device",
     "PandaBase", "panda", "panda_0_0", "VgpuError",
 ]
 
@@ -308,6 +308,25 @@ class Environment:
             pass
 
 
+# ---- sampling ---------------------------------------------------------------------------------
+def halton(dim: int, first: int, n: int, ctx: Optional[Context] = None) -> np.ndarray:
+    """rng::Halton<dim>::next draws first .. first+n-1 (1-based) of a fresh sampler, on the GPU."""
+    ctx = ctx or context()
+    out = np.empty((n, dim), np.float32)
+    check(load().vgpu_halton_host(ctx.h, dim, first, n, out.ctypes.data_as(_lib.F32P)), ctx.h)
+    return out
+
+
+def compact_device(rows_ptr: int, valid_ptr: int, n: int, dim: int, rows_out_ptr: int, index_out_ptr: int,
+                   ctx: Optional[Context] = None) -> int:
+    """Stream compaction on the device (selected row indices ascending); returns the count."""
+    ctx = ctx or context()
+    cnt = C.c_size_t()
+    check(load().vgpu_compact(ctx.h, C.c_void_p(rows_ptr or 0), C.c_void_p(valid_ptr), n, dim,
+                              C.c_void_p(rows_out_ptr or 0), C.c_void_p(index_out_ptr), C.byref(cnt)), ctx.h)
+    return int(cnt.value)
+
+
 # ---- robots -----------------------------------------------------------------------------------
 class Robot:
     """Python face of vamp::robots::PandaBase<X100, Y100, Z100> (robots/panda_base.hh:15-75)."""
@@ -415,6 +434,22 @@ class Robot:
         ctx = ctx or context()
         check(load().vgpu_sphere_fk(ctx.h, C.byref(self.c_robot), C.c_void_p(q_ptr), n, C.c_void_p(out_ptr), ld),
               ctx.h)
+
+    def sample_fkcc(self, first: int, n: int, environment: Environment, ctx: Optional[Context] = None):
+        """Halton<dimension> draws first .. first+n-1 -> scale_configuration -> fkcc, fused on the
+        GPU (the PRM sampling stage, prm.hh:236-251).  Returns (q [n, dim], valid [n])."""
+        ctx = ctx or context()
+        q = np.empty((n, self.dimension()), np.float32)
+        ok = np.empty(n, np.uint8)
+        check(load().vgpu_sample_fkcc_host(ctx.h, C.byref(self.c_robot), environment.handle(ctx), first, n,
+                                           q.ctypes.data_as(_lib.F32P), ok.ctypes.data_as(_lib.U8P)), ctx.h)
+        return q, ok.astype(bool)
+
+    def sample_fkcc_device(self, first: int, n: int, environment: Environment, q_ptr: int, valid_ptr: int,
+                           ctx: Optional[Context] = None):
+        ctx = ctx or context()
+        check(load().vgpu_sample_fkcc(ctx.h, C.byref(self.c_robot), environment.handle(ctx), first, n,
+                                      C.c_void_p(q_ptr or 0), C.c_void_p(valid_ptr)), ctx.h)
 
     def fkcc_device(self, q_ptr: int, n: int, environment: Environment, valid_ptr: int,
                     ctx: Optional[Context] = None):

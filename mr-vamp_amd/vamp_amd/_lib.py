@@ -62,6 +62,12 @@ SIGNATURES = {
     "vgpu_sphere_fk_host": (C.c_int, [VP, C.POINTER(VgpuRobot), F32P, C.c_size_t, F32P]),
     "vgpu_fkcc_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P]),
     "vgpu_validate_motions_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P]),
+    "vgpu_halton": (C.c_int, [VP, C.c_int, C.c_uint64, C.c_size_t, VP]),
+    "vgpu_sample_configurations": (C.c_int, [VP, C.POINTER(VgpuRobot), C.c_uint64, C.c_size_t, VP]),
+    "vgpu_sample_fkcc": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, C.c_uint64, C.c_size_t, VP, VP]),
+    "vgpu_compact": (C.c_int, [VP, VP, VP, C.c_size_t, C.c_int, VP, VP, C.POINTER(C.c_size_t)]),
+    "vgpu_halton_host": (C.c_int, [VP, C.c_int, C.c_uint64, C.c_size_t, F32P]),
+    "vgpu_sample_fkcc_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, C.c_uint64, C.c_size_t, F32P, U8P]),
     "vgpu_robot_info": (C.c_int, [C.c_int32, I32P, I32P, I32P]),
 }
 

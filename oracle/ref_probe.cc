@@ -152,6 +152,22 @@ __attribute__((noinline)) static void probe_hf(const float *x, const float *y, c
     (Z - R - zhs).to_array(out);
 }
 
+// Robot::scale_configuration shape (robots/panda/fk.hh:34-37): q * s_m + s_a on FloatVector<7>
+// with the Panda constants restated from fk.hh:14-30 (fk.hh itself needs Eigen via its includes)
+__attribute__((noinline)) static void probe_scale(const float *q, float *out)
+{
+    alignas(32) static const std::array<float, 7> sm{5.9342f, 3.6652f, 5.9342f, 3.2289f, 5.9342f, 3.9096f, 5.9342f};
+    alignas(32) static const std::array<float, 7> sa{-2.9671f, -1.8326f, -2.9671f, -3.1416f, -2.9671f, -0.0873f,
+                                                      -2.9671f};
+    const FloatVector<7> s_m(sm), s_a(sa);
+    alignas(32) float buf[8] = {0};
+    std::memcpy(buf, q, 28);
+    FloatVector<7> v(buf);
+    v = v * s_m + s_a;
+    v.to_array(buf);
+    std::memcpy(out, buf, 28);
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 4) { std::fprintf(stderr, "usage: ref_probe mode in out [args]\n"); return 2; }
@@ -274,6 +290,15 @@ int main(int argc, char **argv)
             std::fprintf(stderr, "dim must be 7 or 8\n");
             return 2;
         }
+        write_f32(argv[3], out);
+    }
+    else if (mode == "scale")
+    {
+        // in: N x 7 unit-cube samples.  out: N x 7 scaled configurations
+        auto in = read_f32(argv[2]);
+        const size_t n = in.size() / 7;
+        std::vector<float> out(7 * n);
+        for (size_t i = 0; i < n; ++i) probe_scale(launder(&in[7 * i]), &out[7 * i]);
         write_f32(argv[3], out);
     }
     else if (mode == "sql2")

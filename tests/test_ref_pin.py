@@ -150,3 +150,10 @@ def test_heightfield_bit_exact(oracle, ext):
         n_in += 1
         assert v.view(np.uint32) == want.view(np.uint32)
     assert n_in > 0.9 * len(q)
+
+
+def test_scale_configuration_bit_exact(oracle, ext):
+    """Robot::scale_configuration q * s_m + s_a (robots/panda/fk.hh:34-37) compiles to one fma
+    per joint; the Halton -> configuration step of the sampling path."""
+    got = oracle.scale(ext["scale_u"])
+    assert np.array_equal(got.view(np.uint32), ext["scale_q"].view(np.uint32))

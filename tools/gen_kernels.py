@@ -361,7 +361,12 @@ class RobotGen:
 def main():
     model = json.load(open(sys.argv[1]))
     g = RobotGen(model)
-    out = g.gen_sphere_fk() + "\n" + g.gen_fkcc()
+    name = g.name
+    consts = [f"// Robot::scale_configuration q * s_m + s_a (one fma per joint, pinned by ref_probe \"scale\")"]
+    for key in ("s_m", "s_a"):
+        vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model[key])
+        consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
+    out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
     open(sys.argv[2], "w").write(out)
     print(f"wrote {sys.argv[2]} ({len(out.splitlines())} lines)")
 

@@ -109,7 +109,11 @@ def make_ext_pins(rng):
     q[:, 2] = rng.uniform(0, 1, N)
     q[:, 3] = np.repeat(rng.uniform(0.01, 0.1, N // 8), 8)
     hf = probe("hf", np.concatenate([hdr, data, q.ravel()]))
-    np.savez_compressed(os.path.join(GOLD, "ref_pins_ext.npz"), sql2_in=sql2_in, sql2=sql2, box_in=box_in,
+    u = rng.random((4096, 7), dtype=F)
+    u[:2] = [[0] * 7, [1] * 7]
+    scaled = probe("scale", u).reshape(-1, 7)
+    np.savez_compressed(os.path.join(GOLD, "ref_pins_ext.npz"), scale_u=u, scale_q=scaled,
+                        sql2_in=sql2_in, sql2=sql2, box_in=box_in,
                         box_vec=box[0], box_rc=box[1], vol_distsq=box[2], vol_ball=box[3], hf_hdr=hdr,
                         hf_data=data, hf_q=q, hf=hf)
 
