@@ -41,11 +41,21 @@ __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b 
 struct Grp1 {
     static constexpr int G = 1;
     __device__ static __forceinline__ bool any(bool p) { return p; }
+    __device__ static __forceinline__ bool any_bits(uint32_t b) { return (b >> 31) != 0u; }
     __device__ static __forceinline__ float max(float v) { return v; }
 };
 
 struct Grp8 {
     static constexpr int G = 8;
+    // any lane of the group with its sign bit set (bits OR-reduced over the DPP half-row)
+    __device__ static __forceinline__ bool any_bits(uint32_t b)
+    {
+        int x = (int)b;
+        x |= dpp_i<0xB1>(x);
+        x |= dpp_i<0x4E>(x);
+        x |= dpp_i<0x141>(x);
+        return x < 0;
+    }
     __device__ static __forceinline__ bool any(bool p)
     {
         int x = p ? 1 : 0;
@@ -132,7 +142,7 @@ __device__ __forceinline__ float halton_coord(uint32_t idx, uint32_t b)
 //   cuboid   stride 16: md x y z a1x a1y a1z a2x a2y a2z a3x a3y a3z r1 r2 r3   (z-cuboid: same)
 enum : int { OBS_SPHERE = 0, OBS_CAPSULE = 1, OBS_ZCAPSULE = 2, OBS_CUBOID = 3, OBS_ZCUBOID = 4, OBS_TYPES = 5 };
 constexpr int kObsStride[OBS_TYPES] = {8, 16, 16, 16, 16};
-constexpr int kObsPad = 4;
+constexpr int kObsPad = 8;  // >= 2 * VGPU_SCAN_UNROLL - 1 (the loop's prefetch reach)
 
 struct EnvView {
     const VGPU_CONST float* obs[OBS_TYPES];
@@ -207,23 +217,38 @@ __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 // One obstacle type: evaluates records while md < emax (this lane's group prefix), two per
 // iteration, the next pair's scalar loads issued before the current pair is tested.  The
 // body is branch-free per lane; the loop exits when no lane of the wave has anything left.
+#ifndef VGPU_SCAN_UNROLL
+#define VGPU_SCAN_UNROLL 2  // records per loop trip (A/B on MI355X: 1 -> 5.15 ms, 2 -> 4.97, 4 -> 5.17)
+#endif
+static_assert(kObsPad >= 2 * VGPU_SCAN_UNROLL - 1, "sentinel padding must cover the prefetch");
 template <int TYPE, class TestFn>
-__device__ __forceinline__ void scan_type(const VGPU_CONST float* o, float emax, bool& hit, TestFn test)
+__device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float emax, uint32_t acc, TestFn test)
 {
+    // The lane state is kept as VALU bit masks (acc: sign bit = hit) instead of per-lane bools:
+    // combining divergent bools costs a 64-bit SALU op each, and the scalar unit -- shared by
+    // the waves of a SIMD -- was the busiest pipe of these kernels.
     constexpr int S = kObsStride[TYPE];
-    float md0 = o[0], md1 = o[S];
+    constexpr int U = VGPU_SCAN_UNROLL;
+    float md[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) md[u] = o[u * S];
     for (;;) {
-        const bool live0 = (md0 < emax) && !hit;
-        if (!__any(live0)) break;  // md is sorted: live1 implies live0
-        const float nmd0 = o[2 * S], nmd1 = o[3 * S];  // prefetch (sentinel-padded)
-        const bool live1 = (md1 < emax);
-        const float v0 = test(o);
-        const float v1 = test(o + S);
-        hit = hit || (live0 && signbit_f(v0)) || (live0 && live1 && signbit_f(v1));
-        o += 2 * S;
-        md0 = nmd0;
-        md1 = nmd1;
+        uint32_t live[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) live[u] = (md[u] < emax) ? 0xFFFFFFFFu : 0u;
+        if (!__any((int)(live[0] & ~acc) < 0)) break;  // md is sorted: live[u] implies live[0]
+        float nmd[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) nmd[u] = o[(U + u) * S];  // prefetch (sentinel-padded)
+        uint32_t hit = 0u;
+#pragma unroll
+        for (int u = 0; u < U; ++u) hit |= __float_as_uint(test(o + u * S)) & live[u];
+        acc |= hit;
+        o += U * S;
+#pragma unroll
+        for (int u = 0; u < U; ++u) md[u] = nmd[u];
     }
+    return acc;
 }
 
 // _mm256_max_ps / _mm256_min_ps operand semantics (a NaN first operand yields the second)
@@ -299,8 +324,10 @@ __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float
     return false;
 }
 
+// Returns acc with this lane's hits OR-ed into the sign bit.  A lane entering with its sign
+// bit already set (an earlier child hit) does not keep any obstacle loop alive.
 template <class Grp, bool EXT = false>
-__device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, float z, float r)
+__device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float y, float z, float r, uint32_t acc = 0u)
 {
     const float d = dot3(x, y, z, x, y, z);
     float me = sqrt_host(d, env.lut, env.kbits) + r;  // validity.hh:55-59
@@ -308,14 +335,13 @@ __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, f
     if (dexp == 0u || dexp == 0x7F800000u || me != me) me = __builtin_inff();
     const float emax = Grp::max(me);
     const float rsq = r * r;
-    bool hit = false;
 
     if (env.n[OBS_SPHERE])  // sphere_sphere.hh:10-22
-        scan_type<OBS_SPHERE>(env.obs[OBS_SPHERE], emax, hit, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_SPHERE>(env.obs[OBS_SPHERE], emax, acc, [&](const VGPU_CONST float* o) {
             return sphere_sphere(o[1], o[2], o[3], o[4], x, y, z, r);
         });
     if (env.n[OBS_CAPSULE])  // sphere_capsule.hh:9-22
-        scan_type<OBS_CAPSULE>(env.obs[OBS_CAPSULE], emax, hit, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_CAPSULE>(env.obs[OBS_CAPSULE], emax, acc, [&](const VGPU_CONST float* o) {
             const float dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
             const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
             const float px = __builtin_fmaf(o[4], cdf, o[1]);
@@ -326,7 +352,7 @@ __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, f
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
         });
     if (env.n[OBS_ZCAPSULE])  // sphere_capsule.hh:30-43
-        scan_type<OBS_ZCAPSULE>(env.obs[OBS_ZCAPSULE], emax, hit, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_ZCAPSULE>(env.obs[OBS_ZCAPSULE], emax, acc, [&](const VGPU_CONST float* o) {
             const float dot = (z - o[3]) * o[6];
             const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
             const float pz = __builtin_fmaf(o[6], cdf, o[3]);
@@ -335,7 +361,7 @@ __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, f
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
         });
     if (env.n[OBS_CUBOID])  // sphere_cuboid.hh:9-27
-        scan_type<OBS_CUBOID>(env.obs[OBS_CUBOID], emax, hit, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_CUBOID>(env.obs[OBS_CUBOID], emax, acc, [&](const VGPU_CONST float* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
             const float a1 = max0(__builtin_fabsf(dot3(o[4], o[5], o[6], xs, ys, zs)) - o[13]);
             const float a2 = max0(__builtin_fabsf(dot3(o[7], o[8], o[9], xs, ys, zs)) - o[14]);
@@ -343,7 +369,7 @@ __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, f
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
         });
     if (env.n[OBS_ZCUBOID])  // sphere_cuboid.hh:35-52
-        scan_type<OBS_ZCUBOID>(env.obs[OBS_ZCUBOID], emax, hit, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_ZCUBOID>(env.obs[OBS_ZCUBOID], emax, acc, [&](const VGPU_CONST float* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
             const float a1 = max0(__builtin_fabsf(dot2(o[4], o[5], xs, ys)) - o[13]);
             const float a2 = max0(__builtin_fabsf(dot2(o[7], o[8], xs, ys)) - o[14]);
@@ -351,12 +377,20 @@ __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, f
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
         });
     if constexpr (EXT) {
+        bool hit = (acc >> 31) != 0u;
         for (int i = 0; i < env.n_hf; ++i)
             if (!hit) hit = hf_lane(env.hf + kExtHdr * i, env.base, x, y, z, r);
         for (int i = 0; i < env.n_pc; ++i)
             if (!hit) hit = capt_lane(env.pc + kExtHdr * i, env.base, x, y, z, r);
+        if (hit) acc |= 0x80000000u;
     }
-    return hit;
+    return acc;
+}
+
+template <class Grp, bool EXT = false>
+__device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, float z, float r)
+{
+    return (env_bits<Grp, EXT>(env, x, y, z, r) >> 31) != 0u;
 }
 
 // sphere_sphere_self_collision (collision/validity.hh:13-44)

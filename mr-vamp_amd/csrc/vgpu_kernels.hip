@@ -23,7 +23,11 @@
 
 #include "vgpu_device.hh"
 
+#ifdef VGPU_FK_INC  // A/B builds of alternative generated code
+#include VGPU_FK_INC
+#else
 #include "gen/panda_fk.inc"
+#endif
 
 namespace vgpu {
 

@@ -24,6 +24,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 F = np.float32
+REMAT = False  # rebuild rotation matrices per check (A/B on MI355X: 5.80 -> 6.81 ms, off)
 
 
 def flit(v) -> str:
@@ -74,6 +75,17 @@ class Emitter:
 
     def raw(self, line):
         self.lines.append("    " * self.indent + line)
+
+    def opaque(self, a: SV) -> SV:
+        """A copy of a runtime value the compiler cannot see through (empty asm with a "+v"
+        constraint), so values recomputed from it are not merged back with earlier ones by
+        CSE/GVN -- rematerialisation instead of a long live range."""
+        if a.kind != "var":
+            return a
+        name = f"t{self.n}"
+        self.n += 1
+        self.lines.append("    " * self.indent + f"float {name} = {a.name}; __asm__ volatile(\"\" : \"+v\"({name}));")
+        return SV("var", name=name)
 
     # --- sv arithmetic mirroring oracle/vamp_oracle.c sv_* ---
     def mul(self, a: SV, b: SV) -> SV:
@@ -249,10 +261,20 @@ class RobotGen:
                 Q[f] = A
             P[f] = xform(E, R[p], P[p], fr["t"])
 
+        # Rotation matrices live only within one check: a frame needed again by a later check
+        # keeps its quaternion (4 values) + origin (3) and rebuilds R (9) from an opaque copy
+        # of the quaternion (bit-identical values, ~20 flops) instead of holding 12 registers
+        # across the whole hierarchy.
+        built = set()
+
         def ensure_R(f):
             ensure_frame(f)
             if f not in R:
-                R[f] = qmat(E, Q[f])
+                if f in built and REMAT:
+                    R[f] = qmat(E, tuple(E.opaque(v) for v in Q[f]))
+                else:
+                    R[f] = qmat(E, Q[f])
+                    built.add(f)
 
         bc = {}
 
@@ -269,6 +291,8 @@ class RobotGen:
                     for i in range(3)]
 
         for o in m["check_order"]:
+            if REMAT:
+                R.clear()
             if o["kind"] == "env":
                 ck = m["env_checks"][o["index"]]
                 b = links.index(ck["link"])
@@ -277,19 +301,15 @@ class RobotGen:
                     ensure_R(spheres[kid["sphere"]]["frame"])
                 w = world(bound_center(b), bd["base"])
                 E.raw(f"// env: {ck['link']} bounding sphere r={bd['radius']} (+{len(ck['children'])} children)")
-                E.raw(f"if (Grp::any(env_lane<Grp, EXT>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])}))) {{")
+                E.raw(f"if (Grp::any_bits(env_bits<Grp, EXT>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])}))) {{")
                 E.indent += 1
-                E.raw("bool h = false;")
+                E.raw("uint32_t h = 0u;  // sign bit: this lane hit (a hit lane keeps no obstacle loop alive)")
                 for kid in ck["children"]:
                     sp = spheres[kid["sphere"]]
-                    E.raw("if (!h) {")
-                    E.indent += 1
                     c = self.center(E, R, P, sp["frame"], sp["offset"])
                     cw = world(c, kid["base"])
-                    E.raw(f"h = env_lane<Grp, EXT>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])});")
-                    E.indent -= 1
-                    E.raw("}")
-                E.raw("if (Grp::any(h)) return false;")
+                    E.raw(f"h = env_bits<Grp, EXT>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])}, h);")
+                E.raw("if (Grp::any_bits(h)) return false;")
                 E.indent -= 1
                 E.raw("}")
             else:
@@ -340,8 +360,8 @@ class RobotGen:
                     E.indent -= 1
                     E.raw("}")
                     if ci + 1 < nchunks:
-                        E.raw("if (Grp::any((h >> 31) != 0u)) return false;  // early exit (work only)")
-                E.raw("if (Grp::any((h >> 31) != 0u)) return false;")
+                        E.raw("if (Grp::any_bits(h)) return false;  // early exit (work only)")
+                E.raw("if (Grp::any_bits(h)) return false;")
                 E.indent -= 1
                 E.raw("}")
         E.raw("return true;")
@@ -359,6 +379,10 @@ class RobotGen:
 
 
 def main():
+    global REMAT
+    if "--no-remat" in sys.argv:
+        REMAT = False
+        sys.argv.remove("--no-remat")
     model = json.load(open(sys.argv[1]))
     g = RobotGen(model)
     name = g.name

@@ -14,8 +14,8 @@ if [ "$2" = "pmc" ]; then
   rocprofv3 -L > gpurun_out/ab/counters.txt 2>&1 || true
   i=0
   for set in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY" \
-             "SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_SCA SQ_INST_CYCLES_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE" \
-             "SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_DCACHE_HITS SQC_DCACHE_MISSES SQ_IFETCH"; do
+             "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_INSTS_BRANCH SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE" \
+             "SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_ADD_F32 SQ_INSTS_VALU_MUL_F32 SQ_WAIT_ANY SQ_INST_CYCLES_SALU" ${PMC_EXTRA:-}; do
     i=$((i+1))
     VAMP_AMD_LIB=$PWD/$lib timeout -k 10 300 rocprofv3 --pmc $set --kernel-include-regex "panda_validate|panda_fkcc" -d gpurun_out/ab/pmc$i -o pmc --output-format csv -- python3 tools/kbench.py --edges 262144 --reps 1 --tag pmc > gpurun_out/ab/pmc$i.log 2>&1 || { echo "pmc pass $i failed"; tail -20 gpurun_out/ab/pmc$i.log; exit 1; }
   done
