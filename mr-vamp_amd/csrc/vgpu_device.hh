@@ -221,6 +221,10 @@ __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 #define VGPU_SCAN_UNROLL 2  // records per loop trip (A/B on MI355X: 1 -> 5.15 ms, 2 -> 4.97, 4 -> 5.17)
 #endif
 static_assert(kObsPad >= 2 * VGPU_SCAN_UNROLL - 1, "sentinel padding must cover the prefetch");
+template <int S>
+struct ObsRec {
+    float v[S];
+};
 template <int TYPE, class TestFn>
 __device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float emax, uint32_t acc, TestFn test)
 {
@@ -229,24 +233,31 @@ __device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float e
     // the waves of a SIMD -- was the busiest pipe of these kernels.
     constexpr int S = kObsStride[TYPE];
     constexpr int U = VGPU_SCAN_UNROLL;
+    using Rec = ObsRec<S>;  // one record: a single s_load per field group
+    const VGPU_CONST Rec* p = (const VGPU_CONST Rec*)o;
     float md[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) md[u] = o[u * S];
+    for (int u = 0; u < U; ++u) md[u] = p[u].v[0];
     for (;;) {
         uint32_t live[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) live[u] = (md[u] < emax) ? 0xFFFFFFFFu : 0u;
-        if (!__any((int)(live[0] & ~acc) < 0)) break;  // md is sorted: live[u] implies live[0]
+        // md is sorted: live[u] implies live[0].  ballot of an opaque value: otherwise
+        // instcombine folds the test back into an i1 AND, which the backend lowers as
+        // compare -> v_cndmask -> compare
+        uint32_t pend = live[0] & ~acc;
+        __asm__("" : "+v"(pend));
+        if (__builtin_amdgcn_ballot_w64((int)pend < 0) == 0) break;
         float nmd[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) nmd[u] = o[(U + u) * S];  // prefetch (sentinel-padded)
+        for (int u = 0; u < U; ++u) nmd[u] = p[U + u].v[0];  // prefetch (sentinel-padded)
         uint32_t hit = 0u;
 #pragma unroll
-        for (int u = 0; u < U; ++u) hit |= __float_as_uint(test(o + u * S)) & live[u];
-        acc |= hit;
-        o += U * S;
+        for (int u = 0; u < U; ++u) hit |= __float_as_uint(test(p[u].v)) & live[u];
 #pragma unroll
         for (int u = 0; u < U; ++u) md[u] = nmd[u];
+        acc |= hit;
+        p += U;
     }
     return acc;
 }
@@ -337,11 +348,11 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
     const float rsq = r * r;
 
     if (env.n[OBS_SPHERE])  // sphere_sphere.hh:10-22
-        acc = scan_type<OBS_SPHERE>(env.obs[OBS_SPHERE], emax, acc, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_SPHERE>(env.obs[OBS_SPHERE], emax, acc, [&](const auto* o) {
             return sphere_sphere(o[1], o[2], o[3], o[4], x, y, z, r);
         });
     if (env.n[OBS_CAPSULE])  // sphere_capsule.hh:9-22
-        acc = scan_type<OBS_CAPSULE>(env.obs[OBS_CAPSULE], emax, acc, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_CAPSULE>(env.obs[OBS_CAPSULE], emax, acc, [&](const auto* o) {
             const float dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
             const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
             const float px = __builtin_fmaf(o[4], cdf, o[1]);
@@ -352,7 +363,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
         });
     if (env.n[OBS_ZCAPSULE])  // sphere_capsule.hh:30-43
-        acc = scan_type<OBS_ZCAPSULE>(env.obs[OBS_ZCAPSULE], emax, acc, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_ZCAPSULE>(env.obs[OBS_ZCAPSULE], emax, acc, [&](const auto* o) {
             const float dot = (z - o[3]) * o[6];
             const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
             const float pz = __builtin_fmaf(o[6], cdf, o[3]);
@@ -361,7 +372,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
         });
     if (env.n[OBS_CUBOID])  // sphere_cuboid.hh:9-27
-        acc = scan_type<OBS_CUBOID>(env.obs[OBS_CUBOID], emax, acc, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_CUBOID>(env.obs[OBS_CUBOID], emax, acc, [&](const auto* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
             const float a1 = max0(__builtin_fabsf(dot3(o[4], o[5], o[6], xs, ys, zs)) - o[13]);
             const float a2 = max0(__builtin_fabsf(dot3(o[7], o[8], o[9], xs, ys, zs)) - o[14]);
@@ -369,7 +380,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
         });
     if (env.n[OBS_ZCUBOID])  // sphere_cuboid.hh:35-52
-        acc = scan_type<OBS_ZCUBOID>(env.obs[OBS_ZCUBOID], emax, acc, [&](const VGPU_CONST float* o) {
+        acc = scan_type<OBS_ZCUBOID>(env.obs[OBS_ZCUBOID], emax, acc, [&](const auto* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
             const float a1 = max0(__builtin_fabsf(dot2(o[4], o[5], xs, ys)) - o[13]);
             const float a2 = max0(__builtin_fabsf(dot2(o[7], o[8], xs, ys)) - o[14]);
