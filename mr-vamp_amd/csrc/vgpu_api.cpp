@@ -12,6 +12,7 @@
 #include <array>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -30,6 +31,27 @@ hipError_t vgpu_launch_compact(const uint8_t* valid, size_t n, uint32_t* idx_out
                                size_t tmp_bytes, hipStream_t st);
 hipError_t vgpu_launch_gather_rows(const float* q, const uint32_t* idx, const uint32_t* count, size_t max_rows,
                                    int dim, float* out, hipStream_t st);
+hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, size_t n_edges, uint32_t* item_edge,
+                                     hipStream_t st);
+int vgpu_staged_checks(void);
+hipError_t vgpu_launch_staged_bound(int kind, const void* src0, const void* src1, const void* src2, const void* src3,
+                                    uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by,
+                                    float bz, uint32_t* mask, uint8_t* valid, hipStream_t st);
+uint32_t vgpu_staged_blocks(int kind, uint32_t n_groups);
+uint32_t vgpu_staged_env_checks(void);
+hipError_t vgpu_launch_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,
+                                    const uint32_t* mask, uint32_t n_groups, uint32_t set, const uint8_t* valid,
+                                    uint32_t* counts, hipStream_t st);
+hipError_t vgpu_launch_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,
+                                    const uint32_t* mask, uint32_t n_groups, uint32_t set, const uint8_t* valid,
+                                    const uint32_t* offs, const uint32_t* seg, uint32_t* items, uint32_t n_items,
+                                    hipStream_t st);
+hipError_t vgpu_launch_staged_children(int kind, const void* src0, const void* src1, const void* src2,
+                                       const void* src3, uint64_t first, const uint32_t* seg, const uint32_t* items,
+                                       const EnvView* env, float bx, float by, float bz, uint8_t* valid,
+                                       hipStream_t st);
+hipError_t vgpu_launch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
+                                   int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
 hipError_t vgpu_launch_capt_query(const float* centers, const float* radii, size_t n, const EnvView* env, int index,
                                   int simd, uint8_t* out, hipStream_t st);
 hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float by, float bz, float* out,
@@ -145,6 +167,16 @@ struct vgpu_ctx {
     // compaction workspace (selected indices' count word + hipcub temp)
     void* aux = nullptr;
     size_t aux_bytes = 0;
+    // staged checks (vgpu_staged.hip): bounding masks, per-check counts/cursors, item list
+    bool staged = true;
+    std::vector<uint32_t> rounds;  // check sets run in order (staged); empty = chosen per batch
+    uint32_t* st_mask = nullptr;
+    size_t st_mask_cap = 0;
+    uint32_t* st_cnt = nullptr;   // per-(check, block) counts, then their exclusive scan, + scan temp
+    size_t st_cnt_cap = 0;
+    uint32_t* st_host = nullptr;  // pinned: the 33 segment boundaries of the scan
+    uint32_t* st_items = nullptr;
+    size_t st_items_cap = 0;
     // optional phase timing
     bool prof = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -201,6 +233,16 @@ extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
         return VGPU_ERR_HIP;
     }
     c->cur = c->own;
+    if (const char* s = std::getenv("VAMP_AMD_STAGED")) c->staged = std::strcmp(s, "0") != 0;
+    if (const char* s = std::getenv("VAMP_AMD_ROUNDS")) {  // A/B: comma-separated check bit masks
+        for (const char* p = s; *p;) {
+            char* end = nullptr;
+            const unsigned long v = std::strtoul(p, &end, 0);
+            if (end == p) break;
+            c->rounds.push_back((uint32_t)v);
+            p = (*end == ',') ? end + 1 : end;
+        }
+    }
     int rc = probe_host_rsqrt(c->lut, c->kbits, c->err);
     if (rc != VGPU_OK) {
         (void)hipStreamDestroy(c->own);
@@ -227,6 +269,10 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->ws) (void)hipFree(c->ws);
     if (c->items) (void)hipFree(c->items);
     if (c->aux) (void)hipFree(c->aux);
+    if (c->st_mask) (void)hipFree(c->st_mask);
+    if (c->st_cnt) (void)hipFree(c->st_cnt);
+    if (c->st_items) (void)hipFree(c->st_items);
+    if (c->st_host) (void)hipHostFree(c->st_host);
     if (c->total_host) (void)hipHostFree(c->total_host);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -675,6 +721,98 @@ extern "C" int vgpu_sphere_fk(vgpu_ctx* c, const vgpu_robot* r, const float* q, 
     return VGPU_OK;
 }
 
+// One staged pass (vgpu_staged.hip) over n groups of a source kind (0 configurations, 1 Halton
+// samples, 2 validate head, 3 validate tail): bound -> counts to host -> queue -> children.
+static int grow(vgpu_ctx* c, uint32_t** p, size_t* cap, size_t need)
+{
+    if (need <= *cap) return VGPU_OK;
+    if (*p) {
+        HIPCHK(c, hipStreamSynchronize(c->cur));
+        HIPCHK(c, hipFree(*p));
+        *p = nullptr;
+    }
+    const size_t n = std::max(need + need / 4, (size_t)1 << 16);
+    HIPCHK(c, hipMalloc((void**)p, n * sizeof(uint32_t)));
+    *cap = n;
+    return VGPU_OK;
+}
+
+static int staged_pass(vgpu_ctx* c, int kind, const void* s0, const void* s1, const void* s2, const void* s3,
+                       uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid)
+{
+    if (n == 0) return VGPU_OK;
+    if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many groups in one call (< 2^31)");
+    const int checks = vgpu_staged_checks();
+    const uint32_t W = (kind >= 2) ? 8u : 64u;  // items per wave: 64 lanes / group size
+    const size_t nb = vgpu_staged_blocks(kind, (uint32_t)n);
+    const size_t cells = (size_t)checks * nb;
+    const size_t scan_bytes = vgpu_validate_scan_bytes(cells);
+    const size_t cells_al = (cells + 1 + 63) & ~(size_t)63;
+    int rc;
+    if ((rc = grow(c, &c->st_mask, &c->st_mask_cap, n))) return rc;
+    if ((rc = grow(c, &c->st_cnt, &c->st_cnt_cap, 2 * cells_al + scan_bytes / 4 + 64))) return rc;
+    if (!c->st_host) HIPCHK(c, hipHostMalloc((void**)&c->st_host, 128 * sizeof(uint32_t), hipHostMallocDefault));
+    uint32_t* counts = c->st_cnt;
+    uint32_t* offs = c->st_cnt + cells_al;
+    void* tmp = c->st_cnt + 2 * cells_al;
+    HIPCHK(c, vgpu_launch_staged_bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, b[0], b[1], b[2], c->st_mask,
+                                       valid, c->cur));
+    const uint32_t all = checks >= 32 ? 0xFFFFFFFFu : ((1u << checks) - 1u);
+    const uint32_t env_bits = vgpu_staged_env_checks();
+    // counts of every check's fired groups (all groups are valid at this point)
+    auto count_round = [&](uint32_t set, uint32_t fired[64]) -> int {
+        HIPCHK(c, hipMemsetAsync(counts + cells, 0, sizeof(uint32_t), c->cur));
+        HIPCHK(c, vgpu_launch_staged_count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, counts, c->cur));
+        HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
+        // segment boundaries offs[k * nb], k = 0..checks (the last one is the total)
+        HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t),
+                                   checks + 1, hipMemcpyDeviceToHost, c->cur));
+        HIPCHK(c, hipStreamSynchronize(c->cur));
+        for (int k = 0; k < checks; ++k) fired[k] = c->st_host[k + 1] - c->st_host[k];
+        return VGPU_OK;
+    };
+    // queue + children for the checks of `set`, with `fired` counted under the current flags
+    auto run_round = [&](uint32_t set, const uint32_t fired[64]) -> int {
+        uint32_t seg[65];
+        seg[0] = 0;
+        for (int k = 0; k < checks; ++k) seg[k + 1] = seg[k] + (((set >> k) & 1u) ? (fired[k] + W - 1) / W * W : 0u);
+        const size_t total = seg[checks];
+        if (total == 0) return VGPU_OK;
+        int r = grow(c, &c->st_items, &c->st_items_cap, total);
+        if (r) return r;
+        HIPCHK(c, vgpu_launch_staged_queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, offs, seg,
+                                           c->st_items, (uint32_t)total, c->cur));
+        HIPCHK(c, vgpu_launch_staged_children(kind, s0, s1, s2, s3, first, seg, c->st_items, v, b[0], b[1], b[2],
+                                              valid, c->cur));
+        return VGPU_OK;
+    };
+    uint32_t fired[64];
+    if ((rc = count_round(all, fired))) return rc;
+    std::vector<uint32_t> rounds = c->rounds;
+    if (rounds.empty()) {
+        // Rounds from this batch's bounding statistics: (1) the first three environment checks
+        // that fire at all (the links that leave the base region -- they invalidate most groups
+        // cheaply), (3) self checks whose bounding spheres overlap for ~every group (adjacent
+        // links: many children, rarely a hit), (2) everything else.  Later rounds only see the
+        // groups still valid: the reference's early exit, recovered at round granularity.
+        uint32_t r1 = 0, r3 = 0;
+        for (int k = 0, taken = 0; k < checks && taken < 3; ++k)
+            if (((env_bits >> k) & 1u) && fired[k]) r1 |= 1u << k, ++taken;
+        for (int k = 0; k < checks; ++k)
+            if (!((env_bits >> k) & 1u) && fired[k] >= n - n / 100) r3 |= 1u << k;
+        rounds = {r1, all & ~r1 & ~r3, r3};
+    }
+    bool counted = true;  // `fired` is valid for the first round (no group invalidated yet)
+    for (uint32_t set : rounds) {
+        set &= all;
+        if (!set) continue;
+        if (!counted && (rc = count_round(set, fired))) return rc;
+        counted = false;
+        if ((rc = run_round(set, fired))) return rc;
+    }
+    return VGPU_OK;
+}
+
 extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n, uint8_t* valid)
 {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
@@ -685,6 +823,7 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
+    if (c->staged) return staged_pass(c, 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_fkcc(q, n, &v, b[0], b[1], b[2], valid, c->cur));
     return VGPU_OK;
 }
@@ -729,8 +868,13 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     size_t tmp_bytes;
     if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
-    HIPCHK(c, vgpu_launch_panda_validate_head(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, cnt,
-                                              c->cur));
+    if (c->staged) {
+        if ((rc = staged_pass(c, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
+        HIPCHK(c, vgpu_launch_tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
+    } else {
+        HIPCHK(c, vgpu_launch_panda_validate_head(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, cnt,
+                                                  c->cur));
+    }
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[1], c->cur));
     HIPCHK(c, vgpu_launch_scan(cnt, off, n_edges, tmp, tmp_bytes, c->cur));
     // number of back-step work items: one D2H word (the item buffer is sized from it)
@@ -745,8 +889,15 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
         c->items_cap = cap;
     }
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[2], c->cur));
-    HIPCHK(c, vgpu_launch_panda_validate_tail(starts, goals, n_edges, n_items, &v, b[0], b[1], b[2], ok, cnt, off,
-                                              c->items, c->cur));
+    if (c->staged) {
+        if (n_items) {
+            HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
+            if ((rc = staged_pass(c, 3, starts, goals, c->items, off, 0, n_items, &v, b, ok))) return rc;
+        }
+    } else {
+        HIPCHK(c, vgpu_launch_panda_validate_tail(starts, goals, n_edges, n_items, &v, b[0], b[1], b[2], ok, cnt,
+                                                  off, c->items, c->cur));
+    }
     if (c->prof) {
         HIPCHK(c, hipEventRecord(c->ev[3], c->cur));
         HIPCHK(c, hipEventSynchronize(c->ev[3]));
@@ -817,6 +968,7 @@ extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, u
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
+    if (c->staged) return staged_pass(c, 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_sample_fkcc(first, n, &v, b[0], b[1], b[2], q, valid, c->cur));
     return VGPU_OK;
 }

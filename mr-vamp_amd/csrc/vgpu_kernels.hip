@@ -21,20 +21,9 @@
 // nothing is a dense contraction worth MFMA (DESIGN.md "Why no MFMA").
 #include <hipcub/hipcub.hpp>
 
-#include "vgpu_device.hh"
-
-#ifdef VGPU_FK_INC  // A/B builds of alternative generated code
-#include VGPU_FK_INC
-#else
-#include "gen/panda_fk.inc"
-#endif
+#include "vgpu_panda.hh"
 
 namespace vgpu {
-
-#ifndef VGPU_WAVES_PER_EU
-#define VGPU_WAVES_PER_EU 7  // A/B on MI355X: 4 -> 6.84 ms, 6 -> 5.96, 7 -> 5.84, 8 -> 5.96 (validate, 1M edges)
-#endif
-constexpr int kBlock = 256;
 
 template <bool EXT>
 __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_fkcc_kernel(const float* __restrict__ q, size_t n, EnvView env,
@@ -48,15 +37,6 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_fkcc_kernel(c
 }
 
 // ---- sampling: Halton<7> draw -> scale_configuration -> fkcc (prm.hh:236-251) ----
-__device__ __forceinline__ void panda_sample(uint64_t k, float q[7])
-{
-    uint32_t idx, cyc;
-    halton_index(k, idx, cyc);
-#pragma unroll
-    for (int d = 0; d < 7; ++d)
-        q[d] = __builtin_fmaf(halton_coord(idx, kHaltonPrimes[(d + cyc) % 7u]), panda_s_m[d], panda_s_a[d]);
-}
-
 __global__ __launch_bounds__(kBlock) void panda_sample_kernel(uint64_t first, size_t n, float* __restrict__ q)
 {
     const size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x;
@@ -81,27 +61,6 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_sample_fkcc_k
         for (int d = 0; d < 7; ++d) q[7 * i + d] = v[d];
     }
     valid[i] = panda_fkcc<Grp1, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, bx, by, bz) ? 1 : 0;
-}
-
-// ---- validate_vector: shared rake arithmetic (validate.hh:31-50) ----------------------------
-struct Rake {
-    float v[7];
-    int n;
-};
-
-__device__ __forceinline__ Rake rake_setup(const float* __restrict__ s, const float* __restrict__ g)
-{
-    Rake r;
-#pragma unroll
-    for (int j = 0; j < 7; ++j) r.v[j] = g[j] - s[j];  // validate.hh:72
-    // l2_norm in the AVX hsum lane order (vector/avx.hh:441-452); lane 7 is padding 0
-    const float a = (r.v[0] * r.v[0] + r.v[4] * r.v[4]) + (r.v[2] * r.v[2] + r.v[6] * r.v[6]);
-    const float c = (r.v[1] * r.v[1] + r.v[5] * r.v[5]) + (r.v[3] * r.v[3] + 0.0f);
-    const float distance = __builtin_sqrtf(a + c);
-    float nf = __builtin_ceilf(distance / 8.0f * 32.0f);  // validate.hh:41
-    if (!(nf > 1.0f)) nf = 1.0f;
-    r.n = nf < 2147483520.0f ? (int)nf : 2147483520;
-    return r;
 }
 
 template <bool EXT>
@@ -275,6 +234,16 @@ hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goa
     else
         hipLaunchKernelGGL(vgpu::panda_validate_head_kernel<false>, dim3(grid), dim3(vgpu::kBlock), 0, st, starts,
                            goals, n_edges, *env, bx, by, bz, ok, n_blocks, cnt);
+    return hipGetLastError();
+}
+
+hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, size_t n_edges, uint32_t* item_edge,
+                                     hipStream_t st)
+{
+    if (n_edges == 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n_edges + vgpu::kBlock - 1) / vgpu::kBlock);
+    hipLaunchKernelGGL(vgpu::scatter_items_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, cnt, off, n_edges,
+                       item_edge);
     return hipGetLastError();
 }
 

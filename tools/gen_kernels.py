@@ -224,30 +224,27 @@ class RobotGen:
         ]
         return "\n".join(hdr + E.lines + ["}", ""])
 
-    def gen_fkcc(self) -> str:
-        """fkcc with lazily emitted frames (short live ranges -> fewer VGPRs) and the
-        reference's group semantics per check: a bounding test fires for the group if any
-        lane fires (Grp::any); the children's per-lane hits are OR-ed and reduced once, which
-        equals the reference's per-child `return false` (any lane, any child)."""
-        E = Emitter()
-        m = self.m
-        dim = m["dimension"]
-        frames = m["frames"]
-        spheres, bounding = m["spheres"], m["bounding"]
-        links = [b["link"] for b in bounding]
-        Q, P, R = {}, {}, {}
+    # ---------------------------------------------------------------------------------
+    class Frames:
+        """Lazily emitted frame poses (Q, P, R) and bounding centres over one Emitter."""
 
-        def ensure_frame(f):
+        def __init__(self, gen, E):
+            self.g, self.E = gen, E
+            self.Q, self.P, self.R, self.bc = {}, {}, {}, {}
+            self.built = set()
+
+        def frame(self, f):
+            Q, P, E = self.Q, self.P, self.E
             if f in Q:
                 return
-            fr = frames[f]
+            fr = self.g.m["frames"][f]
             qf = tuple(SV.const(v) for v in fr["qf"])
             if fr["parent"] < 0:
                 Q[f] = qf
                 P[f] = [SV.const(v) for v in fr["t"]]
                 return
             p = fr["parent"]
-            ensure_R(p)
+            self.rot(p)
             ident = list(fr["qf"]) == [1.0, 0.0, 0.0, 0.0]
             A = Q[p] if ident else qmul(E, Q[p], qf)
             d = fr["dof"]
@@ -259,123 +256,212 @@ class RobotGen:
                 Q[f] = qmul(E, A, (c, SV.zero(), SV.zero(), sn))
             else:
                 Q[f] = A
-            P[f] = xform(E, R[p], P[p], fr["t"])
+            P[f] = xform(E, self.R[p], P[p], fr["t"])
 
-        # Rotation matrices live only within one check: a frame needed again by a later check
-        # keeps its quaternion (4 values) + origin (3) and rebuilds R (9) from an opaque copy
-        # of the quaternion (bit-identical values, ~20 flops) instead of holding 12 registers
-        # across the whole hierarchy.
-        built = set()
-
-        def ensure_R(f):
-            ensure_frame(f)
-            if f not in R:
-                if f in built and REMAT:
-                    R[f] = qmat(E, tuple(E.opaque(v) for v in Q[f]))
+        def rot(self, f):
+            # REMAT: rotation matrices live only within one check (A/B: slower, kept off)
+            self.frame(f)
+            if f not in self.R:
+                if f in self.built and REMAT:
+                    self.R[f] = qmat(self.E, tuple(self.E.opaque(v) for v in self.Q[f]))
                 else:
-                    R[f] = qmat(E, Q[f])
-                    built.add(f)
+                    self.R[f] = qmat(self.E, self.Q[f])
+                    self.built.add(f)
 
-        bc = {}
+        def center(self, frame, off):
+            self.rot(frame)
+            return xform(self.E, self.R[frame], self.P[frame], off)
 
-        def bound_center(b):
-            if b not in bc:
-                ensure_R(bounding[b]["frame"])
-                bc[b] = self.center(E, R, P, bounding[b]["frame"], bounding[b]["offset"])
-            return bc[b]
+        def bound_center(self, b):
+            if b not in self.bc:
+                bd = self.g.m["bounding"][b]
+                self.bc[b] = self.center(bd["frame"], bd["offset"])
+            return self.bc[b]
 
-        def world(c, base):
-            if not base:
-                return [x.expr() for x in c]
-            return [f"({c[i].expr()} + {('bx', 'by', 'bz')[i]})" if c[i].kind != "zero" else ("bx", "by", "bz")[i]
-                    for i in range(3)]
+    @staticmethod
+    def world(c, base):
+        if not base:
+            return [x.expr() for x in c]
+        return [f"({c[i].expr()} + {('bx', 'by', 'bz')[i]})" if c[i].kind != "zero" else ("bx", "by", "bz")[i]
+                for i in range(3)]
 
+    def bound_test(self, fr, o):
+        """(kind, C expression) of the bounding test of check `o`: env -> bit pattern whose sign
+        is this lane's hit; self -> bool of this lane."""
+        m = self.m
+        links = [b["link"] for b in m["bounding"]]
+        if o["kind"] == "env":
+            ck = m["env_checks"][o["index"]]
+            b = links.index(ck["link"])
+            bd = m["bounding"][b]
+            w = self.world(fr.bound_center(b), bd["base"])
+            return "env", f"env_bits<Grp, EXT>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])})", ck
+        ck = m["self_checks"][o["index"]]
+        (ca, ra), (cb, rb) = self.self_ent(fr, ck["a"]), self.self_ent(fr, ck["b"])
+        return "self", (f"self_lane({ca[0].expr()}, {ca[1].expr()}, {ca[2].expr()}, {flit(ra)}, "
+                        f"{cb[0].expr()}, {cb[1].expr()}, {cb[2].expr()}, {flit(rb)})"), ck
+
+    def self_ent(self, fr, e):
+        m = self.m
+        if "sphere" in e:
+            sp = m["spheres"][e["sphere"]]
+            return fr.center(sp["frame"], sp["offset"]), sp["radius"]
+        links = [b["link"] for b in m["bounding"]]
+        bi = links.index(e["bound"])
+        return fr.bound_center(bi), m["bounding"][bi]["radius"]
+
+    def emit_children(self, E, fr, kind, ck, on_hit):
+        """Children of a fired check; `on_hit` is the statement run when any lane's child fires."""
+        spheres = self.m["spheres"]
+        if kind == "env":
+            E.raw("uint32_t h = 0u;  // sign bit: this lane hit (a hit lane keeps no obstacle loop alive)")
+            for kid in ck["children"]:
+                sp = spheres[kid["sphere"]]
+                cw = self.world(fr.center(sp["frame"], sp["offset"]), kid["base"])
+                E.raw(f"h = env_bits<Grp, EXT>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])}, h);")
+            E.raw(f"if (Grp::any_bits(h)) {on_hit}")
+            return
+        pairs = ck["children"]
+        drop = set(ck.get("unreachable", []))
+        if not drop:
+            self.emit_self_pairs(E, fr, pairs, on_hit)
+            return
+        # pairs that cannot fire while the joints between the two links stay inside the analysed
+        # range (tools/prune_pairs.py) are skipped for groups entirely inside it
+        lo, hi = self.m["reach_lo"], self.m["reach_hi"]
+        inside = " && ".join(f"q{d} >= {flit(lo[d])} && q{d} <= {flit(hi[d])}" for d in ck["reach_dofs"])
+        E.raw(f"if (Grp::any(!({inside}))) {{  // some lane outside the analysed joint range: all pairs")
+        E.indent += 1
+        self.emit_self_pairs(E, fr, pairs, on_hit)
+        E.indent -= 1
+        E.raw(f"}} else {{  // {len(pairs) - len(drop)} of {len(pairs)} pairs can fire")
+        E.indent += 1
+        self.emit_self_pairs(E, fr, [p for i, p in enumerate(pairs) if i not in drop], on_hit)
+        E.indent -= 1
+        E.raw("}")
+
+    def emit_self_pairs(self, E, fr, pairs, on_hit):
+        spheres = self.m["spheres"]
+        E.raw("{")
+        E.indent += 1
+        E.raw("uint32_t h = 0u;  // OR of the children's test-value bits: sign bit = any child fired")
+        # Child pairs in chunks of CH distinct b-spheres: the chunk's b centres stay in
+        # registers while each a-sphere centre is recomputed per chunk (bounded live set;
+        # the OR is order-independent).
+        CH = 6
+        bs = sorted(set(p[1] for p in pairs))
+        nchunks = (len(bs) + CH - 1) // CH
+        for ci in range(nchunks):
+            chunk = bs[ci * CH:(ci + 1) * CH]
+            E.raw("{")
+            E.indent += 1
+            bcen = {sb: fr.center(spheres[sb]["frame"], spheres[sb]["offset"]) for sb in chunk}
+            for sa in sorted(set(p[0] for p in pairs if p[1] in bcen)):
+                a_ = fr.center(spheres[sa]["frame"], spheres[sa]["offset"])
+                for sb in chunk:
+                    if [sa, sb] not in pairs:
+                        continue
+                    b_ = bcen[sb]
+                    E.raw(f"h |= self_bits({a_[0].expr()}, {a_[1].expr()}, {a_[2].expr()}, "
+                          f"{flit(spheres[sa]['radius'])}, {b_[0].expr()}, {b_[1].expr()}, {b_[2].expr()}, "
+                          f"{flit(spheres[sb]['radius'])});")
+            E.indent -= 1
+            E.raw("}")
+            if ci + 1 < nchunks:
+                E.raw(f"if (Grp::any_bits(h)) {on_hit}  // early exit (work only)")
+        E.raw(f"if (Grp::any_bits(h)) {on_hit}")
+        E.indent -= 1
+        E.raw("}")
+
+    def signature(self, ret, fname, extra=""):
+        dim = self.m["dimension"]
+        return [f"template <class Grp, bool EXT>",
+                f"__device__ __forceinline__ {ret} {self.name}_{fname}(",
+                f"    {extra}" + ", ".join(f"float q{i}" for i in range(dim)) + ",",
+                "    const EnvView& env, float bx, float by, float bz)",
+                "{"]
+
+    def gen_fkcc(self) -> str:
+        """Monolithic fkcc: FK emitted lazily in check order; per check the bounding test, and
+        the children only when any lane of the group fires (Grp::any), early return."""
+        E = Emitter()
+        fr = self.Frames(self, E)
+        m = self.m
         for o in m["check_order"]:
             if REMAT:
-                R.clear()
-            if o["kind"] == "env":
-                ck = m["env_checks"][o["index"]]
-                b = links.index(ck["link"])
-                bd = bounding[b]
-                for kid in ck["children"]:
-                    ensure_R(spheres[kid["sphere"]]["frame"])
-                w = world(bound_center(b), bd["base"])
-                E.raw(f"// env: {ck['link']} bounding sphere r={bd['radius']} (+{len(ck['children'])} children)")
-                E.raw(f"if (Grp::any_bits(env_bits<Grp, EXT>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])}))) {{")
-                E.indent += 1
-                E.raw("uint32_t h = 0u;  // sign bit: this lane hit (a hit lane keeps no obstacle loop alive)")
-                for kid in ck["children"]:
-                    sp = spheres[kid["sphere"]]
-                    c = self.center(E, R, P, sp["frame"], sp["offset"])
-                    cw = world(c, kid["base"])
-                    E.raw(f"h = env_bits<Grp, EXT>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])}, h);")
-                E.raw("if (Grp::any_bits(h)) return false;")
-                E.indent -= 1
-                E.raw("}")
+                fr.R.clear()
+            if o["kind"] == "env":  # children frames first (short bounding->children gap)
+                for kid in m["env_checks"][o["index"]]["children"]:
+                    fr.rot(m["spheres"][kid["sphere"]]["frame"])
             else:
-                ck = m["self_checks"][o["index"]]
-
-                def ent(e):
-                    if "sphere" in e:
-                        sp = spheres[e["sphere"]]
-                        ensure_R(sp["frame"])
-                        return self.center(E, R, P, sp["frame"], sp["offset"]), sp["radius"]
-                    bi = links.index(e["bound"])
-                    return bound_center(bi), bounding[bi]["radius"]
-
-                for sa, sb in ck["children"]:
-                    ensure_R(spheres[sa]["frame"])
-                    ensure_R(spheres[sb]["frame"])
-                (ca, ra), (cb, rb) = ent(ck["a"]), ent(ck["b"])
-                E.raw(f"// self: {ck['links'][0]} vs {ck['links'][1]} ({len(ck['children'])} children)")
-                E.raw(f"if (Grp::any(self_lane({ca[0].expr()}, {ca[1].expr()}, {ca[2].expr()}, {flit(ra)}, "
-                      f"{cb[0].expr()}, {cb[1].expr()}, {cb[2].expr()}, {flit(rb)}))) {{")
-                E.indent += 1
-                E.raw("uint32_t h = 0u;  // OR of the children's test-value bits: sign bit = any child fired")
-                # Evaluate the child pairs in chunks of CH distinct b-spheres: the chunk's b
-                # centres stay in registers while each a-sphere centre is recomputed per chunk,
-                # bounding the live set (the OR is order-independent).
-                CH = 6
-                pairs = ck["children"]
-                bs = sorted(set(p[1] for p in pairs))
-                nchunks = (len(bs) + CH - 1) // CH
-                for ci in range(nchunks):
-                    chunk = bs[ci * CH:(ci + 1) * CH]
-                    E.raw("{")
-                    E.indent += 1
-                    bcen = {}
-                    for sb in chunk:
-                        sp = spheres[sb]
-                        bcen[sb] = self.center(E, R, P, sp["frame"], sp["offset"])
-                    for sa in sorted(set(p[0] for p in pairs if p[1] in bcen)):
-                        sp = spheres[sa]
-                        a_ = self.center(E, R, P, sp["frame"], sp["offset"])
-                        for sb in chunk:
-                            if [sa, sb] not in pairs:
-                                continue
-                            b_ = bcen[sb]
-                            E.raw(f"h |= self_bits({a_[0].expr()}, {a_[1].expr()}, {a_[2].expr()}, "
-                                  f"{flit(spheres[sa]['radius'])}, {b_[0].expr()}, {b_[1].expr()}, {b_[2].expr()}, "
-                                  f"{flit(spheres[sb]['radius'])});")
-                    E.indent -= 1
-                    E.raw("}")
-                    if ci + 1 < nchunks:
-                        E.raw("if (Grp::any_bits(h)) return false;  // early exit (work only)")
-                E.raw("if (Grp::any_bits(h)) return false;")
-                E.indent -= 1
-                E.raw("}")
+                for sa, sb in m["self_checks"][o["index"]]["children"]:
+                    fr.rot(m["spheres"][sa]["frame"])
+                    fr.rot(m["spheres"][sb]["frame"])
+            kind, test, ck = self.bound_test(fr, o)
+            label = ck["link"] if kind == "env" else " vs ".join(ck["links"])
+            E.raw(f"// {kind}: {label} ({len(ck['children'])} children)")
+            if kind == "env":
+                E.raw(f"if (Grp::any_bits({test})) {{")
+            else:
+                E.raw(f"if (Grp::any({test})) {{")
+            E.indent += 1
+            self.emit_children(E, fr, kind, ck, "return false;")
+            E.indent -= 1
+            E.raw("}")
         E.raw("return true;")
-        hdr = [
-            f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
-            "// FK emitted lazily in check order; checks follow the reference hierarchy",
-            "// (link-bounding sphere first, children only when the group's bounding test fires).",
-            "template <class Grp, bool EXT>",
-            f"__device__ __forceinline__ bool {self.name}_fkcc(",
-            "    " + ", ".join(f"float q{i}" for i in range(dim)) + ",",
-            "    const EnvView& env, float bx, float by, float bz)",
-            "{",
-        ]
+        hdr = [f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
+               "// Monolithic fkcc: checks follow the reference hierarchy (link-bounding sphere first,",
+               "// children only when the group's bounding test fires)."] + self.signature("bool", "fkcc")
         return "\n".join(hdr + E.lines + ["}", ""])
+
+    def gen_staged(self) -> str:
+        """Staged fkcc (same result, see DESIGN.md "Staged checks"):
+        <robot>_bound_mask  FK + every bounding test, bit c set when check c's bounding test
+                            fires for the group (no children, no early exit);
+        <robot>_children    check c's children for one group (recomputing the frames it needs);
+                            true when any child fires.
+        valid == no check whose bounding test AND some child fire -- the reference's hierarchy
+        evaluated check by check instead of in one divergent pass."""
+        m = self.m
+        order = m["check_order"]
+        assert len(order) <= 32
+        E = Emitter()
+        fr = self.Frames(self, E)
+        E.raw("uint32_t mask = 0u;")
+        for c, o in enumerate(order):
+            kind, test, ck = self.bound_test(fr, o)
+            if kind == "env":
+                E.raw(f"if (Grp::any_bits({test})) mask |= {1 << c}u;")
+            else:
+                E.raw(f"if (Grp::any({test})) mask |= {1 << c}u;")
+        E.raw("return mask;")
+        env_bits = sum(1 << c for c, o in enumerate(order) if o["kind"] == "env")
+        out = [f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
+               f"constexpr int {self.name}_n_checks = {len(order)};",
+               f"constexpr uint32_t {self.name}_env_check_bits = {env_bits:#x}u;  // environment checks"]
+        out += self.signature("uint32_t", "bound_mask") + E.lines + ["}", ""]
+        body = []
+        for c, o in enumerate(order):
+            E = Emitter()
+            E.indent = 2
+            fr = self.Frames(self, E)
+            kind = o["kind"]
+            ck = m["env_checks"][o["index"]] if kind == "env" else m["self_checks"][o["index"]]
+            label = ck["link"] if kind == "env" else " vs ".join(ck["links"])
+            # frames first, outside the chunk scopes of emit_children
+            if kind == "env":
+                for kid in ck["children"]:
+                    fr.rot(m["spheres"][kid["sphere"]]["frame"])
+            else:
+                for sa, sb in ck["children"]:
+                    fr.rot(m["spheres"][sa]["frame"])
+                    fr.rot(m["spheres"][sb]["frame"])
+            self.emit_children(E, fr, kind, ck, "return true;")
+            body += [f"    case {c}: {{  // {kind}: {label} ({len(ck['children'])} children)"] + E.lines + \
+                    ["        return false;", "    }"]
+        out += self.signature("bool", "children", "int check, ")
+        out += ["    switch (check) {"] + body + ["    default:", "        return false;", "    }", "}", ""]
+        return "\n".join(out)
 
 
 def main():
@@ -390,7 +476,7 @@ def main():
     for key in ("s_m", "s_a"):
         vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model[key])
         consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
-    out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
+    out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc() + "\n" + g.gen_staged()
     open(sys.argv[2], "w").write(out)
     print(f"wrote {sys.argv[2]} ({len(out.splitlines())} lines)")
 

@@ -9,12 +9,16 @@ tot = collections.defaultdict(lambda: collections.defaultdict(float))
 nd = collections.defaultdict(set)
 for f in sorted(glob.glob(f"{d}/pmc*/pmc_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        k = r["Kernel_Name"].split("(")[0].split("::")[-1]
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "").replace("vgpu::", "")
         tot[k][r["Counter_Name"]] += float(r["Counter_Value"])
         nd[(k, r["Counter_Name"])].add(r["Dispatch_Id"])
 for k, v in tot.items():
     print(k)
     waves = v.get("SQ_WAVES", 0) / max(1, len(nd[(k, "SQ_WAVES")]))
+    if v.get("SQ_ACTIVE_INST_VALU"):
+        n1 = len(nd[(k, "SQ_THREAD_CYCLES_VALU")]) or 1
+        n2 = len(nd[(k, "SQ_ACTIVE_INST_VALU")]) or 1
+        print(f"  VALUUtilization(%)           {100 * (v['SQ_THREAD_CYCLES_VALU'] / n1) / ((v['SQ_ACTIVE_INST_VALU'] / n2) * 64):14.1f}")
     for c, x in sorted(v.items()):
         n = len(nd[(k, c)])
         per = x / n
