@@ -293,30 +293,23 @@ def main():
                 "parallelism": f"dp{world} (independent edge shards, no collective)",
             },
             "roofline": {
-                "kernel": "panda_validate_head_kernel",
-                "bound": "valu",
-                "achieved": achieved,
-                "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved / FP32_PEAK_TFLOPS,
-                "traffic": (tr or {}).get("head_bytes_per_launch"),
-                "algorithmic_flops_per_launch": f_head * E,
-                "algorithmic_flops_per_edge": f_head,
-                "kernel_ms": head_ms,
-                "algorithmic_bytes_per_launch": EDGE_BYTES * E,
-                "hbm_frac": EDGE_BYTES * E / (head_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "traffic_source": (tr or {}).get("source"),
-            },
-            "roofline_step": {
-                "kernels": "head + scan + scatter + tail (one vgpu_validate_motions call)",
+                "kernel": "validate_motions step: staged bound/queue/children kernels of head and tail "
+                          "(vgpu_staged.hip), one call",
                 "bound": "valu",
                 "achieved": achieved_step,
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_step / FP32_PEAK_TFLOPS,
-                "step_kernel_ms": kern_ms,
-                "phase_ms": {"head": head_ms, "scan_and_count": scan_ms, "tail": tail_ms},
+                "traffic": (tr or {}).get("step_bytes_per_call"),
+                "algorithmic_flops_per_launch": (f_head + f_tail) * E,
                 "algorithmic_flops_per_edge": f_head + f_tail,
+                "kernel_ms": kern_ms,
+                "algorithmic_bytes_per_launch": EDGE_BYTES * E,
+                "hbm_frac": EDGE_BYTES * E / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "traffic_source": (tr or {}).get("source"),
+                "phase_ms": {"head": head_ms, "scan_and_count": scan_ms, "tail": tail_ms},
+                "phase_frac": {"head": achieved / FP32_PEAK_TFLOPS,
+                               "tail": f_tail * E / (max(tail_ms, 1e-9) * 1e-3) / 1e12 / FP32_PEAK_TFLOPS},
             },
             "roofline_hbm_fk": fk_leg,
             "cpu_baseline": cpu,

@@ -36,7 +36,7 @@ hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, s
 int vgpu_staged_checks(void);
 hipError_t vgpu_launch_staged_bound(int kind, const void* src0, const void* src1, const void* src2, const void* src3,
                                     uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by,
-                                    float bz, uint32_t* mask, uint8_t* valid, hipStream_t st);
+                                    float bz, uint32_t* mask, uint8_t* valid, uint32_t* counts, hipStream_t st);
 uint32_t vgpu_staged_blocks(int kind, uint32_t n_groups);
 uint32_t vgpu_staged_env_checks(void);
 hipError_t vgpu_launch_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,
@@ -755,14 +755,16 @@ static int staged_pass(vgpu_ctx* c, int kind, const void* s0, const void* s1, co
     uint32_t* counts = c->st_cnt;
     uint32_t* offs = c->st_cnt + cells_al;
     void* tmp = c->st_cnt + 2 * cells_al;
+    HIPCHK(c, hipMemsetAsync(counts + cells, 0, sizeof(uint32_t), c->cur));
     HIPCHK(c, vgpu_launch_staged_bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, b[0], b[1], b[2], c->st_mask,
-                                       valid, c->cur));
+                                       valid, counts, c->cur));
     const uint32_t all = checks >= 32 ? 0xFFFFFFFFu : ((1u << checks) - 1u);
     const uint32_t env_bits = vgpu_staged_env_checks();
     // counts of every check's fired groups (all groups are valid at this point)
-    auto count_round = [&](uint32_t set, uint32_t fired[64]) -> int {
-        HIPCHK(c, hipMemsetAsync(counts + cells, 0, sizeof(uint32_t), c->cur));
-        HIPCHK(c, vgpu_launch_staged_count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, counts, c->cur));
+    auto count_round = [&](uint32_t set, uint32_t fired[64], bool have_counts) -> int {
+        if (!have_counts)
+            HIPCHK(c, vgpu_launch_staged_count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, counts,
+                                               c->cur));
         HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
         // segment boundaries offs[k * nb], k = 0..checks (the last one is the total)
         HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t),
@@ -787,7 +789,7 @@ static int staged_pass(vgpu_ctx* c, int kind, const void* s0, const void* s1, co
         return VGPU_OK;
     };
     uint32_t fired[64];
-    if ((rc = count_round(all, fired))) return rc;
+    if ((rc = count_round(all, fired, true))) return rc;  // the bound kernel counted every check
     std::vector<uint32_t> rounds = c->rounds;
     if (rounds.empty()) {
         // Rounds from this batch's bounding statistics: (1) the first three environment checks
@@ -806,7 +808,7 @@ static int staged_pass(vgpu_ctx* c, int kind, const void* s0, const void* s1, co
     for (uint32_t set : rounds) {
         set &= all;
         if (!set) continue;
-        if (!counted && (rc = count_round(set, fired))) return rc;
+        if (!counted && (rc = count_round(set, fired, false))) return rc;
         counted = false;
         if ((rc = run_round(set, fired))) return rc;
     }

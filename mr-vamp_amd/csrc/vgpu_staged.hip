@@ -94,17 +94,38 @@ struct GrpOf<8> {
     using T = Grp8;
 };
 
+// per-(check, block) counts of the set bits of m over the block, check-major:
+// counts[c * gridDim.x + blockIdx.x]
+__device__ __forceinline__ void block_counts(uint32_t m, uint32_t* __restrict__ counts)
+{
+    __shared__ uint32_t cnt[kChecks];
+    if (threadIdx.x < kChecks) cnt[threadIdx.x] = 0u;
+    __syncthreads();
+    uint32_t any = m;
+    for (int off = 32; off >= 1; off >>= 1) any |= __shfl_xor(any, off);
+    any = __builtin_amdgcn_readfirstlane(any);
+    for (uint32_t a = any; a; a &= a - 1u) {
+        const int c = __builtin_ctz(a);
+        const uint64_t b = __builtin_amdgcn_ballot_w64((m >> c) & 1u);
+        if (__lane_id() == 0) atomicAdd(&cnt[c], (uint32_t)__builtin_popcountll(b));
+    }
+    __syncthreads();
+    if (threadIdx.x < kChecks) counts[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
+}
+
 // ---- stage 1: bounding masks ---------------------------------------------------------------
 template <class Src, bool EXT>
 __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
                                                                           float bx, float by, float bz,
                                                                           uint32_t* __restrict__ mask,
-                                                                          uint8_t* __restrict__ valid)
+                                                                          uint8_t* __restrict__ valid,
+                                                                          uint32_t* __restrict__ counts)
 {
     using Grp = typename GrpOf<Src::G>::T;
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const uint32_t g = (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);
+    uint32_t m = 0u;
     if (g < n_groups) {  // group-uniform
         float v[7];
         src.load(g, lane, v);
@@ -114,12 +135,16 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void bound_kernel(Src sr
                 for (int j = 0; j < 7; ++j) src.q_out[7 * (size_t)g + j] = v[j];
             }
         }
-        const uint32_t m = panda_bound_mask<Grp, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, bx, by, bz);
+        m = panda_bound_mask<Grp, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, bx, by, bz);
         if (lane == 0) {
             mask[g] = m;
             if constexpr (Src::kInit) valid[src.out(g)] = 1;
         }
     }
+    // the first round's per-(check, block) counts: every group is still valid here (tail items
+    // exist only for edges that passed the head)
+    if (lane != 0) m = 0u;
+    block_counts(m, counts);
 }
 
 // ---- rounds: the fired (group, check) pairs of a set of checks, for groups still valid ----------------
@@ -145,19 +170,7 @@ __global__ __launch_bounds__(kBlock) void count_kernel(Src src, const uint32_t* 
     const size_t tid = (size_t)blockIdx.x * kBlock + threadIdx.x;
     const uint32_t g = (uint32_t)(tid / Src::G);
     const uint32_t m = round_bits(src, mask, n_groups, set, valid, g, (tid % Src::G) == 0);
-    __shared__ uint32_t cnt[kChecks];
-    if (threadIdx.x < kChecks) cnt[threadIdx.x] = 0u;
-    __syncthreads();
-    uint32_t any = m;
-    for (int off = 32; off >= 1; off >>= 1) any |= __shfl_xor(any, off);
-    any = __builtin_amdgcn_readfirstlane(any);
-    for (uint32_t a = any; a; a &= a - 1u) {
-        const int c = __builtin_ctz(a);
-        const uint64_t b = __builtin_amdgcn_ballot_w64((m >> c) & 1u);
-        if (__lane_id() == 0) atomicAdd(&cnt[c], (uint32_t)__builtin_popcountll(b));
-    }
-    __syncthreads();
-    if (threadIdx.x < kChecks) counts[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
+    block_counts(m, counts);
 }
 
 // Position of group g in check c's segment:
@@ -243,17 +256,17 @@ __global__ __launch_bounds__(kBlock) void tail_counts_kernel(const float* __rest
 namespace {
 template <class Src>
 hipError_t launch_bound(const Src& src, uint32_t n_groups, const EnvView* env, float bx, float by, float bz,
-                        uint32_t* mask, uint8_t* valid, hipStream_t st)
+                        uint32_t* mask, uint8_t* valid, uint32_t* counts, hipStream_t st)
 {
     const size_t threads = (size_t)n_groups * Src::G;
     const unsigned grid = (unsigned)((threads + vgpu::kBlock - 1) / vgpu::kBlock);
     if (n_groups == 0) return hipSuccess;
     if (env->n_hf > 0 || env->n_pc > 0)
         hipLaunchKernelGGL((vgpu::bound_kernel<Src, true>), dim3(grid), dim3(vgpu::kBlock), 0, st, src, n_groups,
-                           *env, bx, by, bz, mask, valid);
+                           *env, bx, by, bz, mask, valid, counts);
     else
         hipLaunchKernelGGL((vgpu::bound_kernel<Src, false>), dim3(grid), dim3(vgpu::kBlock), 0, st, src, n_groups,
-                           *env, bx, by, bz, mask, valid);
+                           *env, bx, by, bz, mask, valid, counts);
     return hipGetLastError();
 }
 
@@ -335,10 +348,10 @@ uint32_t vgpu_staged_blocks(int kind, uint32_t n_groups)
 
 hipError_t vgpu_launch_staged_bound(int kind, const void* s0, const void* s1, const void* s2, const void* s3,
                                     uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by,
-                                    float bz, uint32_t* mask, uint8_t* valid, hipStream_t st)
+                                    float bz, uint32_t* mask, uint8_t* valid, uint32_t* counts, hipStream_t st)
 {
     return with_source(kind, s0, s1, s2, s3, first,
-                       [&](auto src) { return launch_bound(src, n_groups, env, bx, by, bz, mask, valid, st); });
+                       [&](auto src) { return launch_bound(src, n_groups, env, bx, by, bz, mask, valid, counts, st); });
 }
 
 hipError_t vgpu_launch_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,

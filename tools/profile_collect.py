@@ -21,6 +21,8 @@ if stats:
     shutil.copy(stats[0], f"{P}/{R}_bench_kernel_stats.csv")
     print("kernel stats ->", f"{P}/{R}_bench_kernel_stats.csv")
 per = collections.defaultdict(lambda: collections.defaultdict(list))
+step_bytes = collections.defaultdict(float)
+calls = 0
 for c in ("FETCH_SIZE", "WRITE_SIZE"):
     for f in glob.glob(f"{G}/pmc_{R}_{c}/**/*counter_collection.csv", recursive=True):
         rows = list(csv.DictReader(open(f)))
@@ -28,11 +30,18 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
         name = {}
         for r in rows:
             byd[r["Dispatch_Id"]] += float(r["Counter_Value"])
-            name[r["Dispatch_Id"]] = (r["Kernel_Name"].split("(")[0].split("::")[-1], r["Grid_Size"])
+            name[r["Dispatch_Id"]] = (r["Kernel_Name"].split("(")[0].replace("void ", "").replace("vgpu::", ""),
+                                      r["Grid_Size"])
         for d, v in byd.items():
             per[name[d]][c].append(v)
+            if "sphere_fk" not in name[d][0]:
+                step_bytes[c] += v
+        if c == "FETCH_SIZE":
+            calls = sum(1 for d in byd if name[d][0].startswith("bound_kernel<SrcHead")) or \
+                sum(1 for d in byd if name[d][0].startswith("panda_validate_head_kernel"))
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes (tools/profile_round.sh {R}), "
-                  "kbench 2^20-edge cage workload; bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
+                  "bench.py 2^20-edge cage workload, every validate_motions kernel; "
+                  "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
                   "(MI355X_MICROARCH.md: FETCH_SIZE reads 1/2 of a wide streaming read on gfx950; "
                   "uncalibrated for other access widths)", "kernels": {}}
 for (k, grid), d in per.items():
@@ -41,8 +50,8 @@ for (k, grid), d in per.items():
     rec = {"grid": int(grid), "fetch_kb": f, "write_kb": w, "bytes_corrected": (2 * f + w) * 1024,
            "bytes_raw": (f + w) * 1024}
     out["kernels"].setdefault(k, []).append(rec)
-heads = [r for r in out["kernels"].get("panda_validate_head_kernel", []) if r["grid"] == 8 * (1 << 20)]
-if heads:
-    out["head_bytes_per_launch"] = heads[0]["bytes_corrected"]
+if calls:
+    out["validate_calls"] = calls
+    out["step_bytes_per_call"] = (2 * step_bytes["FETCH_SIZE"] + step_bytes["WRITE_SIZE"]) * 1024 / calls
 json.dump(out, open(f"{P}/traffic_{R}.json", "w"), indent=1)
 print(json.dumps(out, indent=1)[:2000])
