@@ -113,7 +113,28 @@ float vo_capt_box_vec(const float c[3], const float lo[3], const float up[3]);
 float vo_capt_vol_distsq(const float p[3], const float lo[3], const float up[3]);
 float vo_capt_vol_ball(const float p[3], const float lo[3], const float up[3]);
 
-/* ---- Panda (robots/panda_base.hh, robots/panda/fk.hh) ---- */
+/* ---- robots ---- */
+/* robot ids (same values as the product's VGPU_ROBOT_*): Panda = PandaBase<X100,Y100,Z100>
+ * (robots/panda_base.hh:15-75), Fetch (robots/fetch.hh:8-48, 8 dof, no base offset) */
+#define VO_ROBOT_PANDA 1
+#define VO_ROBOT_FETCH 2
+int vo_robot_dim(int robot);
+int vo_robot_nspheres(int robot);
+float vo_l2_norm(const float *v, int dim);                                   /* dim <= 8 */
+void vo_robot_scale(int robot, float *q);                                    /* scale_configuration */
+void vo_robot_sphere_fk(int robot, const float *q, int bx100, int by100, int bz100, float out_xyz[][3]);
+/* q is [G][dim]; returns 1 = valid */
+int vo_robot_fkcc_block(int robot, const vo_env *env, const float *q, int G, int bx100, int by100, int bz100,
+                        vo_stats *stats);
+int vo_robot_validate_motion(int robot, const vo_env *env, const float *start, const float *goal, int bx100,
+                             int by100, int bz100, int *n_out, vo_stats *stats);
+void vo_robot_fkcc_configs(int robot, const vo_env *env, const float *q, size_t n, int bx100, int by100,
+                           int bz100, uint8_t *valid, int threads);
+void vo_robot_validate_motions(int robot, const vo_env *env, const float *starts, const float *goals,
+                               size_t n_edges, int bx100, int by100, int bz100, uint8_t *ok, int32_t *n_out,
+                               int threads);
+
+/* ---- Panda (robots/panda_base.hh, robots/panda/fk.hh): wrappers of the vo_robot_* calls ---- */
 void vo_panda_scale(float q[7]);                                               /* fk.hh:34-37 */
 void vo_panda_sphere_fk(const float q[7], int bx100, int by100, int bz100,
                         float out_xyz[][3]);                                    /* fk.hh:104-1333 */

@@ -107,6 +107,20 @@ def lib():
         L.vo_capt_collides_batch.argtypes = [C.POINTER(VoCapt), F32P, F32P, C.c_size_t, C.c_int, U8P,
                                              C.POINTER(C.c_double)]
         L.vo_panda_scale.argtypes = [F32P]
+        L.vo_robot_scale.argtypes = [C.c_int, F32P]
+        L.vo_robot_sphere_fk.argtypes = [C.c_int, F32P, C.c_int, C.c_int, C.c_int, F32P]
+        L.vo_robot_fkcc_block.restype = C.c_int
+        L.vo_robot_fkcc_block.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.POINTER(VoStats)]
+        L.vo_robot_validate_motion.restype = C.c_int
+        L.vo_robot_validate_motion.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, F32P, C.c_int, C.c_int, C.c_int,
+                                               C.POINTER(C.c_int), C.POINTER(VoStats)]
+        L.vo_robot_fkcc_configs.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, C.c_size_t, C.c_int, C.c_int, C.c_int,
+                                            U8P, C.c_int]
+        L.vo_robot_validate_motions.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, F32P, C.c_size_t, C.c_int,
+                                                C.c_int, C.c_int, U8P, I32P, C.c_int]
+        L.vo_l2_norm.restype = C.c_float
+        L.vo_l2_norm.argtypes = [F32P, C.c_int]
         _lib = L
     return _lib
 
@@ -331,3 +345,89 @@ def validate_flops(env: Env, starts, goals, base100=(0, 0, 0)):
         L.vo_panda_validate_motion_split(C.byref(ce), fp(s), fp(g), *base100, C.byref(n), C.byref(h), C.byref(t))
         head[i], tail[i] = h.flops, t.flops
     return head, tail
+
+
+# ---- robot-generic views (robot = "panda" | "fetch"; ids match VGPU_ROBOT_*) ----
+ROBOTS = {"panda": (1, 7, 59), "fetch": (2, 8, 111)}
+
+
+def robot_scale(robot, u):
+    rid, dim, _ = ROBOTS[robot]
+    q = np.ascontiguousarray(u, np.float32).reshape(-1, dim).copy()
+    for i in range(q.shape[0]):
+        lib().vo_robot_scale(rid, fp(q[i]))
+    return q
+
+
+def robot_sphere_fk(robot, q, base100=(0, 0, 0)):
+    rid, dim, ns = ROBOTS[robot]
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, dim)
+    out = np.zeros((q.shape[0], ns, 3), np.float32)
+    for i in range(q.shape[0]):
+        lib().vo_robot_sphere_fk(rid, fp(q[i]), *base100, fp(out[i]))
+    return out
+
+
+def robot_fkcc(robot, env: Env, q, base100=(0, 0, 0), G=1, stats=False):
+    rid, dim, _ = ROBOTS[robot]
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, dim)
+    N = q.shape[0]
+    assert N % G == 0
+    ce = env.c()
+    res = np.zeros(N // G, bool)
+    tm = np.zeros(N // G)
+    cm = np.zeros(N // G)
+    fl = np.zeros(N // G)
+    for i in range(N // G):
+        st = VoStats(np.inf, np.inf, 0.0)
+        res[i] = lib().vo_robot_fkcc_block(rid, C.byref(ce), fp(q[i * G:(i + 1) * G]), G, *base100, C.byref(st))
+        tm[i], cm[i], fl[i] = st.test_margin, st.cull_margin, st.flops
+    return (res, tm, cm, fl) if stats else res
+
+
+def robot_fkcc_threads(robot, env: Env, q, base100=(0, 0, 0), threads=8):
+    rid, dim, _ = ROBOTS[robot]
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, dim)
+    out = np.zeros(q.shape[0], np.uint8)
+    ce = env.c()
+    lib().vo_robot_fkcc_configs(rid, C.byref(ce), fp(q), q.shape[0], *base100, out.ctypes.data_as(U8P), threads)
+    return out.astype(bool)
+
+
+def robot_validate_motions(robot, env: Env, starts, goals, base100=(0, 0, 0), threads=8):
+    rid, dim, _ = ROBOTS[robot]
+    s = np.ascontiguousarray(starts, np.float32).reshape(-1, dim)
+    g = np.ascontiguousarray(goals, np.float32).reshape(-1, dim)
+    ok = np.zeros(s.shape[0], np.uint8)
+    n = np.zeros(s.shape[0], np.int32)
+    ce = env.c()
+    lib().vo_robot_validate_motions(rid, C.byref(ce), fp(s), fp(g), s.shape[0], *base100, ok.ctypes.data_as(U8P),
+                                    n.ctypes.data_as(I32P), threads)
+    return ok.astype(bool), n
+
+
+def mbm_env(scene: dict) -> Env:
+    """A MotionBenchMaker scene (resources/<robot>/problems.tar.bz2 scene*.yaml) as an
+    environment: boxes -> cuboids by the RESOLVED axes of the pose quaternion (columns of its
+    rotation matrix, float64 -> float32), half extents = dimensions / 2; cylinders -> capsules by
+    endpoints centre -+ axis_z * length / 2 (src/vamp/__init__.py:135-184 routes cylinders to
+    capsules and boxes to cuboids; its Euler -> Eigen axes step is restated, parity unpinned,
+    which is why fixtures carry the resolved rows)."""
+    e = Env()
+    for obj in scene["world"]["collision_objects"]:
+        for prim, pose in zip(obj["primitives"], obj["primitive_poses"]):
+            x, y, z, w = pose["orientation"]
+            R = np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                          [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                          [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+            c = np.array(pose["position"], np.float64)
+            if prim["type"] == "box":
+                h = np.array(prim["dimensions"], np.float64) / 2
+                e.add_cuboid_axes(c, R[:, 0], R[:, 1], R[:, 2], h)
+            elif prim["type"] == "cylinder":
+                length, radius = prim["dimensions"]
+                a = R[:, 2] * (length / 2)
+                e.add_capsule_endpoints(c - a, c + a, np.float32(radius))
+            elif prim["type"] == "sphere":
+                e.add_sphere(c, np.float32(prim["dimensions"][0]))
+    return e

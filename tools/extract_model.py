@@ -37,17 +37,35 @@ def collect_calls(ast, Q, base100):
     return calls
 
 
-def extract_panda(ref):
-    urdf = f"{ref}/resources/panda/panda_spherized.urdf"
-    fkhh = f"{ref}/src/impl/vamp/robots/panda/fk.hh"
+# Per-robot sources: spherized URDF (the file the reference's FK generator consumed), generated
+# fk.hh, root link, and the robot struct's resolution (robots/panda_base.hh:21, robots/fetch.hh:13).
+ROBOTS = {
+    "panda": dict(urdf="resources/panda/panda_spherized.urdf", fk="src/impl/vamp/robots/panda/fk.hh",
+                  root="panda_link0", resolution=32, has_base=True),
+    "fetch": dict(urdf="resources/fetch/fetch_spherized.urdf", fk="src/impl/vamp/robots/fetch/fk.hh",
+                  root="base_link", resolution=32, has_base=False),
+}
+
+
+def parse_const_array(src, name):
+    m = re.search(name + r"\{([^}]*)\}", src)
+    return [float(v.strip().rstrip("f")) for v in m.group(1).split(",")]
+
+
+def extract_robot(ref, robot):
+    cfg = ROBOTS[robot]
+    urdf = f"{ref}/{cfg['urdf']}"
+    fkhh = f"{ref}/{cfg['fk']}"
     src = open(fkhh).read()
     links, joints = rm.parse_urdf(urdf)
-    frames = rm.build_frames(links, joints, "panda_link0")
+    frames = rm.build_frames(links, joints, cfg["root"])
     fname = [f["name"] for f in frames]
     fk = fi.parse_function(src, r"inline void sphere_fk\(")
     cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
     cc_text = fi.function_body(src, r"inline bool interleaved_sphere_fk\(")
-    labels = re.findall(r"if \(/\*(.*?)\*/", cc_text)
+    # top-level checks in text order: the generator's link label, or None for an unlabeled
+    # single-sphere link tested directly (a leaf: its hit is a collision, no children)
+    labels = [m.group(2) for m in re.finditer(r"^        if \((/\*(.*?)\*/)?", cc_text, re.M)]
 
     rng = np.random.default_rng(12345)
     K = 8
@@ -105,9 +123,18 @@ def extract_panda(ref):
         c = calls0[t]
         if c["kind"] != "env":
             continue
+        pts = np.stack(c["args"][:3]).T
+        if lab is None:  # leaf: one sphere, `return false` on a hit (fetch/fk.hh torso_lift_link_collision_2)
+            s = sphere_at(pts, float(c["args"][3][0]))
+            assert s is not None and not any(cc_["parent"] == t for cc_ in calls0)
+            link = spheres[s]["link"]
+            b = dict(link=link, frame=spheres[s]["frame"], offset=spheres[s]["offset"], radius=spheres[s]["radius"],
+                     base=has_base(t, range(3)), leaf_sphere=s)
+            bounding[link] = b
+            env_checks.append(dict(link=link, bounding_base=b["base"], children=[], leaf=True))
+            continue
         link = lab.strip()
         fidx = fname.index(link)
-        pts = np.stack(c["args"][:3]).T
         loc, spread = local_in(fidx, pts)
         assert spread < 2e-6, (link, spread)
         r = float(c["args"][3][0])
@@ -137,7 +164,8 @@ def extract_panda(ref):
     for t, lab in zip(top, labels):
         c = calls0[t]
         if c["kind"] == "env":
-            order.append(dict(kind="env", index=[e["link"] for e in env_checks].index(lab.strip())))
+            lk = lab.strip() if lab is not None else spheres[sphere_at(np.stack(c["args"][:3]).T, float(c["args"][3][0]))]["link"]
+            order.append(dict(kind="env", index=[e["link"] for e in env_checks].index(lk)))
             continue
         a_link, b_link = [s.strip() for s in lab.split("vs.")]
         pa, pb = np.stack(c["args"][:3]).T, np.stack(c["args"][4:7]).T
@@ -154,18 +182,25 @@ def extract_panda(ref):
         order.append(dict(kind="self", index=len(self_checks) - 1))
 
     dof_frames = [f for f in frames if f["dof"] >= 0]
+    s_m = parse_const_array(src, "s_m_a")
+    s_a = parse_const_array(src, "s_a_a")
+    d_m = parse_const_array(src, "d_m_a")
+    space = float(re.search(r"space_measure\(\) noexcept -> float\s*\{\s*return ([0-9.e+-]+);", src).group(1))
+    assert len(s_m) == len(dof_frames)
     model = dict(
-        robot="panda",
-        source=dict(urdf="resources/panda/panda_spherized.urdf", fk="src/impl/vamp/robots/panda/fk.hh"),
+        robot=robot,
+        source=dict(urdf=cfg["urdf"], fk=cfg["fk"]),
         dimension=len(dof_frames),
-        resolution=32,  # robots/panda_base.hh:21
-        # scale_configuration: q * s_m + s_a (robots/panda/fk.hh:14-37); descale (fk.hh:39-62)
-        s_m=[5.9342, 3.6652, 5.9342, 3.2289, 5.9342, 3.9095999999999997, 5.9342],
-        s_a=[-2.9671, -1.8326, -2.9671, -3.1416, -2.9671, -0.0873, -2.9671],
-        d_m=[0.1685147113342995, 0.2728364072901888, 0.1685147113342995, 0.30970299482796, 0.1685147113342995,
-             0.25578064252097404, 0.1685147113342995],
-        space_measure=878819.1112640093,
-        frames=[dict(name=f["name"], parent=f["parent"], t=f["t"], qf=f["qf"], dof=f["dof"]) for f in frames],
+        resolution=cfg["resolution"],
+        # scale_configuration: q * s_m + s_a; descale (q - s_a) * d_m (fk.hh s_m_a/s_a_a/d_m_a arrays)
+        s_m=s_m,
+        s_a=s_a,
+        d_m=d_m,
+        space_measure=space,
+        frames=[dict(name=f["name"], parent=f["parent"], t=f["t"], qf=f["qf"], dof=f["dof"],
+                     **({} if f["jtype"] in ("fixed", "root") or (f["jtype"] != "prismatic" and f["axis"] == [0.0, 0.0, 1.0])
+                        else dict(jtype=f["jtype"], axis=f["axis"])))
+                for f in frames],
         spheres=spheres,
         bounding=list(bounding.values()),
         env_checks=env_checks,
@@ -178,9 +213,12 @@ def extract_panda(ref):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
-    ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "model", "panda.json"))
+    ap.add_argument("--robot", default="panda", choices=sorted(ROBOTS))
+    ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    m = extract_panda(a.ref)
+    if a.out is None:
+        a.out = os.path.join(os.path.dirname(__file__), "..", "model", f"{a.robot}.json")
+    m = extract_robot(a.ref, a.robot)
     with open(a.out, "w") as f:
         json.dump(m, f, indent=1)
     print(f"wrote {a.out}: {len(m['spheres'])} spheres, {len(m['env_checks'])} env checks "

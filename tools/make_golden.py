@@ -125,10 +125,11 @@ def sphere_cage():
 
 def interp_validate(cc, starts, goals, base, envnp, rs):
     """validate_motion (planning/validate.hh:23-75) over E edges, 8-lane groups."""
-    E = starts.shape[0]
+    E, D = starts.shape
     v = (goals - starts).astype(F)
-    sq = (v * v).astype(F)
-    dist = np.sqrt((((sq[:, 0] + sq[:, 4]) + (sq[:, 2] + sq[:, 6])) + ((sq[:, 1] + sq[:, 5]) + (sq[:, 3] + F(0))))
+    sq = np.zeros((E, 8), F)
+    sq[:, :D] = (v * v).astype(F)
+    dist = np.sqrt((((sq[:, 0] + sq[:, 4]) + (sq[:, 2] + sq[:, 6])) + ((sq[:, 1] + sq[:, 5]) + (sq[:, 3] + sq[:, 7])))
                    .astype(F)).astype(F)
     n = np.maximum(np.ceil((dist / F(8) * F(32)).astype(F)), F(1)).astype(np.int64)
     pct = (np.arange(1, 9, dtype=F) / F(8)).astype(F)
@@ -144,7 +145,7 @@ def interp_validate(cc, starts, goals, base, envnp, rs):
         idx = np.where(alive & (n > k))[0]
         if len(idx) == 0:
             break
-        q = block[idx].reshape(-1, 7)
+        q = block[idx].reshape(-1, D)
         valid, st = fi.run_fkcc(cc, q, base, envnp, rs, G=8)
         valid = valid.reshape(-1, 8)[:, 0]
         tmarg[idx] = np.minimum(tmarg[idx], st.test_margin.reshape(-1, 8).min(1))
@@ -154,8 +155,70 @@ def interp_validate(cc, starts, goals, base, envnp, rs):
     return ok, n, tmarg, cmarg
 
 
+def mbm_scene(robot, name):
+    import tarfile
+
+    import yaml
+    with tarfile.open(f"/root/reference/resources/{robot}/problems.tar.bz2") as t:
+        return yaml.safe_load(t.extractfile(f"problems/{name}").read().decode())
+
+
+def envnp_of(env):
+    a = env.arrays()
+    return fi.EnvNP(spheres=a["spheres"], capsules=a["capsules"], zcapsules=a["zcapsules"], cuboids=a["cuboids"],
+                    zcuboids=a["zcuboids"])
+
+
+def make_fetch(rng):
+    """Fetch (robots/fetch.hh, 8 dof): FK centres, per-configuration masks and edges on the
+    empty scene and MotionBenchMaker table_pick_fetch scene0001, from the reference's generated
+    fetch/fk.hh evaluated by tools/fkhh_interp.py."""
+    src = open("/root/reference/src/impl/vamp/robots/fetch/fk.hh").read()
+    fk = fi.parse_function(src, r"inline void sphere_fk\(")
+    cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
+    lut, kb = op.rsqrt_probe()
+    rs = fi.RsqrtHost(lut, kb)
+    q = op.robot_scale("fetch", rng.random((1024, 8), dtype=F))
+    xyz, r = fi.run_sphere_fk(fk, q, (0, 0, 0))
+    np.savez_compressed(os.path.join(GOLD, "fk_fetch.npz"), q=q, radii=r.astype(F),
+                        xyz=np.ascontiguousarray(np.transpose(xyz, (2, 1, 0))))
+    print("fk_fetch.npz")
+    env = op.mbm_env(mbm_scene("fetch", "table_pick_fetch/scene0001.yaml"))
+    arr = env.arrays()
+    envnp = envnp_of(env)
+    empty = fi.EnvNP(spheres=np.zeros((0, 5), F))
+    q = op.robot_scale("fetch", rng.random((16384, 8), dtype=F))
+    valid, st = fi.run_fkcc(cc, q, (0, 0, 0), envnp, rs, G=1)
+    qe = op.robot_scale("fetch", rng.random((4096, 8), dtype=F))
+    valid_e, st_e = fi.run_fkcc(cc, qe, (0, 0, 0), empty, rs, G=1)
+    # edges: raw pairs (short) and valid-endpoint pairs capped at length 1.0
+    E = 1024
+    s = op.robot_scale("fetch", rng.random((E, 8), dtype=F))
+    g = op.robot_scale("fetch", rng.random((E, 8), dtype=F))
+    g = (s + (g - s) * F(0.25)).astype(F)
+    vq = q[valid]
+    sb, gb = vq[0:2 * E:2][:E], vq[1:2 * E:2][:E]
+    d = np.linalg.norm((gb - sb).astype(np.float64), axis=1)
+    sc = np.minimum(1.0, 1.0 / np.maximum(d, 1e-9)).astype(F)
+    gb = (sb + (gb - sb) * sc[:, None]).astype(F)
+    starts = np.concatenate([s, sb])
+    goals = np.concatenate([g, gb])
+    starts[:4] = goals[:4]
+    ok, n, tm, cm = interp_validate(cc, starts, goals, (0, 0, 0), envnp, rs)
+    np.savez_compressed(os.path.join(GOLD, "fetch_table_pick.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
+                        **{"env_" + k: v for k, v in arr.items()},
+                        q=q, valid=valid, test_margin=st.test_margin.astype(F), cull_margin=st.cull_margin.astype(F),
+                        q_empty=qe, valid_empty=valid_e, test_margin_empty=st_e.test_margin.astype(F),
+                        starts=starts, goals=goals, ok=ok, n=n.astype(np.int32), edge_test_margin=tm.astype(F),
+                        edge_cull_margin=cm.astype(F))
+    print("fetch_table_pick.npz", valid.mean(), valid_e.mean(), ok[:E].mean(), ok[E:].mean(), n.max())
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
+    if "--fetch" in sys.argv:
+        make_fetch(np.random.default_rng(20261016))
+        return
     if not os.path.exists(PROBE):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "ref"])
     rng = np.random.default_rng(20251015)

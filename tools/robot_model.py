@@ -126,15 +126,17 @@ def build_frames(links, joints, root_link):
                 continue
             qf = [round_const(v) for v in rpy_to_quat(*j["rpy"])]
             d = -1
-            if j["type"] in ("revolute", "continuous"):
-                assert j["axis"] == [0.0, 0.0, 1.0], f"only z-axis revolute joints supported ({j['name']})"
+            axis = [0.0, 0.0, 0.0]
+            if j["type"] in ("revolute", "continuous", "prismatic"):
+                # unit coordinate axes (+-x, +-y, +-z): the joint quaternion / displacement keeps
+                # the other two components structurally zero
+                assert sorted(abs(v) for v in j["axis"]) == [0.0, 0.0, 1.0], f"axis {j['axis']} ({j['name']})"
+                axis = [float(v) for v in j["axis"]]
                 d = dof
                 dof += 1
-            elif j["type"] == "prismatic":
-                raise NotImplementedError("prismatic joints")
             frames.append(
-                dict(name=c, parent=idx[ln], t=[float(v) for v in j["xyz"]], qf=qf, dof=d, jtype=j["type"],
-                     lower=j["lower"], upper=j["upper"])
+                dict(name=c, parent=idx[ln], t=[float(v) for v in j["xyz"]], qf=qf, dof=d,
+                     jtype=j["type"] if d >= 0 else "fixed", axis=axis, lower=j["lower"], upper=j["upper"])
             )
             idx[c] = len(frames) - 1
             order.append(c)
@@ -153,10 +155,14 @@ def fk_exact(frames, q):
             continue
         qp, pp = Q[f["parent"]], P[f["parent"]]
         qc = qmul(qp, tuple(f["qf"]))
-        if f["dof"] >= 0:
-            th = q[f["dof"]]
-            qc = qmul(qc, (math.cos(th / 2), 0.0, 0.0, math.sin(th / 2)))
         pc = pp + qmat(qp) @ np.array(f["t"])
+        if f["dof"] >= 0 and f.get("jtype") == "prismatic":
+            pc = pc + qmat(qc) @ (q[f["dof"]] * np.array(f["axis"]))
+        elif f["dof"] >= 0:
+            th = q[f["dof"]]
+            ax = f.get("axis", [0.0, 0.0, 1.0])
+            s = math.sin(th / 2)
+            qc = qmul(qc, (math.cos(th / 2), s * ax[0], s * ax[1], s * ax[2]))
         Q.append(qc)
         P.append(pc)
     return Q, P
