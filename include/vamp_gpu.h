@@ -43,6 +43,9 @@ typedef struct vgpu_env vgpu_env;
  * (robots/panda_base.hh:15-75); the fork's default vamp::robots::Panda is base (200, 200, 0)
  * (robots/panda_grid.hh:39). */
 #define VGPU_ROBOT_PANDA 1
+/* kind = VGPU_ROBOT_FETCH reproduces vamp::robots::Fetch (robots/fetch.hh:8-48): 8 dof (prismatic
+ * torso + 7 revolute), 111 spheres, resolution 32, no base offset (base_*100 must be 0). */
+#define VGPU_ROBOT_FETCH 2
 typedef struct vgpu_robot {
     int32_t kind;
     int32_t base_x100, base_y100, base_z100;

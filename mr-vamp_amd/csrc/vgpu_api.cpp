@@ -58,6 +58,17 @@ hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float
                                        size_t ld, hipStream_t st);
 hipError_t vgpu_launch_panda_fkcc(const float* q, size_t n, const EnvView* env, float bx, float by, float bz,
                                   uint8_t* valid, hipStream_t st);
+hipError_t vgpu_launch_fetch_sphere_fk(const float* q, size_t n, float* out, size_t ld, hipStream_t st);
+hipError_t vgpu_launch_fetch_fkcc(const float* q, size_t n, const EnvView* env, uint8_t* valid, hipStream_t st);
+hipError_t vgpu_launch_fetch_sample(uint64_t first, size_t n, float* q, hipStream_t st);
+hipError_t vgpu_launch_fetch_sample_fkcc(uint64_t first, size_t n, const EnvView* env, float* q, uint8_t* valid,
+                                         hipStream_t st);
+hipError_t vgpu_launch_fetch_validate_head(const float* starts, const float* goals, size_t n_edges,
+                                           const EnvView* env, uint8_t* ok, int32_t* n_blocks, uint32_t* cnt,
+                                           hipStream_t st);
+hipError_t vgpu_launch_fetch_validate_tail(const float* starts, const float* goals, size_t n_items,
+                                           const EnvView* env, uint8_t* ok, const uint32_t* off,
+                                           const uint32_t* item_edge, hipStream_t st);
 size_t vgpu_validate_scan_bytes(size_t n_edges);
 hipError_t vgpu_launch_scan(const uint32_t* cnt, uint32_t* off, size_t n_edges, void* scan_tmp, size_t scan_bytes,
                             hipStream_t st);
@@ -75,6 +86,9 @@ namespace {
 constexpr int kPandaDim = 7;
 constexpr int kPandaResolution = 32;  // robots/panda_base.hh:21
 constexpr int kPandaSpheres = 59;     // robots/panda/fk.hh:93
+constexpr int kFetchDim = 8;          // robots/fetch.hh:12
+constexpr int kFetchResolution = 32;  // robots/fetch.hh:13
+constexpr int kFetchSpheres = 111;    // robots/fetch/fk.hh:104
 
 inline uint32_t f2u(float f)
 {
@@ -691,6 +705,12 @@ static EnvView make_view(const vgpu_env* e)
 // ---------------------------------------------------------------------------------------
 extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t* ns)
 {
+    if (kind == VGPU_ROBOT_FETCH) {
+        if (dim) *dim = kFetchDim;
+        if (res) *res = kFetchResolution;
+        if (ns) *ns = kFetchSpheres;
+        return VGPU_OK;
+    }
     if (kind != VGPU_ROBOT_PANDA) return VGPU_ERR_UNSUPPORTED;
     if (dim) *dim = kPandaDim;
     if (res) *res = kPandaResolution;
@@ -701,6 +721,12 @@ extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t
 static int check_robot(vgpu_ctx* c, const vgpu_robot* r, float base[3])
 {
     if (!r) return fail(c, VGPU_ERR_INVALID_ARG, "null robot");
+    if (r->kind == VGPU_ROBOT_FETCH) {  // robots/fetch.hh: no base offset
+        if (r->base_x100 || r->base_y100 || r->base_z100)
+            return fail(c, VGPU_ERR_INVALID_ARG, "Fetch has no base offset (robots/fetch.hh)");
+        base[0] = base[1] = base[2] = 0.0f;
+        return VGPU_OK;
+    }
     if (r->kind != VGPU_ROBOT_PANDA) return fail(c, VGPU_ERR_UNSUPPORTED, "unsupported robot kind");
     // robots/panda/fk.hh:109-111: static_cast<float>(base_x100) / 100.0f
     base[0] = (float)r->base_x100 / 100.0f;
@@ -717,6 +743,10 @@ extern "C" int vgpu_sphere_fk(vgpu_ctx* c, const vgpu_robot* r, const float* q, 
     if (rc) return rc;
     if (n && (!q || !xyz || ld < n)) return fail(c, VGPU_ERR_INVALID_ARG, "bad sphere_fk arguments");
     HIPCHK(c, hipSetDevice(c->device));
+    if (r->kind == VGPU_ROBOT_FETCH) {
+        HIPCHK(c, vgpu_launch_fetch_sphere_fk(q, n, xyz, ld, c->cur));
+        return VGPU_OK;
+    }
     HIPCHK(c, vgpu_launch_panda_sphere_fk(q, n, b[0], b[1], b[2], xyz, ld, c->cur));
     return VGPU_OK;
 }
@@ -825,6 +855,10 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
+    if (r->kind == VGPU_ROBOT_FETCH) {
+        HIPCHK(c, vgpu_launch_fetch_fkcc(q, n, &v, valid, c->cur));
+        return VGPU_OK;
+    }
     if (c->staged) return staged_pass(c, 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_fkcc(q, n, &v, b[0], b[1], b[2], valid, c->cur));
     return VGPU_OK;
@@ -869,8 +903,11 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     void* tmp;
     size_t tmp_bytes;
     if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
+    const bool fetch = r->kind == VGPU_ROBOT_FETCH;  // monolithic head/tail kernels
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
-    if (c->staged) {
+    if (fetch) {
+        HIPCHK(c, vgpu_launch_fetch_validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
+    } else if (c->staged) {
         if ((rc = staged_pass(c, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
         HIPCHK(c, vgpu_launch_tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
     } else {
@@ -891,7 +928,12 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
         c->items_cap = cap;
     }
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[2], c->cur));
-    if (c->staged) {
+    if (fetch) {
+        if (n_items) {
+            HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
+            HIPCHK(c, vgpu_launch_fetch_validate_tail(starts, goals, n_items, &v, ok, off, c->items, c->cur));
+        }
+    } else if (c->staged) {
         if (n_items) {
             HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
             if ((rc = staged_pass(c, 3, starts, goals, c->items, off, 0, n_items, &v, b, ok))) return rc;
@@ -953,7 +995,10 @@ extern "C" int vgpu_sample_configurations(vgpu_ctx* c, const vgpu_robot* r, uint
     if (n == 0) return VGPU_OK;
     if (!q) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, vgpu_launch_panda_sample(first, n, q, c->cur));
+    if (r->kind == VGPU_ROBOT_FETCH)
+        HIPCHK(c, vgpu_launch_fetch_sample(first, n, q, c->cur));
+    else
+        HIPCHK(c, vgpu_launch_panda_sample(first, n, q, c->cur));
     return VGPU_OK;
 }
 
@@ -970,6 +1015,10 @@ extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, u
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
+    if (r->kind == VGPU_ROBOT_FETCH) {
+        HIPCHK(c, vgpu_launch_fetch_sample_fkcc(first, n, &v, q, valid, c->cur));
+        return VGPU_OK;
+    }
     if (c->staged) return staged_pass(c, 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_sample_fkcc(first, n, &v, b[0], b[1], b[2], q, valid, c->cur));
     return VGPU_OK;
@@ -1023,16 +1072,23 @@ static int stage(vgpu_ctx* c, size_t bytes, char** p)
 
 static size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// configuration width and sphere count of a robot selection (host staging sizes)
+static size_t dim_of(const vgpu_robot* r) { return (r && r->kind == VGPU_ROBOT_FETCH) ? kFetchDim : kPandaDim; }
+static size_t spheres_of(const vgpu_robot* r)
+{
+    return (r && r->kind == VGPU_ROBOT_FETCH) ? kFetchSpheres : kPandaSpheres;
+}
+
 extern "C" int vgpu_sphere_fk_host(vgpu_ctx* c, const vgpu_robot* r, const float* q, size_t n, float* xyz)
 {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
-    const size_t qb = al(n * kPandaDim * 4), ob = (size_t)3 * kPandaSpheres * n * 4;
+    const size_t qb = al(n * dim_of(r) * 4), ob = (size_t)3 * spheres_of(r) * n * 4;
     int rc = stage(c, qb + ob, &d);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpyAsync(d, q, n * kPandaDim * 4, hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipMemcpyAsync(d, q, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     if ((rc = vgpu_sphere_fk(c, r, (const float*)d, n, (float*)(d + qb), n))) return rc;
     HIPCHK(c, hipMemcpyAsync(xyz, d + qb, ob, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
@@ -1045,11 +1101,11 @@ extern "C" int vgpu_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, con
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
-    const size_t qb = al(n * kPandaDim * 4);
+    const size_t qb = al(n * dim_of(r) * 4);
     int rc = stage(c, qb + n, &d);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpyAsync(d, q, n * kPandaDim * 4, hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipMemcpyAsync(d, q, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     if ((rc = vgpu_fkcc(c, r, e, (const float*)d, n, (uint8_t*)(d + qb)))) return rc;
     HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
@@ -1062,13 +1118,13 @@ extern "C" int vgpu_validate_motions_host(vgpu_ctx* c, const vgpu_robot* r, vgpu
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
-    const size_t qb = al(n * kPandaDim * 4);
+    const size_t qb = al(n * dim_of(r) * 4);
     const size_t okb = al(n), nbb = al(n * 4);
     int rc = stage(c, 2 * qb + okb + nbb, &d);
     if (rc) return rc;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipMemcpyAsync(d, starts, n * kPandaDim * 4, hipMemcpyHostToDevice, c->cur));
-    HIPCHK(c, hipMemcpyAsync(d + qb, goals, n * kPandaDim * 4, hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipMemcpyAsync(d, starts, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipMemcpyAsync(d + qb, goals, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     uint8_t* okd = (uint8_t*)(d + 2 * qb);
     int32_t* nbd = (int32_t*)(d + 2 * qb + okb);
     if ((rc = vgpu_validate_motions(c, r, e, (const float*)d, (const float*)(d + qb), n, okd, nbd))) return rc;
@@ -1117,11 +1173,11 @@ extern "C" int vgpu_sample_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
-    const size_t qb = al(n * kPandaDim * 4);
+    const size_t qb = al(n * dim_of(r) * 4);
     int rc = stage(c, qb + n, &d);
     if (rc) return rc;
     if ((rc = vgpu_sample_fkcc(c, r, e, first, n, q ? (float*)d : nullptr, (uint8_t*)(d + qb)))) return rc;
-    if (q) HIPCHK(c, hipMemcpyAsync(q, d, n * kPandaDim * 4, hipMemcpyDeviceToHost, c->cur));
+    if (q) HIPCHK(c, hipMemcpyAsync(q, d, n * dim_of(r) * 4, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;

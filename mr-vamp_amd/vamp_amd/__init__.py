@@ -329,19 +329,33 @@ def compact_device(rows_ptr: int, valid_ptr: int, n: int, dim: int, rows_out_ptr
 
 # ---- robots -----------------------------------------------------------------------------------
 class Robot:
-    """Python face of vamp::robots::PandaBase<X100, Y100, Z100> (robots/panda_base.hh:15-75)."""
+    """Python face of a vamp::robots robot: PandaBase<X100, Y100, Z100>
+    (robots/panda_base.hh:15-75) or Fetch (robots/fetch.hh:8-48)."""
 
-    S_M = np.array([5.9342, 3.6652, 5.9342, 3.2289, 5.9342, 3.9095999999999997, 5.9342], np.float32)
-    S_A = np.array([-2.9671, -1.8326, -2.9671, -3.1416, -2.9671, -0.0873, -2.9671], np.float32)
-    D_M = np.array([0.1685147113342995, 0.2728364072901888, 0.1685147113342995, 0.30970299482796,
-                    0.1685147113342995, 0.25578064252097404, 0.1685147113342995], np.float32)
+    # scale_configuration q * s_m + s_a, descale (q - s_a) * d_m (panda/fk.hh:14-62, fetch/fk.hh:20-97)
+    _SCALE = {
+        _lib.VGPU_ROBOT_PANDA: (
+            [5.9342, 3.6652, 5.9342, 3.2289, 5.9342, 3.9095999999999997, 5.9342],
+            [-2.9671, -1.8326, -2.9671, -3.1416, -2.9671, -0.0873, -2.9671],
+            [0.1685147113342995, 0.2728364072901888, 0.1685147113342995, 0.30970299482796, 0.1685147113342995,
+             0.25578064252097404, 0.1685147113342995]),
+        _lib.VGPU_ROBOT_FETCH: (
+            [0.38615, 3.2112, 2.739, 6.28318, 4.502, 6.28318, 4.32, 6.28318],
+            [0.0, -1.6056, -1.221, -3.14159, -2.251, -3.14159, -2.16, -3.14159],
+            [2.589667227761233, 0.31141006477329347, 0.36509675063891933, 0.15915507752443828,
+             0.22212350066637052, 0.15915507752443828, 0.23148148148148145, 0.15915507752443828]),
+    }
 
     def __init__(self, name: str, base_x100: int, base_y100: int, base_z100: int, kind: int = _lib.VGPU_ROBOT_PANDA):
         self.name = name
         self.c_robot = _lib.VgpuRobot(kind, base_x100, base_y100, base_z100)
-        dim, res, ns = C.c_int32(), C.c_int32(), C.c_int32()
         self._info = None
         self.kind = kind
+        sm, sa, dm = self._SCALE[kind]
+        self.S_M = np.array(sm, np.float32)
+        self.S_A = np.array(sa, np.float32)
+        self.D_M = np.array(dm, np.float32)
+        self.radii = _PANDA_RADII if kind == _lib.VGPU_ROBOT_PANDA else _FETCH_RADII
 
     def _meta(self):
         if self._info is None:
@@ -378,7 +392,7 @@ class Robot:
     def fk(self, configuration, ctx: Optional[Context] = None) -> List[Sphere]:
         """vamp.<robot>.fk(q) (bindings/common.hh:132-152): the collision spheres."""
         xyz = self.sphere_fk_batch(np.asarray(configuration, np.float32)[None, :], ctx)[0]
-        radii = _PANDA_RADII
+        radii = self.radii
         return [Sphere(xyz[s], float(radii[s])) for s in range(xyz.shape[0])]
 
     def validate(self, configuration, environment: Environment, ctx: Optional[Context] = None) -> bool:
@@ -472,6 +486,14 @@ _PANDA_RADII = np.array(
     np.float32)
 
 
+# robots/fetch/fk.hh:118-228 sphere radii (reference order)
+_FETCH_RADII = np.array(
+    [0.24, 0.066, 0.22] + [0.066] * 5 + [0.22] + [0.066] * 5 + [0.15] * 6 + [0.07, 0.15] + [0.05] * 5 + [0.03] * 22 +
+    [0.055] * 4 + [0.04] * 4 + [0.055] * 6 + [0.03] * 4 + [0.055] + [0.03] * 4 + [0.055] * 3 + [0.03] * 6 +
+    [0.055] * 2 + [0.03] * 4 + [0.055] * 2 + [0.05] * 4 + [0.012] * 12 + [0.12] * 6, np.float32)
+assert _FETCH_RADII.shape == (111,)
+
+
 def PandaBase(base_x100: int, base_y100: int, base_z100: int, name: Optional[str] = None) -> Robot:
     """vamp::robots::PandaBase<X100, Y100, Z100> (robots/panda_base.hh:15)."""
     return Robot(name or f"panda_{base_x100}_{base_y100}_{base_z100}", base_x100, base_y100, base_z100)
@@ -483,3 +505,8 @@ for _i in range(3):
     for _j in range(3):
         globals()[f"panda_{_i}_{_j}"] = PandaBase(100 * _i, 100 * _j, 0, f"panda_{_i}_{_j}")
         __all__.append(f"panda_{_i}_{_j}")
+
+
+# robots/fetch.hh: vamp::robots::Fetch (8 dof, no base offset)
+fetch = Robot("fetch", 0, 0, 0, kind=_lib.VGPU_ROBOT_FETCH)
+__all__.append("fetch")

@@ -15,6 +15,7 @@ LIB_PATH = os.environ.get("VAMP_AMD_LIB") or os.path.join(HERE, "libvampgpu.so")
 
 VGPU_OK = 0
 VGPU_ROBOT_PANDA = 1
+VGPU_ROBOT_FETCH = 2
 ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of memory", -4: "unsupported", -5: "host rsqrt probe"}
 
 F32P = C.POINTER(C.c_float)

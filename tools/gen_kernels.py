@@ -166,6 +166,33 @@ def xform(E: Emitter, R, P, o):
     return out
 
 
+def joint(E: Emitter, fr: dict, A, R_A, P):
+    """Apply frame fr's joint after its fixed rotation: returns (Q, P).  Revolute about the unit
+    axis a: Q = A (x) (c, s*a) (other components structurally zero; a negative axis negates s).
+    Prismatic along a: Q = A, P += R(A) (a*q) (oracle/vamp_oracle.c robot_fk_frames)."""
+    d = fr["dof"]
+    if d < 0:
+        return A, P
+    ax = fr.get("axis", [0.0, 0.0, 1.0])
+    if fr.get("jtype") == "prismatic":
+        qv = SV("var", name=f"q{d}")
+        dq = [SV.zero() if a == 0 else (qv if a > 0 else E.neg(qv)) for a in ax]
+        RA = R_A()
+        out = []
+        for i in range(3):
+            acc = SV.zero()
+            for k in range(3):
+                acc = E.add(acc, E.mul(RA[i][k], dq[k]))
+            out.append(E.add(P[i], acc))
+        return A, out
+    h = E.tmp(f"q{d} * 0.5f")
+    c = E.tmp(f"vamp_cos({h.name})")
+    sn = E.tmp(f"vamp_sin({h.name})")
+    E.flops += 2 * 16
+    comp = [SV.zero() if a == 0 else (sn if a > 0 else E.neg(sn)) for a in ax]
+    return qmul(E, A, (c, comp[0], comp[1], comp[2])), P
+
+
 class RobotGen:
     def __init__(self, model):
         self.m = model
@@ -184,18 +211,16 @@ class RobotGen:
                 p = fr["parent"]
                 ident = list(fr["qf"]) == [1.0, 0.0, 0.0, 0.0]
                 A = Q[p] if ident else qmul(E, Q[p], qf)
-                d = fr["dof"]
-                if d >= 0:
-                    h = E.tmp(f"q{d} * 0.5f")
-                    c = E.tmp(f"vamp_cos({h.name})")
-                    s = E.tmp(f"vamp_sin({h.name})")
-                    E.flops += 2 * 16
-                    Q[f] = qmul(E, A, (c, SV.zero(), SV.zero(), s))
-                else:
-                    Q[f] = A
-                if p not in R:
-                    R[p] = qmat(E, Q[p])
-                P[f] = xform(E, R[p], P[p], fr["t"])
+                if fr.get("jtype") == "prismatic":
+                    if p not in R:
+                        R[p] = qmat(E, Q[p])
+                    Pt = xform(E, R[p], P[p], fr["t"])
+                    Q[f], P[f] = joint(E, fr, A, lambda: R[p] if ident else qmat(E, A), Pt)
+                else:  # emission order as before the prismatic support (same generated Panda code)
+                    Q[f], _ = joint(E, fr, A, None, None)
+                    if p not in R:
+                        R[p] = qmat(E, Q[p])
+                    P[f] = xform(E, R[p], P[p], fr["t"])
             R[f] = qmat(E, Q[f])
         return Q, P, R
 
@@ -247,16 +272,12 @@ class RobotGen:
             self.rot(p)
             ident = list(fr["qf"]) == [1.0, 0.0, 0.0, 0.0]
             A = Q[p] if ident else qmul(E, Q[p], qf)
-            d = fr["dof"]
-            if d >= 0:
-                h = E.tmp(f"q{d} * 0.5f")
-                c = E.tmp(f"vamp_cos({h.name})")
-                sn = E.tmp(f"vamp_sin({h.name})")
-                E.flops += 2 * 16
-                Q[f] = qmul(E, A, (c, SV.zero(), SV.zero(), sn))
+            if fr.get("jtype") == "prismatic":
+                Pt = xform(E, self.R[p], P[p], fr["t"])
+                Q[f], P[f] = joint(E, fr, A, lambda: self.R[p] if ident else qmat(E, A), Pt)
             else:
-                Q[f] = A
-            P[f] = xform(E, self.R[p], P[p], fr["t"])
+                Q[f], _ = joint(E, fr, A, None, None)
+                P[f] = xform(E, self.R[p], P[p], fr["t"])
 
         def rot(self, f):
             # REMAT: rotation matrices live only within one check (A/B: slower, kept off)
@@ -400,6 +421,9 @@ class RobotGen:
             kind, test, ck = self.bound_test(fr, o)
             label = ck["link"] if kind == "env" else " vs ".join(ck["links"])
             E.raw(f"// {kind}: {label} ({len(ck['children'])} children)")
+            if kind == "env" and ck.get("leaf"):  # single-sphere link: its own hit is the collision
+                E.raw(f"if (Grp::any_bits({test})) return false;")
+                continue
             if kind == "env":
                 E.raw(f"if (Grp::any_bits({test})) {{")
             else:
@@ -476,7 +500,9 @@ def main():
     for key in ("s_m", "s_a"):
         vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model[key])
         consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
-    out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc() + "\n" + g.gen_staged()
+    out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
+    if len(model["check_order"]) <= 32 and not any(c.get("leaf") for c in model["env_checks"]):
+        out += "\n" + g.gen_staged()  # the staged pipeline keys checks by a 32-bit mask
     open(sys.argv[2], "w").write(out)
     print(f"wrote {sys.argv[2]} ({len(out.splitlines())} lines)")
 
