@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--workload", default="validate", choices=["validate", "fetch_prm"],
+                    help="validate: BASELINE configs[1] (the headline); fetch_prm: configs[3] vertex stage")
+    ap.add_argument("--draws", type=int, default=4_000_000, help="fetch_prm: Halton draws per step (whole job)")
     return ap.parse_args()
 
 
@@ -163,6 +166,119 @@ def reduce_over_ranks(dist, torch, wall, units, dev, world):
     return float(mx[0]), float(sm[0])
 
 
+def fetch_scene(vamp):
+    """MotionBenchMaker table_pick_fetch scene0001 as resolved obstacle rows (the committed
+    fixture tests/golden/fetch_table_pick.npz; tests/oracle_py.py:mbm_env builds it)."""
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "fetch_table_pick.npz"), allow_pickle=False)
+    env = vamp.Environment()
+    for row in fx["env_spheres"]:
+        env.add_sphere(vamp.Sphere(row[0:3], float(row[3])))
+    for row in np.concatenate([fx["env_cuboids"], fx["env_zcuboids"]]):
+        env.add_cuboid(vamp.Cuboid.from_axes(row[0:3], row[3:6], row[6:9], row[9:12], row[12:15]))
+    for row in np.concatenate([fx["env_capsules"], fx["env_zcapsules"]]):
+        p1 = np.array(row[0:3], np.float32)
+        env.add_capsule(vamp.Cylinder(p1, (p1 + np.array(row[3:6], np.float32)).astype(np.float32), float(row[6])))
+    return env, fx
+
+
+def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
+    """BASELINE configs[3], vertex stage: draws 1..D of Halton<8> ->
+    scale -> Fetch fkcc on the MBM table_pick scene, sharded by contiguous draw ranges over the
+    ranks, valid vertices compacted on the device and all-gathered over RCCL.  Total draws fixed
+    as N grows (strong scaling); one step = the whole stage including the exchange."""
+    from vamp_amd import roadmap
+
+    env, fx = fetch_scene(vamp)
+    robot = vamp.fetch
+    lo, n = roadmap.shard_range(a.draws, rank, world, 1)
+
+    def step():
+        rows, draws, cnt = roadmap.sample_valid_shard(torch, robot, env, lo, n, ctx, dev)
+        if world > 1:
+            rows, draws = roadmap.allgather_vertices(torch, dist, rows, draws, cnt)
+            return rows.shape[0]
+        return cnt
+
+    for _ in range(a.warmup):
+        n_vertices = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        n_vertices = step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    wall_max, units_all = reduce_over_ranks(dist, torch, t1 - t0, float(n), dev, world)
+
+    # the dominant kernel alone (fused sample + fkcc), HIP events on the launch stream
+    q = torch.empty((max(n, 1), 8), dtype=torch.float32, device=dev)
+    valid = torch.empty(max(n, 1), dtype=torch.uint8, device=dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(a.steps):
+        robot.sample_fkcc_device(lo, n, env, q.data_ptr(), valid.data_ptr(), ctx)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    kern_ms = e0.elapsed_time(e1) / a.steps
+    if rank != 0:
+        return
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as op
+    from test_oracle_fetch import fetch_env
+
+    oenv = fetch_env(op, fx)
+    ks = np.arange(1, 1 + 4096) * max(1, a.draws // 4096)
+    qs = op.robot_scale("fetch", op.halton(8, ks))
+    _, _, _, fl = op.robot_fkcc("fetch", oenv, qs, stats=True)
+    f_sample = float(fl.mean())
+    achieved = f_sample * n / (kern_ms * 1e-3) / 1e12
+    cpu = None
+    if not a.no_cpu and world == 1:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        m0 = 16384
+        t = time.perf_counter()
+        op.robot_fkcc_threads("fetch", oenv, op.robot_scale("fetch", op.halton(8, np.arange(1, m0 + 1))),
+                              threads=threads)
+        dt0 = max(time.perf_counter() - t, 1e-3)
+        m = int(min(a.draws, m0 * a.cpu_seconds / dt0))
+        qc = op.robot_scale("fetch", op.halton(8, np.arange(1, m + 1)))
+        t = time.perf_counter()
+        op.robot_fkcc_threads("fetch", oenv, qc, threads=threads)
+        dt = time.perf_counter() - t
+        cpu = {"value": m / dt, "unit": "samples/s", "cores": threads, "kind": "port",
+               "sample": f"draws 1..{m} of the same stage (Halton<8> scaling on the host untimed), "
+                         f"oracle/vamp_oracle.c Fetch fkcc, {threads} threads, {dt:.1f} s",
+               "cpu_model": cpu_model()}
+    line = {
+        "metric": "PRM vertex-stage samples/sec (Fetch 8-DOF Halton<8> + FK+CC, RCCL all-gather of valid vertices)",
+        "value": units_all * a.steps / wall_max,
+        "unit": "samples/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": wall_max / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Halton<8> draws 1..D, the reference sampler; MBM table_pick_fetch scene0001)",
+        "config": {"workload": f"BASELINE configs[3]: Fetch 8-DOF PRM vertex stage, {a.draws} draws sharded over "
+                               f"{world} GPU(s), all-gather of valid vertices",
+                   "robot": "Fetch", "draws_total": a.draws, "vertices": int(n_vertices),
+                   "parallelism": f"dp{world} (contiguous draw ranges, one all-gather)"},
+        "roofline": {"kernel": "fetch_sample_fkcc_kernel", "bound": "valu", "achieved": achieved,
+                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+                     "traffic": None, "kernel_ms": kern_ms, "algorithmic_flops_per_sample": f_sample,
+                     "algorithmic_bytes_per_sample": 8 * 4 + 1},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+
+
 def main():
     a = parse()
     import torch
@@ -184,6 +300,11 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
+    if a.workload == "fetch_prm":
+        run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     env = vamp.Environment()
     for c in CAGE:
         env.add_sphere(vamp.Sphere(c, 0.2))

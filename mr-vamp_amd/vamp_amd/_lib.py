@@ -83,6 +83,14 @@ def load() -> C.CDLL:
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: build it with `make -C mr-vamp_amd` "
                            "(or __graft_entry__.build()); there is no CPU fallback")
+    # One HIP runtime per process: torch ships its own libamdhip64 (SONAME libamdhip64.so.7) and
+    # its libc10_hip asks for it as "libamdhip64.so".  Loaded first, it satisfies this library's
+    # libamdhip64.so.7 dependency too; loaded after /opt/rocm's copy, torch would bring in a second
+    # runtime, which then finds no GPU.  So torch (when installed) is imported before the CDLL.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)

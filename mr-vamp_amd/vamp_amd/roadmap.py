@@ -1,0 +1,110 @@
+"""PRM roadmap vertex stage, sharded over the GPUs of one node.
+
+Reference: ``Roadmap::build_roadmap`` (src/impl/vamp/planning/prm.hh:197-299) draws
+``rng->next()`` (Halton<dim>), scales it (``Robot::scale_configuration``), checks it with
+``Robot::fkcc`` on the configuration broadcast to the rake (prm.hh:246-254) and appends every
+valid sample to the roadmap in draw order, after the start and goal vertices (prm.hh:228-233).
+
+Here the draws 1..N are split into contiguous ranges, one per rank (one process per GPU).  Each
+rank runs the fused Halton -> scale -> fkcc kernel over its range and compacts its valid rows on
+the device (vgpu_sample_fkcc + vgpu_compact).  One exchange step follows: an all-gather of the
+per-rank counts, then an all-gather of the count-padded rows and draw indices
+(torch.distributed, backend "nccl" = RCCL over xGMI on MI355X).  Concatenated in rank order, the
+result is exactly the reference's vertex sequence: valid samples in draw order.
+
+The kernels run on the context's stream; set it to torch's current stream
+(``Context.set_stream``) so the collective is ordered after them.  There is no CPU fallback:
+without the HIP library the calls raise.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+
+def shard_range(n_draws: int, rank: int, world: int, first: int = 1) -> Tuple[int, int]:
+    """(first draw index, count) of this rank's contiguous slice of draws first..first+n-1."""
+    chunk = (n_draws + world - 1) // world
+    lo = min(n_draws, rank * chunk)
+    hi = min(n_draws, lo + chunk)
+    return first + lo, hi - lo
+
+
+def allgather_vertices(torch, dist, rows, draws, count: int, group=None):
+    """Exchange the ranks' compacted vertices.  rows [>= count, dim] float32 and draws
+    [>= count] int64 (this rank's first `count` entries valid) -> (all rows, all draws) in rank
+    order.  Two collectives: counts, then the rows and draw indices padded to the largest count
+    (one all_gather_into_tensor each).  Works on CUDA tensors (RCCL) and CPU tensors (gloo)."""
+    world = dist.get_world_size(group)
+    dev = rows.device
+    cnt = torch.tensor([count], dtype=torch.int64, device=dev)
+    cnts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(cnts, cnt, group=group)
+    counts = [int(c) for c in cnts.tolist()]
+    mx = max(counts) if counts else 0
+    dim = rows.shape[1]
+    send_r = torch.zeros((mx, dim), dtype=rows.dtype, device=dev)
+    send_d = torch.zeros(mx, dtype=torch.int64, device=dev)
+    if count:
+        send_r[:count] = rows[:count]
+        send_d[:count] = draws[:count]
+    recv_r = torch.empty((world * mx, dim), dtype=rows.dtype, device=dev)
+    recv_d = torch.empty(world * mx, dtype=torch.int64, device=dev)
+    if mx:
+        dist.all_gather_into_tensor(recv_r, send_r, group=group)
+        dist.all_gather_into_tensor(recv_d, send_d, group=group)
+    keep = torch.cat([torch.arange(r * mx, r * mx + c, device=dev) for r, c in enumerate(counts)]) \
+        if sum(counts) else torch.empty(0, dtype=torch.int64, device=dev)
+    return recv_r.index_select(0, keep), recv_d.index_select(0, keep)
+
+
+def sample_valid_shard(torch, robot, environment, first: int, n: int, ctx, device):
+    """This rank's slice: fused Halton<dim> -> scale -> fkcc over draws first..first+n-1, then
+    device compaction.  Returns (rows [n, dim] with `count` valid leading rows, draws [n] int64,
+    count).  GPU only."""
+    dim = robot.dimension()
+    q = torch.empty((max(n, 1), dim), dtype=torch.float32, device=device)
+    valid = torch.empty(max(n, 1), dtype=torch.uint8, device=device)
+    rows = torch.empty_like(q)
+    idx = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+    count = 0
+    if n:
+        robot.sample_fkcc_device(first, n, environment, q.data_ptr(), valid.data_ptr(), ctx)
+        from . import compact_device
+        count = compact_device(q.data_ptr(), valid.data_ptr(), n, dim, rows.data_ptr(), idx.data_ptr(), ctx)
+    draws = idx.long() + first
+    return rows, draws, count
+
+
+def roadmap_vertices(robot, environment, n_draws: int, first: int = 1, start=None, goal=None,
+                     max_samples: Optional[int] = None, ctx=None, group=None):
+    """Vertices of ``build_roadmap`` after ``n_draws`` sampler iterations (prm.hh:235-254):
+    [start, goal,] then every valid Halton sample in draw order, truncated at max_samples
+    vertices like the reference loop.  Runs sharded when torch.distributed is initialised (one
+    rank per GPU), single-GPU otherwise.  Returns (vertices [M, dim], draw_index [M]) as CUDA
+    tensors; draw_index is -1 for start/goal."""
+    import torch
+    import torch.distributed as dist
+
+    from . import context
+
+    ctx = ctx or context()
+    device = torch.device("cuda", torch.cuda.current_device())
+    ctx.set_stream(torch.cuda.current_stream(device).cuda_stream)
+    sharded = dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    rank, world = (dist.get_rank(group), dist.get_world_size(group)) if sharded else (0, 1)
+    lo, n = shard_range(n_draws, rank, world, first)
+    rows, draws, count = sample_valid_shard(torch, robot, environment, lo, n, ctx, device)
+    if sharded:
+        rows, draws = allgather_vertices(torch, dist, rows, draws, count, group)
+    else:
+        rows, draws = rows[:count], draws[:count]
+    head = []
+    if start is not None and goal is not None:
+        head = [torch.as_tensor(start, dtype=torch.float32, device=device).reshape(1, -1),
+                torch.as_tensor(goal, dtype=torch.float32, device=device).reshape(1, -1)]
+    if head:
+        rows = torch.cat(head + [rows])
+        draws = torch.cat([torch.full((2,), -1, dtype=torch.int64, device=device), draws])
+    if max_samples is not None:
+        rows, draws = rows[:max_samples], draws[:max_samples]
+    return rows, draws

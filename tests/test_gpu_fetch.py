@@ -79,3 +79,25 @@ def test_fetch_sample_fkcc(vamp, oracle):
     qo = oracle.robot_scale("fetch", oracle.halton(8, np.arange(first, first + n)))
     assert np.array_equal(q.view(np.uint32), qo.view(np.uint32))
     assert np.array_equal(ok, oracle.robot_fkcc_threads("fetch", oenv, qo))
+
+
+def test_roadmap_vertices_single_gpu(vamp, oracle):
+    """build_roadmap's vertex sequence (prm.hh:228-254): start, goal, then the valid Halton<8>
+    samples in draw order, truncated at max_samples -- through the sharded entry point
+    (one rank here; the all-gather itself is covered by tests/test_roadmap_dist.py)."""
+    import torch
+    from vamp_amd import roadmap
+    fx = golden("fetch_table_pick.npz")
+    oenv = fetch_env(oracle, fx)
+    env = gpu_env_from_oracle(vamp, oenv)
+    n, first = 30000, 990_001
+    s, g = fx["starts"][-1], fx["goals"][-1]
+    V, D = roadmap.roadmap_vertices(vamp.fetch, env, n, first=first, start=s, goal=g)
+    torch.cuda.synchronize()
+    qo = oracle.robot_scale("fetch", oracle.halton(8, np.arange(first, first + n)))
+    ok = oracle.robot_fkcc_threads("fetch", oenv, qo)
+    want = np.concatenate([s[None], g[None], qo[ok]])
+    assert np.array_equal(V.cpu().numpy().view(np.uint32), want.view(np.uint32))
+    assert np.array_equal(D.cpu().numpy()[2:], np.nonzero(ok)[0] + first)
+    V2, _ = roadmap.roadmap_vertices(vamp.fetch, env, n, first=first, start=s, goal=g, max_samples=1000)
+    assert V2.shape[0] == 1000 and torch.equal(V2, V[:1000])
