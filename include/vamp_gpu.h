@@ -46,9 +46,15 @@ typedef struct vgpu_env vgpu_env;
 /* kind = VGPU_ROBOT_FETCH reproduces vamp::robots::Fetch (robots/fetch.hh:8-48): 8 dof (prismatic
  * torso + 7 revolute), 111 spheres, resolution 32, no base offset (base_*100 must be 0). */
 #define VGPU_ROBOT_FETCH 2
+/* kind = VGPU_ROBOT_PANDA_PAIR: the two-Panda composite of BASELINE configs[4] (14 dof: arm A =
+ * joints 0..6 at base (base_*100), arm B = joints 7..13 at base (base2_*100); resolution 32).
+ * The reference has no composite robot; validity = fkcc_A && fkcc_B && no A-B sphere overlap
+ * (link-bounding pairs first), composed from the reference primitives. */
+#define VGPU_ROBOT_PANDA_PAIR 3
 typedef struct vgpu_robot {
     int32_t kind;
     int32_t base_x100, base_y100, base_z100;
+    int32_t base2_x100, base2_y100, base2_z100; /* second arm (VGPU_ROBOT_PANDA_PAIR only) */
 } vgpu_robot;
 
 /* ---- context -------------------------------------------------------------------------- */

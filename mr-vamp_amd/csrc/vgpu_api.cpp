@@ -69,6 +69,14 @@ hipError_t vgpu_launch_fetch_validate_head(const float* starts, const float* goa
 hipError_t vgpu_launch_fetch_validate_tail(const float* starts, const float* goals, size_t n_items,
                                            const EnvView* env, uint8_t* ok, const uint32_t* off,
                                            const uint32_t* item_edge, hipStream_t st);
+hipError_t vgpu_launch_pair_fkcc(const float* q, size_t n, const EnvView* env, const float base[6], uint8_t* valid,
+                                 hipStream_t st);
+hipError_t vgpu_launch_pair_validate_head(const float* starts, const float* goals, size_t n_edges, const EnvView* env,
+                                          const float base[6], uint8_t* ok, int32_t* n_blocks, uint32_t* cnt,
+                                          hipStream_t st);
+hipError_t vgpu_launch_pair_validate_tail(const float* starts, const float* goals, size_t n_items, const EnvView* env,
+                                          const float base[6], uint8_t* ok, const uint32_t* off,
+                                          const uint32_t* item_edge, hipStream_t st);
 size_t vgpu_validate_scan_bytes(size_t n_edges);
 hipError_t vgpu_launch_scan(const uint32_t* cnt, uint32_t* off, size_t n_edges, void* scan_tmp, size_t scan_bytes,
                             hipStream_t st);
@@ -89,6 +97,7 @@ constexpr int kPandaSpheres = 59;     // robots/panda/fk.hh:93
 constexpr int kFetchDim = 8;          // robots/fetch.hh:12
 constexpr int kFetchResolution = 32;  // robots/fetch.hh:13
 constexpr int kFetchSpheres = 111;    // robots/fetch/fk.hh:104
+constexpr int kPairDim = 14;          // two Panda arms (BASELINE configs[4])
 
 inline uint32_t f2u(float f)
 {
@@ -705,6 +714,12 @@ static EnvView make_view(const vgpu_env* e)
 // ---------------------------------------------------------------------------------------
 extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t* ns)
 {
+    if (kind == VGPU_ROBOT_PANDA_PAIR) {
+        if (dim) *dim = kPairDim;
+        if (res) *res = kPandaResolution;
+        if (ns) *ns = 2 * kPandaSpheres;
+        return VGPU_OK;
+    }
     if (kind == VGPU_ROBOT_FETCH) {
         if (dim) *dim = kFetchDim;
         if (res) *res = kFetchResolution;
@@ -718,6 +733,17 @@ extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t
     return VGPU_OK;
 }
 
+// both arms' bases of a VGPU_ROBOT_PANDA_PAIR, metres (panda/fk.hh:109-111 per arm)
+static void pair_bases(const vgpu_robot* r, float pb[6])
+{
+    pb[0] = (float)r->base_x100 / 100.0f;
+    pb[1] = (float)r->base_y100 / 100.0f;
+    pb[2] = (float)r->base_z100 / 100.0f;
+    pb[3] = (float)r->base2_x100 / 100.0f;
+    pb[4] = (float)r->base2_y100 / 100.0f;
+    pb[5] = (float)r->base2_z100 / 100.0f;
+}
+
 static int check_robot(vgpu_ctx* c, const vgpu_robot* r, float base[3])
 {
     if (!r) return fail(c, VGPU_ERR_INVALID_ARG, "null robot");
@@ -727,7 +753,8 @@ static int check_robot(vgpu_ctx* c, const vgpu_robot* r, float base[3])
         base[0] = base[1] = base[2] = 0.0f;
         return VGPU_OK;
     }
-    if (r->kind != VGPU_ROBOT_PANDA) return fail(c, VGPU_ERR_UNSUPPORTED, "unsupported robot kind");
+    if (r->kind != VGPU_ROBOT_PANDA && r->kind != VGPU_ROBOT_PANDA_PAIR)
+        return fail(c, VGPU_ERR_UNSUPPORTED, "unsupported robot kind");
     // robots/panda/fk.hh:109-111: static_cast<float>(base_x100) / 100.0f
     base[0] = (float)r->base_x100 / 100.0f;
     base[1] = (float)r->base_y100 / 100.0f;
@@ -747,6 +774,8 @@ extern "C" int vgpu_sphere_fk(vgpu_ctx* c, const vgpu_robot* r, const float* q, 
         HIPCHK(c, vgpu_launch_fetch_sphere_fk(q, n, xyz, ld, c->cur));
         return VGPU_OK;
     }
+    if (r->kind == VGPU_ROBOT_PANDA_PAIR)
+        return fail(c, VGPU_ERR_UNSUPPORTED, "sphere_fk of the composite: call it per arm (VGPU_ROBOT_PANDA)");
     HIPCHK(c, vgpu_launch_panda_sphere_fk(q, n, b[0], b[1], b[2], xyz, ld, c->cur));
     return VGPU_OK;
 }
@@ -859,6 +888,12 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
         HIPCHK(c, vgpu_launch_fetch_fkcc(q, n, &v, valid, c->cur));
         return VGPU_OK;
     }
+    if (r->kind == VGPU_ROBOT_PANDA_PAIR) {
+        float pb[6];
+        pair_bases(r, pb);
+        HIPCHK(c, vgpu_launch_pair_fkcc(q, n, &v, pb, valid, c->cur));
+        return VGPU_OK;
+    }
     if (c->staged) return staged_pass(c, 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_fkcc(q, n, &v, b[0], b[1], b[2], valid, c->cur));
     return VGPU_OK;
@@ -904,8 +939,13 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     size_t tmp_bytes;
     if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
     const bool fetch = r->kind == VGPU_ROBOT_FETCH;  // monolithic head/tail kernels
+    const bool pair = r->kind == VGPU_ROBOT_PANDA_PAIR;
+    float pb[6];
+    pair_bases(r, pb);
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
-    if (fetch) {
+    if (pair) {
+        HIPCHK(c, vgpu_launch_pair_validate_head(starts, goals, n_edges, &v, pb, ok, n_blocks, cnt, c->cur));
+    } else if (fetch) {
         HIPCHK(c, vgpu_launch_fetch_validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
     } else if (c->staged) {
         if ((rc = staged_pass(c, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
@@ -928,10 +968,13 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
         c->items_cap = cap;
     }
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[2], c->cur));
-    if (fetch) {
+    if (fetch || pair) {
         if (n_items) {
             HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
-            HIPCHK(c, vgpu_launch_fetch_validate_tail(starts, goals, n_items, &v, ok, off, c->items, c->cur));
+            if (pair)
+                HIPCHK(c, vgpu_launch_pair_validate_tail(starts, goals, n_items, &v, pb, ok, off, c->items, c->cur));
+            else
+                HIPCHK(c, vgpu_launch_fetch_validate_tail(starts, goals, n_items, &v, ok, off, c->items, c->cur));
         }
     } else if (c->staged) {
         if (n_items) {
@@ -995,6 +1038,7 @@ extern "C" int vgpu_sample_configurations(vgpu_ctx* c, const vgpu_robot* r, uint
     if (n == 0) return VGPU_OK;
     if (!q) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
     HIPCHK(c, hipSetDevice(c->device));
+    if (r->kind == VGPU_ROBOT_PANDA_PAIR) return fail(c, VGPU_ERR_UNSUPPORTED, "no sampler for the composite");
     if (r->kind == VGPU_ROBOT_FETCH)
         HIPCHK(c, vgpu_launch_fetch_sample(first, n, q, c->cur));
     else
@@ -1015,6 +1059,7 @@ extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, u
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
+    if (r->kind == VGPU_ROBOT_PANDA_PAIR) return fail(c, VGPU_ERR_UNSUPPORTED, "no sampler for the composite");
     if (r->kind == VGPU_ROBOT_FETCH) {
         HIPCHK(c, vgpu_launch_fetch_sample_fkcc(first, n, &v, q, valid, c->cur));
         return VGPU_OK;
@@ -1073,7 +1118,12 @@ static int stage(vgpu_ctx* c, size_t bytes, char** p)
 static size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // configuration width and sphere count of a robot selection (host staging sizes)
-static size_t dim_of(const vgpu_robot* r) { return (r && r->kind == VGPU_ROBOT_FETCH) ? kFetchDim : kPandaDim; }
+static size_t dim_of(const vgpu_robot* r)
+{
+    if (r && r->kind == VGPU_ROBOT_FETCH) return kFetchDim;
+    if (r && r->kind == VGPU_ROBOT_PANDA_PAIR) return kPairDim;
+    return kPandaDim;
+}
 static size_t spheres_of(const vgpu_robot* r)
 {
     return (r && r->kind == VGPU_ROBOT_FETCH) ? kFetchSpheres : kPandaSpheres;

@@ -13,21 +13,28 @@ struct RakeD {
     int n;
 };
 
-// distance = l2_norm of goal - start: squares summed in the AVX hsum lane order
-// ((l0+l4)+(l2+l6)) + ((l1+l5)+(l3+l7)) (vector/avx.hh:441-452), padding lanes 0;
-// n = max(ceil(d / 8 * resolution), 1) (validate.hh:41)
+// distance = l2_norm of goal - start (interface.hh:402-410): D <= 8 is one AVX register whose
+// squares are summed in the hsum lane order ((l0+l4)+(l2+l6)) + ((l1+l5)+(l3+l7))
+// (vector/avx.hh:441-452); D <= 16 is two registers lo/hi added lane-wise first, which the
+// release build contracts to fma(lo, lo, hi * hi) (pinned by ref_probe "l2norm").  Padding
+// lanes are 0.  n = max(ceil(d / 8 * resolution), 1) (validate.hh:41)
 template <int D, int RES>
 __device__ __forceinline__ RakeD<D> rake_setup_d(const float* __restrict__ s, const float* __restrict__ g)
 {
-    static_assert(D <= 8, "one AVX register");
+    static_assert(D <= 16, "at most two AVX registers");
     RakeD<D> r;
+#pragma unroll
+    for (int j = 0; j < D; ++j) r.v[j] = g[j] - s[j];  // validate.hh:72
     float sq[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) sq[j] = 0.0f;
-#pragma unroll
-    for (int j = 0; j < D; ++j) {
-        r.v[j] = g[j] - s[j];  // validate.hh:72
-        sq[j] = r.v[j] * r.v[j];
+    for (int j = 0; j < 8; ++j) {
+        const float lo = j < D ? r.v[j < D ? j : 0] : 0.0f;
+        if (D <= 8) {
+            sq[j] = lo * lo;
+        } else {
+            const float hi = (j + 8 < D) ? r.v[(j + 8 < D) ? j + 8 : 0] : 0.0f;
+            sq[j] = __builtin_fmaf(lo, lo, hi * hi);
+        }
     }
     const float a = (sq[0] + sq[4]) + (sq[2] + sq[6]);
     const float c = (sq[1] + sq[5]) + (sq[3] + sq[7]);

@@ -346,16 +346,21 @@ class Robot:
              0.22212350066637052, 0.15915507752443828, 0.23148148148148145, 0.15915507752443828]),
     }
 
-    def __init__(self, name: str, base_x100: int, base_y100: int, base_z100: int, kind: int = _lib.VGPU_ROBOT_PANDA):
+    def __init__(self, name: str, base_x100: int, base_y100: int, base_z100: int, kind: int = _lib.VGPU_ROBOT_PANDA,
+                 base2=(0, 0, 0)):
         self.name = name
-        self.c_robot = _lib.VgpuRobot(kind, base_x100, base_y100, base_z100)
+        self.c_robot = _lib.VgpuRobot(kind, base_x100, base_y100, base_z100, *base2)
         self._info = None
         self.kind = kind
-        sm, sa, dm = self._SCALE[kind]
+        if kind == _lib.VGPU_ROBOT_PANDA_PAIR:  # both arms' scaling, concatenated
+            sm, sa, dm = (a + a for a in self._SCALE[_lib.VGPU_ROBOT_PANDA])
+        else:
+            sm, sa, dm = self._SCALE[kind]
         self.S_M = np.array(sm, np.float32)
         self.S_A = np.array(sa, np.float32)
         self.D_M = np.array(dm, np.float32)
-        self.radii = _PANDA_RADII if kind == _lib.VGPU_ROBOT_PANDA else _FETCH_RADII
+        self.radii = {_lib.VGPU_ROBOT_PANDA: _PANDA_RADII, _lib.VGPU_ROBOT_FETCH: _FETCH_RADII}.get(
+            kind, np.concatenate([_PANDA_RADII, _PANDA_RADII]))
 
     def _meta(self):
         if self._info is None:
@@ -510,3 +515,14 @@ for _i in range(3):
 # robots/fetch.hh: vamp::robots::Fetch (8 dof, no base offset)
 fetch = Robot("fetch", 0, 0, 0, kind=_lib.VGPU_ROBOT_FETCH)
 __all__.append("fetch")
+
+
+def PandaPair(a100=(0, 0, 0), b100=(100, 0, 0), name: Optional[str] = None) -> Robot:
+    """The two-Panda composite of BASELINE configs[4] (14 dof: arm A = PandaBase<a100> on joints
+    0..6, arm B = PandaBase<b100> on joints 7..13).  No reference counterpart: validity is
+    fkcc_A && fkcc_B && no A-B sphere overlap (oracle/vamp_oracle.c vo_pair_*)."""
+    return Robot(name or f"panda_pair_{a100}_{b100}", *a100, kind=_lib.VGPU_ROBOT_PANDA_PAIR, base2=tuple(b100))
+
+
+panda_pair = PandaPair((0, 0, 0), (100, 0, 0), "panda_pair")
+__all__ += ["PandaPair", "panda_pair"]

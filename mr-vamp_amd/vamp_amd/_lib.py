@@ -16,6 +16,7 @@ LIB_PATH = os.environ.get("VAMP_AMD_LIB") or os.path.join(HERE, "libvampgpu.so")
 VGPU_OK = 0
 VGPU_ROBOT_PANDA = 1
 VGPU_ROBOT_FETCH = 2
+VGPU_ROBOT_PANDA_PAIR = 3
 ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of memory", -4: "unsupported", -5: "host rsqrt probe"}
 
 F32P = C.POINTER(C.c_float)
@@ -26,7 +27,8 @@ VP = C.c_void_p
 
 
 class VgpuRobot(C.Structure):
-    _fields_ = [("kind", C.c_int32), ("base_x100", C.c_int32), ("base_y100", C.c_int32), ("base_z100", C.c_int32)]
+    _fields_ = [("kind", C.c_int32), ("base_x100", C.c_int32), ("base_y100", C.c_int32), ("base_z100", C.c_int32),
+                ("base2_x100", C.c_int32), ("base2_y100", C.c_int32), ("base2_z100", C.c_int32)]
 
 
 # every exported symbol of include/vamp_gpu.h with its signature (restype, argtypes)

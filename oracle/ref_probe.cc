@@ -256,6 +256,26 @@ int main(int argc, char **argv)
         }
         write_f32(argv[3], out);
     }
+    else if (mode == "l2norm")
+    {
+        // in: E x dim vectors (goal - start); arg: dim (7, 8 or 14).  out: E distances
+        // FloatVector<dim>::l2_norm (interface.hh:402-410): lane-wise sum of the registers
+        // (utils.hh:53-62), then the AVX hsum (avx.hh:441-452), then std::sqrt.
+        auto in = read_f32(argv[2]);
+        const int dim = std::atoi(argv[4]);
+        const size_t E = in.size() / dim;
+        std::vector<float> out(E);
+        alignas(32) float buf[16] = {0};
+        for (size_t e = 0; e < E; ++e)
+        {
+            for (int j = 0; j < dim; ++j) buf[j] = in[dim * e + j];
+            if (dim == 7) out[e] = FloatVector<7>(launder(buf)).l2_norm();
+            else if (dim == 8) out[e] = FloatVector<8>(launder(buf)).l2_norm();
+            else if (dim == 14) out[e] = FloatVector<14>(launder(buf)).l2_norm();
+            else { std::fprintf(stderr, "l2norm: dim %d unsupported\n", dim); return 2; }
+        }
+        write_f32(argv[3], out);
+    }
     else if (mode == "halton")
     {
         // args: dim count skip.  out: count x dim samples (after `skip` draws)

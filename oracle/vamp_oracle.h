@@ -120,7 +120,7 @@ float vo_capt_vol_ball(const float p[3], const float lo[3], const float up[3]);
 #define VO_ROBOT_FETCH 2
 int vo_robot_dim(int robot);
 int vo_robot_nspheres(int robot);
-float vo_l2_norm(const float *v, int dim);                                   /* dim <= 8 */
+float vo_l2_norm(const float *v, int dim);                                   /* dim <= 16 */
 void vo_robot_scale(int robot, float *q);                                    /* scale_configuration */
 void vo_robot_sphere_fk(int robot, const float *q, int bx100, int by100, int bz100, float out_xyz[][3]);
 /* q is [G][dim]; returns 1 = valid */
@@ -157,6 +157,18 @@ void vo_panda_fkcc_configs(const vo_env *env, const float *q /*[N][7]*/, size_t 
 void vo_panda_validate_motions(const vo_env *env, const float *starts, const float *goals,
                                size_t n_edges, int bx100, int by100, int bz100, uint8_t *ok,
                                int32_t *n_out, int threads);
+
+/* ---- two-Panda composite (BASELINE configs[4]; composed from reference primitives) ---- */
+/* q is [G][14] = arm A joints 0..6, arm B joints 7..13; bases in centimetres.  Valid iff
+ * fkcc_A && fkcc_B && no A-B sphere overlap (link-bounding pairs first, then their spheres). */
+int vo_pair_fkcc_block(const vo_env *env, const float *q, int G, const int ba100[3], const int bb100[3],
+                       vo_stats *stats);
+int vo_pair_validate_motion(const vo_env *env, const float start[14], const float goal[14], const int ba100[3],
+                            const int bb100[3], int *n_out, vo_stats *stats);
+void vo_pair_fkcc_configs(const vo_env *env, const float *q, size_t n, const int ba100[3], const int bb100[3],
+                          uint8_t *valid, int threads);
+void vo_pair_validate_motions(const vo_env *env, const float *starts, const float *goals, size_t n_edges,
+                              const int ba100[3], const int bb100[3], uint8_t *ok, int32_t *n_out, int threads);
 
 /* ---- Halton (random/halton.hh:73-104), closed form ---- */
 /* Sample with 1-based draw index k (k-th call to next()) of Halton<dim>, dim <= 16. */

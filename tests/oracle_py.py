@@ -119,6 +119,12 @@ def lib():
                                             U8P, C.c_int]
         L.vo_robot_validate_motions.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, F32P, C.c_size_t, C.c_int,
                                                 C.c_int, C.c_int, U8P, I32P, C.c_int]
+        I3 = C.c_int * 3
+        L.vo_pair_fkcc_block.restype = C.c_int
+        L.vo_pair_fkcc_block.argtypes = [C.POINTER(VoEnv), F32P, C.c_int, I3, I3, C.POINTER(VoStats)]
+        L.vo_pair_fkcc_configs.argtypes = [C.POINTER(VoEnv), F32P, C.c_size_t, I3, I3, U8P, C.c_int]
+        L.vo_pair_validate_motions.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_size_t, I3, I3, U8P, I32P,
+                                               C.c_int]
         L.vo_l2_norm.restype = C.c_float
         L.vo_l2_norm.argtypes = [F32P, C.c_int]
         _lib = L
@@ -430,4 +436,50 @@ def mbm_env(scene: dict) -> Env:
                 e.add_capsule_endpoints(c - a, c + a, np.float32(radius))
             elif prim["type"] == "sphere":
                 e.add_sphere(c, np.float32(prim["dimensions"][0]))
+    return e
+
+
+# ---- two-Panda composite (BASELINE configs[4]) ----
+def _i3(b):
+    return (C.c_int * 3)(*[int(v) for v in b])
+
+
+def pair_fkcc(env: Env, q, ba=(0, 0, 0), bb=(100, 0, 0), G=1, stats=False):
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, 14)
+    N = q.shape[0]
+    ce = env.c()
+    res = np.zeros(N // G, bool)
+    fl = np.zeros(N // G)
+    for i in range(N // G):
+        st = VoStats(np.inf, np.inf, 0.0)
+        res[i] = lib().vo_pair_fkcc_block(C.byref(ce), fp(q[i * G:(i + 1) * G]), G, _i3(ba), _i3(bb), C.byref(st))
+        fl[i] = st.flops
+    return (res, fl) if stats else res
+
+
+def pair_fkcc_threads(env: Env, q, ba=(0, 0, 0), bb=(100, 0, 0), threads=8):
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, 14)
+    out = np.zeros(q.shape[0], np.uint8)
+    ce = env.c()
+    lib().vo_pair_fkcc_configs(C.byref(ce), fp(q), q.shape[0], _i3(ba), _i3(bb), out.ctypes.data_as(U8P), threads)
+    return out.astype(bool)
+
+
+def pair_validate_motions(env: Env, starts, goals, ba=(0, 0, 0), bb=(100, 0, 0), threads=8):
+    s = np.ascontiguousarray(starts, np.float32).reshape(-1, 14)
+    g = np.ascontiguousarray(goals, np.float32).reshape(-1, 14)
+    ok = np.zeros(s.shape[0], np.uint8)
+    n = np.zeros(s.shape[0], np.int32)
+    ce = env.c()
+    lib().vo_pair_validate_motions(C.byref(ce), fp(s), fp(g), s.shape[0], _i3(ba), _i3(bb), ok.ctypes.data_as(U8P),
+                                   n.ctypes.data_as(I32P), threads)
+    return ok.astype(bool), n
+
+
+def pair_scene() -> Env:
+    """Config-5 scene: a table surface under both arms plus three spheres between them."""
+    e = Env()
+    e.add_cuboid_axes((0.5, 0.0, -0.15), (1, 0, 0), (0, 1, 0), (0, 0, 1), (1.3, 0.8, 0.05))
+    for c in ((0.5, 0.55, 0.35), (0.5, -0.55, 0.35), (0.5, 0.0, 1.05)):
+        e.add_sphere(c, np.float32(0.1))
     return e

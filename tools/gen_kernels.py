@@ -166,13 +166,14 @@ def xform(E: Emitter, R, P, o):
     return out
 
 
-def joint(E: Emitter, fr: dict, A, R_A, P):
+def joint(E: Emitter, fr: dict, A, R_A, P, qoff: int = 0):
     """Apply frame fr's joint after its fixed rotation: returns (Q, P).  Revolute about the unit
     axis a: Q = A (x) (c, s*a) (other components structurally zero; a negative axis negates s).
     Prismatic along a: Q = A, P += R(A) (a*q) (oracle/vamp_oracle.c robot_fk_frames)."""
     d = fr["dof"]
     if d < 0:
         return A, P
+    d += qoff  # joint variable q<d>: a composite's second arm reads q7..q13
     ax = fr.get("axis", [0.0, 0.0, 1.0])
     if fr.get("jtype") == "prismatic":
         qv = SV("var", name=f"q{d}")
@@ -253,8 +254,8 @@ class RobotGen:
     class Frames:
         """Lazily emitted frame poses (Q, P, R) and bounding centres over one Emitter."""
 
-        def __init__(self, gen, E):
-            self.g, self.E = gen, E
+        def __init__(self, gen, E, qoff=0):
+            self.g, self.E, self.qoff = gen, E, qoff
             self.Q, self.P, self.R, self.bc = {}, {}, {}, {}
             self.built = set()
 
@@ -274,9 +275,9 @@ class RobotGen:
             A = Q[p] if ident else qmul(E, Q[p], qf)
             if fr.get("jtype") == "prismatic":
                 Pt = xform(E, self.R[p], P[p], fr["t"])
-                Q[f], P[f] = joint(E, fr, A, lambda: self.R[p] if ident else qmat(E, A), Pt)
+                Q[f], P[f] = joint(E, fr, A, lambda: self.R[p] if ident else qmat(E, A), Pt, self.qoff)
             else:
-                Q[f], _ = joint(E, fr, A, None, None)
+                Q[f], _ = joint(E, fr, A, None, None, self.qoff)
                 P[f] = xform(E, self.R[p], P[p], fr["t"])
 
         def rot(self, f):
@@ -394,6 +395,60 @@ class RobotGen:
         E.indent -= 1
         E.raw("}")
 
+    def gen_pair_inter(self) -> str:
+        """Inter-robot check of a two-arm composite of this robot (BASELINE configs[4]; the C
+        restatement is oracle/vamp_oracle.c pair_inter_collide): arm A = q0..q(d-1) at base
+        (ax, ay, az), arm B = q(d)..q(2d-1) at base (bx, by, bz).  Every link-bounding pair in
+        link order (world frame: both bases applied to every sphere); when a pair overlaps for
+        any lane of the group, the two links' sphere pairs (frames recomputed inside the block,
+        so only the 2 x 33 bounding centres stay live across the 121 tests).  Returns true on
+        a collision."""
+        m = self.m
+        dim = m["dimension"]
+        E = Emitter()
+        fa, fb = self.Frames(self, E, 0), self.Frames(self, E, dim)
+        nb = len(m["bounding"])
+
+        def wc(c, pre):
+            return [E.add(c[i], SV("var", name=f"{pre}{'xyz'[i]}")) for i in range(3)]
+
+        bca = [wc(fa.bound_center(b), "a") for b in range(nb)]
+        bcb = [wc(fb.bound_center(b), "b") for b in range(nb)]
+        spheres = m["spheres"]
+        links = [b["link"] for b in m["bounding"]]
+        for la in range(nb):
+            for lb in range(nb):
+                ra, rb = m["bounding"][la]["radius"], m["bounding"][lb]["radius"]
+                A_, B_ = bca[la], bcb[lb]
+                E.raw(f"// {links[la]} (A) vs {links[lb]} (B)")
+                E.raw(f"if (Grp::any(self_lane({A_[0].expr()}, {A_[1].expr()}, {A_[2].expr()}, {flit(ra)}, "
+                      f"{B_[0].expr()}, {B_[1].expr()}, {B_[2].expr()}, {flit(rb)}))) {{")
+                E.indent += 1
+                ga, gb = self.Frames(self, E, 0), self.Frames(self, E, dim)
+                sa_ = [i for i, sp in enumerate(spheres) if sp["link"] == links[la]]
+                sb_ = [i for i, sp in enumerate(spheres) if sp["link"] == links[lb]]
+                E.raw("uint32_t h = 0u;")
+                cb = {j: wc(gb.center(spheres[j]["frame"], spheres[j]["offset"]), "b") for j in sb_}
+                for i in sa_:
+                    ca = wc(ga.center(spheres[i]["frame"], spheres[i]["offset"]), "a")
+                    for j in sb_:
+                        E.raw(f"h |= self_bits({ca[0].expr()}, {ca[1].expr()}, {ca[2].expr()}, "
+                              f"{flit(spheres[i]['radius'])}, {cb[j][0].expr()}, {cb[j][1].expr()}, "
+                              f"{cb[j][2].expr()}, {flit(spheres[j]['radius'])});")
+                E.raw("if (Grp::any_bits(h)) return true;")
+                E.indent -= 1
+                E.raw("}")
+        E.raw("return false;")
+        args = ", ".join(f"float q{i}" for i in range(2 * dim))
+        hdr = [f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
+               "// Two-arm composite: inter-robot sphere check, bounding-first.",
+               "template <class Grp>",
+               f"__device__ __forceinline__ bool {self.name}_pair_inter(",
+               f"    {args},",
+               "    float ax, float ay, float az, float bx, float by, float bz)",
+               "{"]
+        return "\n".join(hdr + E.lines + ["}", ""])
+
     def signature(self, ret, fname, extra=""):
         dim = self.m["dimension"]
         return [f"template <class Grp, bool EXT>",
@@ -493,6 +548,8 @@ def main():
     if "--no-remat" in sys.argv:
         REMAT = False
         sys.argv.remove("--no-remat")
+    argv = [a for a in sys.argv if not a.startswith("--")]
+    sys.argv[1:3] = argv[1:3]
     model = json.load(open(sys.argv[1]))
     g = RobotGen(model)
     name = g.name
@@ -503,6 +560,8 @@ def main():
     out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
     if len(model["check_order"]) <= 32 and not any(c.get("leaf") for c in model["env_checks"]):
         out += "\n" + g.gen_staged()  # the staged pipeline keys checks by a 32-bit mask
+    if "--pair" in sys.argv:  # the composite's inter-robot check, as its own include
+        out = g.gen_pair_inter()
     open(sys.argv[2], "w").write(out)
     print(f"wrote {sys.argv[2]} ({len(out.splitlines())} lines)")
 

@@ -214,8 +214,121 @@ def make_fetch(rng):
     print("fetch_table_pick.npz", valid.mean(), valid_e.mean(), ok[:E].mean(), ok[E:].mean(), n.max())
 
 
+def make_l2_pins(rng):
+    """FloatVector<dim>::l2_norm for dim 7, 8 and 14 (ref_probe "l2norm"): the 14-lane form is
+    two registers contracted as fma(lo, lo, hi * hi) before the hsum."""
+    out = {}
+    for dim in (7, 8, 14):
+        v = (rng.normal(size=(4096, dim)) * rng.choice([1e-3, 1.0, 30.0], size=(4096, 1))).astype(F)
+        out[f"v{dim}"] = v
+        out[f"d{dim}"] = probe("l2norm", v, dim)
+    np.savez_compressed(os.path.join(GOLD, "ref_pins_l2.npz"), **out)
+
+
+def pair_inter_flat(xa, xb):
+    """min over the 59 x 59 sphere pairs of arm A vs arm B of sphere_sphere_sql2 (dot_3
+    contracted as fma(x, x, fma(z, z, y*y)), sphere_sphere.hh:10-22), per configuration."""
+    _, rad = None, None
+    r = np.asarray(RADII_PANDA, F)
+    dx = (xa[0][:, :, None] - xb[0][:, None, :]).astype(F)
+    dy = (xa[1][:, :, None] - xb[1][:, None, :]).astype(F)
+    dz = (xa[2][:, :, None] - xb[2][:, None, :]).astype(F)
+    rs = (r[:, None] + r[None, :]).astype(F)
+    d2 = fi.fma32(dx, dx, fi.fma32(dz, dz, (dy * dy).astype(F)))
+    val = fi.fma32(-rs, rs, d2)
+    return val.reshape(val.shape[0], -1)
+
+
+RADII_PANDA = None
+
+
+def make_pair(rng):
+    """Two-Panda composite (BASELINE configs[4]): per-arm masks from the reference DAG
+    (fk.hh interleaved_sphere_fk at bases (0,0,0) and (100,0,0)) and the flat 59 x 59 inter-arm
+    sphere test on the DAG's sphere_fk centres, for configurations and for 14-dof edges (rake
+    over the pinned two-register l2_norm).  There is no reference composite: this fixes the
+    composition (AND of the three) independently of the C restatement's bounding-first order."""
+    global RADII_PANDA
+    fk, cc = fi.load_panda()
+    lut, kb = op.rsqrt_probe()
+    rs = fi.RsqrtHost(lut, kb)
+    env = op.pair_scene()
+    envnp = envnp_of(env)
+    N = 8192
+    u = rng.random((N, 14), dtype=F)
+    q = np.concatenate([op.scale(u[:, :7]), op.scale(u[:, 7:])], 1)
+    va, sta = fi.run_fkcc(cc, q[:, :7], (0, 0, 0), envnp, rs, G=1)
+    vb, stb = fi.run_fkcc(cc, q[:, 7:], (100, 0, 0), envnp, rs, G=1)
+    xa, RADII_PANDA = fi.run_sphere_fk(fk, q[:, :7], (0, 0, 0))
+    xb, _ = fi.run_sphere_fk(fk, q[:, 7:], (100, 0, 0))
+    inter = pair_inter_flat([xa[i].T for i in range(3)], [xb[i].T for i in range(3)])
+    hit = (inter.view(np.uint32) >> 31).astype(bool).any(1)
+    imarg = np.abs(inter).min(1)
+    valid = va & vb & ~hit
+    tm = np.minimum(sta.test_margin, stb.test_margin)
+    cm = np.minimum(sta.cull_margin, stb.cull_margin)
+    # edges between valid composite configurations, each arm's sub-edge capped at 1.0
+    E = 1024
+    vq = q[valid]
+    s, g = vq[0:2 * E:2][:E].copy(), vq[1:2 * E:2][:E].copy()
+    for a in (slice(0, 7), slice(7, 14)):
+        d = np.linalg.norm((g[:, a] - s[:, a]).astype(np.float64), axis=1)
+        sc = np.minimum(1.0, 1.0 / np.maximum(d, 1e-9)).astype(F)
+        g[:, a] = (s[:, a] + (g[:, a] - s[:, a]) * sc[:, None]).astype(F)
+    ok, n, etm = pair_interp_validate(fk, cc, s, g, envnp, rs)
+    np.savez_compressed(os.path.join(GOLD, "pair_scene.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
+                        **{"env_" + k: v for k, v in env.arrays().items()}, q=q, valid=valid,
+                        valid_a=va, valid_b=vb, inter_hit=hit, inter_margin=imarg.astype(F), test_margin=tm.astype(F), cull_margin=cm.astype(F),
+                        starts=s, goals=g, ok=ok, n=n.astype(np.int32), edge_test_margin=etm[0].astype(F),
+                        edge_inter_margin=etm[1].astype(F))
+    print("pair_scene.npz", valid.mean(), hit.mean(), ok.mean(), n.max())
+
+
+def pair_interp_validate(fk, cc, starts, goals, envnp, rs):
+    E, D = starts.shape
+    v = (goals - starts).astype(F)
+    lo, hi = np.zeros((E, 8), F), np.zeros((E, 8), F)
+    lo[:, :8] = v[:, :8]
+    hi[:, :D - 8] = v[:, 8:]
+    sq = fi.fma32(lo, lo, (hi * hi).astype(F))
+    dist = np.sqrt((((sq[:, 0] + sq[:, 4]) + (sq[:, 2] + sq[:, 6])) + ((sq[:, 1] + sq[:, 5]) + (sq[:, 3] + sq[:, 7])))
+                   .astype(F)).astype(F)
+    n = np.maximum(np.ceil((dist / F(8) * F(32)).astype(F)), F(1)).astype(np.int64)
+    pct = (np.arange(1, 9, dtype=F) / F(8)).astype(F)
+    block = fi.fma32(v[:, None, :], pct[None, :, None], starts[:, None, :])
+    back = (v / (F(8) * n[:, None].astype(F))).astype(F)
+    ok = np.ones(E, bool)
+    alive = np.ones(E, bool)
+    tmarg = np.full(E, np.inf)
+    imarg = np.full(E, np.inf)
+    for k in range(int(n.max())):
+        if k > 0:
+            block = (block - back[:, None, :]).astype(F)
+        idx = np.where(alive & (n > k))[0]
+        if len(idx) == 0:
+            break
+        q = block[idx].reshape(-1, 14)
+        va, sa = fi.run_fkcc(cc, q[:, :7], (0, 0, 0), envnp, rs, G=8)
+        vb, sb = fi.run_fkcc(cc, q[:, 7:], (100, 0, 0), envnp, rs, G=8)
+        xa, _ = fi.run_sphere_fk(fk, q[:, :7], (0, 0, 0))
+        xb, _ = fi.run_sphere_fk(fk, q[:, 7:], (100, 0, 0))
+        inter = pair_inter_flat([xa[i].T for i in range(3)], [xb[i].T for i in range(3)])
+        hit = (inter.view(np.uint32) >> 31).astype(bool).any(1).reshape(-1, 8).any(1)
+        valid = va.reshape(-1, 8)[:, 0] & vb.reshape(-1, 8)[:, 0] & ~hit
+        m = np.minimum(sa.test_margin, sb.test_margin).reshape(-1, 8).min(1)
+        tmarg[idx] = np.minimum(tmarg[idx], m)
+        imarg[idx] = np.minimum(imarg[idx], np.abs(inter).min(1).reshape(-1, 8).min(1))
+        ok[idx] &= valid
+        alive[idx] &= valid
+    return ok, n, (tmarg, imarg)
+
+
 def main():
     os.makedirs(GOLD, exist_ok=True)
+    if "--pair" in sys.argv:
+        make_l2_pins(np.random.default_rng(20261017))
+        make_pair(np.random.default_rng(20261018))
+        return
     if "--fetch" in sys.argv:
         make_fetch(np.random.default_rng(20261016))
         return
