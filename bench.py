@@ -51,8 +51,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", default="validate", choices=["validate", "fetch_prm"],
-                    help="validate: BASELINE configs[1] (the headline); fetch_prm: configs[3] vertex stage")
+    ap.add_argument("--workload", default="validate", choices=["validate", "capt", "fetch_prm", "pair"],
+                    help="validate: BASELINE configs[1] (the headline); capt: configs[2]; fetch_prm: configs[3] "
+                         "vertex stage; pair: configs[4] two-Panda composite edges")
     ap.add_argument("--draws", type=int, default=4_000_000, help="fetch_prm: Halton draws per step (whole job)")
     return ap.parse_args()
 
@@ -279,6 +280,176 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     print(json.dumps(line))
 
 
+def timed_steps(a, torch, dist, dev, world, step):
+    """warmup, then exactly `steps` steps between barrier + synchronize; returns wall seconds"""
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    return t1 - t0
+
+
+def contract_line(a, world, wall_max, units_all, metric, unit, scaling, data, config, roofline, cpu):
+    return {"metric": metric, "value": units_all * a.steps / wall_max, "unit": unit, "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": wall_max / a.steps * 1e3, "higher_is_better": True,
+            "scaling": scaling, "vs_baseline": None, "dtype": "f32", "data": data, "config": config,
+            "roofline": roofline, "cpu_baseline": cpu}
+
+
+def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
+    """BASELINE configs[4]: two Pandas (bases (0,0,0) and (1,0,0)), 14-dof
+    edges between collision-free composite configurations, each arm's sub-edge capped at 1.0;
+    validate_motion over the composite (fkcc of both arms + inter-arm spheres).  Independent edge
+    shards per rank (weak scaling, no collective)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as op
+
+    oenv = op.pair_scene()
+    env = vamp.Environment()
+    for x, y, z, r, _ in oenv.spheres:
+        env.add_sphere(vamp.Sphere([x, y, z], r))
+    for row in oenv.cuboids + oenv.zcuboids:
+        env.add_cuboid(vamp.Cuboid.from_axes(row[0:3], row[3:6], row[6:9], row[9:12], row[12:15]))
+    robot = vamp.panda_pair
+    E = a.edges
+    g = torch.Generator(device=dev)
+    g.manual_seed(shard_seed(rank))
+    sm = torch.tensor(S_M * 2, device=dev)
+    sa = torch.tensor(S_A * 2, device=dev)
+    pool, have = [], 0
+    while have < 2 * E:
+        m = 1 << 21
+        q = torch.addcmul(sa, torch.rand((m, 14), generator=g, device=dev), sm).contiguous()
+        ok = torch.empty(m, dtype=torch.uint8, device=dev)
+        robot.fkcc_device(q.data_ptr(), m, env, ok.data_ptr(), ctx)
+        torch.cuda.synchronize(dev)
+        v = q[ok.bool()]
+        pool.append(v)
+        have += v.shape[0]
+    vq = torch.cat(pool)[: 2 * E]
+    starts, goals = vq[0::2].contiguous(), vq[1::2].clone()
+    for sl in (slice(0, 7), slice(7, 14)):
+        d = torch.linalg.vector_norm((goals[:, sl] - starts[:, sl]).double(), dim=1)
+        sc = torch.clamp(1.0 / torch.clamp(d, min=1e-9), max=1.0).float()
+        goals[:, sl] = starts[:, sl] + (goals[:, sl] - starts[:, sl]) * sc[:, None]
+    goals = goals.contiguous()
+    okd = torch.empty(E, dtype=torch.uint8, device=dev)
+    nb = torch.empty(E, dtype=torch.int32, device=dev)
+
+    def step():
+        robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, env, okd.data_ptr(), nb.data_ptr(), ctx)
+
+    wall = timed_steps(a, torch, dist, dev, world, step)
+    units = float(8 * nb.long().sum().item())
+    wall_max, units_all = reduce_over_ranks(dist, torch, wall, units, dev, world)
+    if rank != 0:
+        return
+    s_np, g_np = starts[:256].cpu().numpy(), goals[:256].cpu().numpy()
+    fl = op.pair_validate_flops(oenv, s_np, g_np)  # executed float ops per edge, reference semantics
+    f_edge = float(np.mean(fl))
+    kern_s = wall / a.steps
+    achieved = f_edge * E / kern_s / 1e12
+    cpu = None
+    if not a.no_cpu and world == 1:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        sc_, gc_ = starts[: 1 << 18].cpu().numpy(), goals[: 1 << 18].cpu().numpy()
+        n0 = 1024 * threads
+        t = time.perf_counter()
+        op.pair_validate_motions(oenv, sc_[:n0], gc_[:n0], threads=threads)
+        dt0 = max(time.perf_counter() - t, 1e-3)
+        m = int(min(len(sc_), n0 * a.cpu_seconds / dt0))
+        t = time.perf_counter()
+        okc, nbc = op.pair_validate_motions(oenv, sc_[:m], gc_[:m], threads=threads)
+        dt = time.perf_counter() - t
+        cpu = {"value": float(8 * nbc.astype(np.int64).sum()) / dt, "unit": "interpolants/s", "cores": threads,
+               "kind": "port", "sample": f"{m} edges of the same workload, oracle/vamp_oracle.c vo_pair_validate_motions, "
+                                         f"{threads} threads, {dt:.1f} s", "cpu_model": cpu_model()}
+    line = contract_line(
+        a, world, wall_max, units_all,
+        "validated edge-interpolants/sec (2x Panda 14-DOF composite FK+CC with inter-robot collision)",
+        "interpolants/s", "weak",
+        "synthetic (seeded uniform composite configurations; collision-free endpoints, each arm's sub-edge capped at 1.0)",
+        {"workload": f"BASELINE configs[4]: PandaBase<0,0,0> + PandaBase<100,0,0>, {E} edges per GPU, table + 3 spheres",
+         "robot": "panda_pair", "edges_per_gpu": E, "interpolants_per_gpu": units,
+         "edge_valid_fraction": float(okd.float().mean().item()),
+         "parallelism": f"dp{world} (independent edge shards, no collective)"},
+        {"kernel": "pair_validate_head/tail kernels (one validate_motions call)", "bound": "valu",
+         "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+         "traffic": None, "algorithmic_flops_per_edge": f_edge, "step_ms": kern_s * 1e3},
+        cpu)
+    print(json.dumps(line))
+
+
+def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
+    """BASELINE configs[2]: Panda vs a 10k-point CAPT (points on the 14
+    cage spheres, r_min 0.012, r_max 0.06, r_point 0.0025), per-configuration fkcc of 2^20 uniform
+    configurations against the point-cloud-only environment.  Independent shards per rank."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import scenes
+
+    pts = scenes.cage_points(10000, seed=1)
+    env = vamp.Environment()
+    env.add_pointcloud(pts, scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    robot = vamp.panda_0_0
+    N = a.edges
+    g = torch.Generator(device=dev)
+    g.manual_seed(2 + 7919 * rank)
+    q = torch.addcmul(torch.tensor(S_A, device=dev), torch.rand((N, 7), generator=g, device=dev),
+                      torch.tensor(S_M, device=dev)).contiguous()
+    ok = torch.empty(N, dtype=torch.uint8, device=dev)
+
+    def step():
+        robot.fkcc_device(q.data_ptr(), N, env, ok.data_ptr(), ctx)
+
+    wall = timed_steps(a, torch, dist, dev, world, step)
+    wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(N), dev, world)
+    if rank != 0:
+        return
+    import oracle_py as op
+    oenv = op.Env().add_pointcloud(pts, scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    qs = q[:2048].cpu().numpy()
+    _, _, _, fl = op.fkcc(oenv, qs, (0, 0, 0), stats=True)
+    f_cfg = float(fl.mean())
+    kern_s = wall / a.steps
+    achieved = f_cfg * N / kern_s / 1e12
+    cpu = None
+    if not a.no_cpu and world == 1:
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        qc = q[: 1 << 18].cpu().numpy()
+        n0 = 2048 * threads
+        t = time.perf_counter()
+        op.fkcc_threads(oenv, qc[:n0], (0, 0, 0), threads)
+        dt0 = max(time.perf_counter() - t, 1e-3)
+        m = int(min(len(qc), n0 * a.cpu_seconds / dt0))
+        t = time.perf_counter()
+        op.fkcc_threads(oenv, qc[:m], (0, 0, 0), threads)
+        dt = time.perf_counter() - t
+        cpu = {"value": m / dt, "unit": "configs/s", "cores": threads, "kind": "port",
+               "sample": f"{m} configurations of the same workload, oracle/vamp_oracle.c fkcc + CAPT, {threads} threads, "
+                         f"{dt:.1f} s", "cpu_model": cpu_model()}
+    line = contract_line(
+        a, world, wall_max, units_all, "CAPT point-cloud collision queries/sec (Panda 7-DOF fkcc vs 10k-point cloud)",
+        "configs/s", "weak", "synthetic (10k points on the cage spheres, seed 1; uniform Panda configurations)",
+        {"workload": f"BASELINE configs[2]: Panda 7-DOF vs 10k-point CAPT, {N} configurations per GPU",
+         "robot": "PandaBase<0,0,0>", "configs_per_gpu": N, "valid_fraction": float(ok.float().mean().item()),
+         "parallelism": f"dp{world} (independent shards, no collective)"},
+        {"kernel": "fkcc (staged, point-cloud ext path)", "bound": "valu", "achieved": achieved,
+         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
+         "algorithmic_flops_per_config": f_cfg, "step_ms": kern_s * 1e3,
+         "note": "gather/latency-bound descent + affordance scan; CAPT arrays (~4.7 MB) L2/MALL resident"},
+        cpu)
+    print(json.dumps(line))
+
+
 def main():
     a = parse()
     import torch
@@ -300,8 +471,9 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    if a.workload == "fetch_prm":
-        run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp)
+    if a.workload != "validate":
+        {"fetch_prm": run_fetch_prm, "pair": run_pair, "capt": run_capt}[a.workload](
+            a, torch, dist, rank, world, dev, stream, ctx, vamp)
         if world > 1:
             dist.destroy_process_group()
         return

@@ -122,6 +122,9 @@ def lib():
         I3 = C.c_int * 3
         L.vo_pair_fkcc_block.restype = C.c_int
         L.vo_pair_fkcc_block.argtypes = [C.POINTER(VoEnv), F32P, C.c_int, I3, I3, C.POINTER(VoStats)]
+        L.vo_pair_validate_motion.restype = C.c_int
+        L.vo_pair_validate_motion.argtypes = [C.POINTER(VoEnv), F32P, F32P, I3, I3, C.POINTER(C.c_int),
+                                              C.POINTER(VoStats)]
         L.vo_pair_fkcc_configs.argtypes = [C.POINTER(VoEnv), F32P, C.c_size_t, I3, I3, U8P, C.c_int]
         L.vo_pair_validate_motions.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_size_t, I3, I3, U8P, I32P,
                                                C.c_int]
@@ -483,3 +486,17 @@ def pair_scene() -> Env:
     for c in ((0.5, 0.55, 0.35), (0.5, -0.55, 0.35), (0.5, 0.0, 1.05)):
         e.add_sphere(c, np.float32(0.1))
     return e
+
+
+def pair_validate_flops(env: Env, starts, goals, ba=(0, 0, 0), bb=(100, 0, 0)):
+    """executed float ops of the composite validate_motion per edge (reference semantics)"""
+    ce = env.c()
+    out = np.zeros(len(starts))
+    for i in range(len(starts)):
+        st = VoStats(np.inf, np.inf, 0.0)
+        n = C.c_int()
+        lib().vo_pair_validate_motion(C.byref(ce), fp(np.ascontiguousarray(starts[i], np.float32)),
+                                      fp(np.ascontiguousarray(goals[i], np.float32)), _i3(ba), _i3(bb), C.byref(n),
+                                      C.byref(st))
+        out[i] = st.flops
+    return out
