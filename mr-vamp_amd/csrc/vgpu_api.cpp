@@ -33,23 +33,29 @@ hipError_t vgpu_launch_gather_rows(const float* q, const uint32_t* idx, const ui
                                    int dim, float* out, hipStream_t st);
 hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, size_t n_edges, uint32_t* item_edge,
                                      hipStream_t st);
-int vgpu_staged_checks(void);
-hipError_t vgpu_launch_staged_bound(int kind, const void* src0, const void* src1, const void* src2, const void* src3,
-                                    uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by,
-                                    float bz, uint32_t* mask, uint8_t* valid, uint32_t* counts, hipStream_t st);
-uint32_t vgpu_staged_blocks(int kind, uint32_t n_groups);
-uint32_t vgpu_staged_env_checks(void);
-hipError_t vgpu_launch_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,
-                                    const uint32_t* mask, uint32_t n_groups, uint32_t set, const uint8_t* valid,
-                                    uint32_t* counts, hipStream_t st);
-hipError_t vgpu_launch_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,
-                                    const uint32_t* mask, uint32_t n_groups, uint32_t set, const uint8_t* valid,
-                                    const uint32_t* offs, const uint32_t* seg, uint32_t* items, uint32_t n_items,
-                                    hipStream_t st);
-hipError_t vgpu_launch_staged_children(int kind, const void* src0, const void* src1, const void* src2,
-                                       const void* src3, uint64_t first, const uint32_t* seg, const uint32_t* items,
-                                       const EnvView* env, float bx, float by, float bz, uint8_t* valid,
-                                       hipStream_t st);
+#define VGPU_STAGED_DECL(NAME)                                                                                       \
+    int vgpu_##NAME##_staged_checks(void);                                                                           \
+    uint64_t vgpu_##NAME##_staged_env_checks(void);                                                                  \
+    int vgpu_##NAME##_staged_mask_bytes(void);                                                                       \
+    uint32_t vgpu_##NAME##_staged_blocks(int kind, uint32_t n_groups);                                               \
+    hipError_t vgpu_##NAME##_staged_bound(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
+                                          uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by, \
+                                          float bz, void* mask, uint8_t* valid, uint32_t* counts, hipStream_t st);   \
+    hipError_t vgpu_##NAME##_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
+                                          const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \
+                                          uint32_t* counts, hipStream_t st);                                         \
+    hipError_t vgpu_##NAME##_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
+                                          const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \
+                                          const uint32_t* offs, const uint32_t* seg, uint32_t* items,                \
+                                          uint32_t n_items, hipStream_t st);                                         \
+    hipError_t vgpu_##NAME##_staged_children(int kind, const void* s0, const void* s1, const void* s2,               \
+                                             const void* s3, uint64_t first, const uint32_t* seg,                    \
+                                             const uint32_t* items, const EnvView* env, float bx, float by,          \
+                                             float bz, uint8_t* valid, hipStream_t st);
+VGPU_STAGED_DECL(panda)
+VGPU_STAGED_DECL(fetch)
+hipError_t vgpu_launch_fetch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
+                                         int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
 hipError_t vgpu_launch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
                                    int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
 hipError_t vgpu_launch_capt_query(const float* centers, const float* radii, size_t n, const EnvView* env, int index,
@@ -192,7 +198,7 @@ struct vgpu_ctx {
     size_t aux_bytes = 0;
     // staged checks (vgpu_staged.hip): bounding masks, per-check counts/cursors, item list
     bool staged = true;
-    std::vector<uint32_t> rounds;  // check sets run in order (staged); empty = chosen per batch
+    std::vector<uint64_t> rounds;  // check sets run in order (staged); empty = chosen per batch
     uint32_t* st_mask = nullptr;
     size_t st_mask_cap = 0;
     uint32_t* st_cnt = nullptr;   // per-(check, block) counts, then their exclusive scan, + scan temp
@@ -260,9 +266,9 @@ extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
     if (const char* s = std::getenv("VAMP_AMD_ROUNDS")) {  // A/B: comma-separated check bit masks
         for (const char* p = s; *p;) {
             char* end = nullptr;
-            const unsigned long v = std::strtoul(p, &end, 0);
+            const unsigned long long v = std::strtoull(p, &end, 0);
             if (end == p) break;
-            c->rounds.push_back((uint32_t)v);
+            c->rounds.push_back((uint64_t)v);
             p = (*end == ',') ? end + 1 : end;
         }
     }
@@ -796,34 +802,58 @@ static int grow(vgpu_ctx* c, uint32_t** p, size_t* cap, size_t need)
     return VGPU_OK;
 }
 
-static int staged_pass(vgpu_ctx* c, int kind, const void* s0, const void* s1, const void* s2, const void* s3,
-                       uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid)
+// the staged pipeline of one robot (vgpu_staged.hh instantiations)
+struct StagedOps {
+    int (*checks)(void);
+    uint64_t (*env_checks)(void);
+    int (*mask_bytes)(void);
+    uint32_t (*blocks)(int, uint32_t);
+    hipError_t (*bound)(int, const void*, const void*, const void*, const void*, uint64_t, uint32_t, const EnvView*,
+                        float, float, float, void*, uint8_t*, uint32_t*, hipStream_t);
+    hipError_t (*count)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
+                        const uint8_t*, uint32_t*, hipStream_t);
+    hipError_t (*queue)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
+                        const uint8_t*, const uint32_t*, const uint32_t*, uint32_t*, uint32_t, hipStream_t);
+    hipError_t (*children)(int, const void*, const void*, const void*, const void*, uint64_t, const uint32_t*,
+                           const uint32_t*, const EnvView*, float, float, float, uint8_t*, hipStream_t);
+};
+#define VGPU_STAGED_OPS(NAME)                                                                                        \
+    StagedOps                                                                                                        \
+    {                                                                                                                \
+        vgpu_##NAME##_staged_checks, vgpu_##NAME##_staged_env_checks, vgpu_##NAME##_staged_mask_bytes,               \
+            vgpu_##NAME##_staged_blocks, vgpu_##NAME##_staged_bound, vgpu_##NAME##_staged_count,                     \
+            vgpu_##NAME##_staged_queue, vgpu_##NAME##_staged_children                                                \
+    }
+static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda);
+static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch);
+
+static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* s0, const void* s1, const void* s2,
+                       const void* s3, uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid)
 {
     if (n == 0) return VGPU_OK;
     if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many groups in one call (< 2^31)");
-    const int checks = vgpu_staged_checks();
+    const int checks = ops.checks();
     const uint32_t W = (kind >= 2) ? 8u : 64u;  // items per wave: 64 lanes / group size
-    const size_t nb = vgpu_staged_blocks(kind, (uint32_t)n);
+    const size_t nb = ops.blocks(kind, (uint32_t)n);
     const size_t cells = (size_t)checks * nb;
     const size_t scan_bytes = vgpu_validate_scan_bytes(cells);
     const size_t cells_al = (cells + 1 + 63) & ~(size_t)63;
     int rc;
-    if ((rc = grow(c, &c->st_mask, &c->st_mask_cap, n))) return rc;
+    if ((rc = grow(c, &c->st_mask, &c->st_mask_cap, n * (size_t)ops.mask_bytes() / 4))) return rc;
     if ((rc = grow(c, &c->st_cnt, &c->st_cnt_cap, 2 * cells_al + scan_bytes / 4 + 64))) return rc;
     if (!c->st_host) HIPCHK(c, hipHostMalloc((void**)&c->st_host, 128 * sizeof(uint32_t), hipHostMallocDefault));
     uint32_t* counts = c->st_cnt;
     uint32_t* offs = c->st_cnt + cells_al;
     void* tmp = c->st_cnt + 2 * cells_al;
     HIPCHK(c, hipMemsetAsync(counts + cells, 0, sizeof(uint32_t), c->cur));
-    HIPCHK(c, vgpu_launch_staged_bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, b[0], b[1], b[2], c->st_mask,
-                                       valid, counts, c->cur));
-    const uint32_t all = checks >= 32 ? 0xFFFFFFFFu : ((1u << checks) - 1u);
-    const uint32_t env_bits = vgpu_staged_env_checks();
+    HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, b[0], b[1], b[2], c->st_mask, valid, counts,
+                        c->cur));
+    const uint64_t all = checks >= 64 ? ~0ull : ((1ull << checks) - 1ull);
+    const uint64_t env_bits = ops.env_checks();
     // counts of every check's fired groups (all groups are valid at this point)
-    auto count_round = [&](uint32_t set, uint32_t fired[64], bool have_counts) -> int {
+    auto count_round = [&](uint64_t set, uint32_t fired[64], bool have_counts) -> int {
         if (!have_counts)
-            HIPCHK(c, vgpu_launch_staged_count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, counts,
-                                               c->cur));
+            HIPCHK(c, ops.count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, counts, c->cur));
         HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
         // segment boundaries offs[k * nb], k = 0..checks (the last one is the total)
         HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t),
@@ -833,7 +863,7 @@ static int staged_pass(vgpu_ctx* c, int kind, const void* s0, const void* s1, co
         return VGPU_OK;
     };
     // queue + children for the checks of `set`, with `fired` counted under the current flags
-    auto run_round = [&](uint32_t set, const uint32_t fired[64]) -> int {
+    auto run_round = [&](uint64_t set, const uint32_t fired[64]) -> int {
         uint32_t seg[65];
         seg[0] = 0;
         for (int k = 0; k < checks; ++k) seg[k + 1] = seg[k] + (((set >> k) & 1u) ? (fired[k] + W - 1) / W * W : 0u);
@@ -841,30 +871,29 @@ static int staged_pass(vgpu_ctx* c, int kind, const void* s0, const void* s1, co
         if (total == 0) return VGPU_OK;
         int r = grow(c, &c->st_items, &c->st_items_cap, total);
         if (r) return r;
-        HIPCHK(c, vgpu_launch_staged_queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, offs, seg,
-                                           c->st_items, (uint32_t)total, c->cur));
-        HIPCHK(c, vgpu_launch_staged_children(kind, s0, s1, s2, s3, first, seg, c->st_items, v, b[0], b[1], b[2],
-                                              valid, c->cur));
+        HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, offs, seg, c->st_items,
+                            (uint32_t)total, c->cur));
+        HIPCHK(c, ops.children(kind, s0, s1, s2, s3, first, seg, c->st_items, v, b[0], b[1], b[2], valid, c->cur));
         return VGPU_OK;
     };
     uint32_t fired[64];
     if ((rc = count_round(all, fired, true))) return rc;  // the bound kernel counted every check
-    std::vector<uint32_t> rounds = c->rounds;
+    std::vector<uint64_t> rounds(c->rounds.begin(), c->rounds.end());
     if (rounds.empty()) {
         // Rounds from this batch's bounding statistics: (1) the first three environment checks
         // that fire at all (the links that leave the base region -- they invalidate most groups
         // cheaply), (3) self checks whose bounding spheres overlap for ~every group (adjacent
         // links: many children, rarely a hit), (2) everything else.  Later rounds only see the
         // groups still valid: the reference's early exit, recovered at round granularity.
-        uint32_t r1 = 0, r3 = 0;
+        uint64_t r1 = 0, r3 = 0;
         for (int k = 0, taken = 0; k < checks && taken < 3; ++k)
-            if (((env_bits >> k) & 1u) && fired[k]) r1 |= 1u << k, ++taken;
+            if (((env_bits >> k) & 1u) && fired[k]) r1 |= 1ull << k, ++taken;
         for (int k = 0; k < checks; ++k)
-            if (!((env_bits >> k) & 1u) && fired[k] >= n - n / 100) r3 |= 1u << k;
+            if (!((env_bits >> k) & 1u) && fired[k] >= n - n / 100) r3 |= 1ull << k;
         rounds = {r1, all & ~r1 & ~r3, r3};
     }
     bool counted = true;  // `fired` is valid for the first round (no group invalidated yet)
-    for (uint32_t set : rounds) {
+    for (uint64_t set : rounds) {
         set &= all;
         if (!set) continue;
         if (!counted && (rc = count_round(set, fired, false))) return rc;
@@ -885,6 +914,7 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
     if (r->kind == VGPU_ROBOT_FETCH) {
+        if (c->staged) return staged_pass(c, kFetchStaged, 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
         HIPCHK(c, vgpu_launch_fetch_fkcc(q, n, &v, valid, c->cur));
         return VGPU_OK;
     }
@@ -894,7 +924,7 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
         HIPCHK(c, vgpu_launch_pair_fkcc(q, n, &v, pb, valid, c->cur));
         return VGPU_OK;
     }
-    if (c->staged) return staged_pass(c, 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
+    if (c->staged) return staged_pass(c, kPandaStaged, 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_fkcc(q, n, &v, b[0], b[1], b[2], valid, c->cur));
     return VGPU_OK;
 }
@@ -938,8 +968,9 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     void* tmp;
     size_t tmp_bytes;
     if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
-    const bool fetch = r->kind == VGPU_ROBOT_FETCH;  // monolithic head/tail kernels
-    const bool pair = r->kind == VGPU_ROBOT_PANDA_PAIR;
+    const bool pair = r->kind == VGPU_ROBOT_PANDA_PAIR;  // monolithic head/tail kernels
+    const bool fetch = r->kind == VGPU_ROBOT_FETCH && !c->staged;
+    const StagedOps& ops = r->kind == VGPU_ROBOT_FETCH ? kFetchStaged : kPandaStaged;
     float pb[6];
     pair_bases(r, pb);
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
@@ -948,8 +979,11 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     } else if (fetch) {
         HIPCHK(c, vgpu_launch_fetch_validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
     } else if (c->staged) {
-        if ((rc = staged_pass(c, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
-        HIPCHK(c, vgpu_launch_tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
+        if ((rc = staged_pass(c, ops, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
+        if (r->kind == VGPU_ROBOT_FETCH)
+            HIPCHK(c, vgpu_launch_fetch_tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
+        else
+            HIPCHK(c, vgpu_launch_tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
     } else {
         HIPCHK(c, vgpu_launch_panda_validate_head(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, cnt,
                                                   c->cur));
@@ -979,7 +1013,7 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     } else if (c->staged) {
         if (n_items) {
             HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
-            if ((rc = staged_pass(c, 3, starts, goals, c->items, off, 0, n_items, &v, b, ok))) return rc;
+            if ((rc = staged_pass(c, ops, 3, starts, goals, c->items, off, 0, n_items, &v, b, ok))) return rc;
         }
     } else {
         HIPCHK(c, vgpu_launch_panda_validate_tail(starts, goals, n_edges, n_items, &v, b[0], b[1], b[2], ok, cnt,
@@ -1061,10 +1095,11 @@ extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, u
     HIPCHK(c, hipSetDevice(c->device));
     if (r->kind == VGPU_ROBOT_PANDA_PAIR) return fail(c, VGPU_ERR_UNSUPPORTED, "no sampler for the composite");
     if (r->kind == VGPU_ROBOT_FETCH) {
+        if (c->staged) return staged_pass(c, kFetchStaged, 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
         HIPCHK(c, vgpu_launch_fetch_sample_fkcc(first, n, &v, q, valid, c->cur));
         return VGPU_OK;
     }
-    if (c->staged) return staged_pass(c, 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
+    if (c->staged) return staged_pass(c, kPandaStaged, 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_sample_fkcc(first, n, &v, b[0], b[1], b[2], q, valid, c->cur));
     return VGPU_OK;
 }

@@ -1,0 +1,73 @@
+// vgpu_fetch_staged.hip -- the staged collision hierarchy (vgpu_staged.hh) instantiated for the
+// Fetch (robots/fetch.hh: 8 dof, 63 checks of fetch/fk.hh:1461-16079 incl. one leaf, 64-bit check
+// masks), plus the Fetch validate head -> tail back-step counts.
+#include "vgpu_rake.hh"
+#include "vgpu_staged.hh"
+
+#include "gen/fetch_fk.inc"
+
+#ifndef VGPU_FETCH_STAGED_WAVES_PER_EU
+#define VGPU_FETCH_STAGED_WAVES_PER_EU 6
+#endif
+
+namespace vgpu {
+
+struct FetchR {
+    static constexpr int D = 8;
+    static constexpr int kRes = 32;  // robots/fetch.hh:13
+    static constexpr int kChecks = fetch_n_checks;
+    static constexpr int kWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
+    using Mask = fetch_mask_t;
+    static constexpr Mask kEnvChecks = fetch_env_check_bits;
+    __device__ static __forceinline__ void sample(uint64_t k, float v[8]) { sample_d<8>(k, fetch_s_m, fetch_s_a, v); }
+    __device__ static __forceinline__ void head(const float* s, const float* g, int lane, float v[8])
+    {
+        const RakeD<8> rk = rake_setup_d<8, kRes>(s, g);
+        rake_block_d<8>(s, rk, lane, 0, v);
+    }
+    __device__ static __forceinline__ void tail(const float* s, const float* g, int lane, int k, float v[8])
+    {
+        const RakeD<8> rk = rake_setup_d<8, kRes>(s, g);
+        rake_block_d<8>(s, rk, lane, k, v);
+    }
+    template <class Grp, bool EXT>
+    __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, float, float, float)
+    {
+        return fetch_bound_mask<Grp, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], env, 0.0f, 0.0f, 0.0f);
+    }
+    template <class Grp, bool EXT>
+    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, float, float, float)
+    {
+        return fetch_children<Grp, EXT>(c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], env, 0.0f, 0.0f, 0.0f);
+    }
+};
+
+__global__ __launch_bounds__(kStagedBlock) void fetch_tail_counts_kernel(const float* __restrict__ starts,
+                                                                         const float* __restrict__ goals,
+                                                                         size_t n_edges,
+                                                                         const uint8_t* __restrict__ ok,
+                                                                         int32_t* __restrict__ n_blocks,
+                                                                         uint32_t* __restrict__ cnt)
+{
+    const size_t e = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
+    if (e >= n_edges) return;
+    const RakeD<8> rk = rake_setup_d<8, FetchR::kRes>(starts + 8 * e, goals + 8 * e);
+    if (n_blocks) n_blocks[e] = rk.n;
+    cnt[e] = (ok[e] && rk.n > 1) ? (uint32_t)(rk.n - 1) : 0u;
+}
+
+}  // namespace vgpu
+
+VGPU_STAGED_EXPORTS(vgpu::FetchR, fetch)
+
+extern "C" hipError_t vgpu_launch_fetch_tail_counts(const float* starts, const float* goals, size_t n_edges,
+                                                    const uint8_t* ok, int32_t* n_blocks, uint32_t* cnt,
+                                                    hipStream_t st)
+{
+    hipError_t err = hipMemsetAsync(cnt + n_edges, 0, sizeof(uint32_t), st);
+    if (err != hipSuccess || n_edges == 0) return err;
+    const unsigned grid = (unsigned)((n_edges + vgpu::kStagedBlock - 1) / vgpu::kStagedBlock);
+    hipLaunchKernelGGL(vgpu::fetch_tail_counts_kernel, dim3(grid), dim3(vgpu::kStagedBlock), 0, st, starts, goals,
+                       n_edges, ok, n_blocks, cnt);
+    return hipGetLastError();
+}

@@ -503,22 +503,25 @@ class RobotGen:
         evaluated check by check instead of in one divergent pass."""
         m = self.m
         order = m["check_order"]
-        assert len(order) <= 32
+        assert len(order) <= 64
+        wide = len(order) > 32
+        mt, one = ("uint64_t", "1ull") if wide else ("uint32_t", "1u")
         E = Emitter()
         fr = self.Frames(self, E)
-        E.raw("uint32_t mask = 0u;")
+        E.raw(f"{mt} mask = 0u;")
         for c, o in enumerate(order):
             kind, test, ck = self.bound_test(fr, o)
             if kind == "env":
-                E.raw(f"if (Grp::any_bits({test})) mask |= {1 << c}u;")
+                E.raw(f"if (Grp::any_bits({test})) mask |= {one} << {c};")
             else:
-                E.raw(f"if (Grp::any({test})) mask |= {1 << c}u;")
+                E.raw(f"if (Grp::any({test})) mask |= {one} << {c};")
         E.raw("return mask;")
         env_bits = sum(1 << c for c, o in enumerate(order) if o["kind"] == "env")
         out = [f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
                f"constexpr int {self.name}_n_checks = {len(order)};",
-               f"constexpr uint32_t {self.name}_env_check_bits = {env_bits:#x}u;  // environment checks"]
-        out += self.signature("uint32_t", "bound_mask") + E.lines + ["}", ""]
+               f"using {self.name}_mask_t = {mt};",
+               f"constexpr {mt} {self.name}_env_check_bits = {env_bits:#x}{'ull' if wide else 'u'};  // environment checks"]
+        out += self.signature(mt, "bound_mask") + E.lines + ["}", ""]
         body = []
         for c, o in enumerate(order):
             E = Emitter()
@@ -527,6 +530,9 @@ class RobotGen:
             kind = o["kind"]
             ck = m["env_checks"][o["index"]] if kind == "env" else m["self_checks"][o["index"]]
             label = ck["link"] if kind == "env" else " vs ".join(ck["links"])
+            if kind == "env" and ck.get("leaf"):  # the bounding hit itself is the collision
+                body += [f"    case {c}: {{  // env: {label} (leaf)", "        return true;", "    }"]
+                continue
             # frames first, outside the chunk scopes of emit_children
             if kind == "env":
                 for kid in ck["children"]:
@@ -558,8 +564,7 @@ def main():
         vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model[key])
         consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
     out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
-    if len(model["check_order"]) <= 32 and not any(c.get("leaf") for c in model["env_checks"]):
-        out += "\n" + g.gen_staged()  # the staged pipeline keys checks by a 32-bit mask
+    out += "\n" + g.gen_staged()  # check masks: 32-bit up to 32 checks, 64-bit up to 64
     if "--pair" in sys.argv:  # the composite's inter-robot check, as its own include
         out = g.gen_pair_inter()
     open(sys.argv[2], "w").write(out)
