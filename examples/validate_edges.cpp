@@ -12,6 +12,18 @@
 
 using namespace vamp_gpu;
 
+// The other robot types of the mirror, instantiated so the header's templates are compiled
+// (-Wall -Werror in tests/test_c_abi.py): Fetch and the two-Panda composite.
+[[maybe_unused]] static auto other_robots(collision::Environment &env) -> std::size_t
+{
+    const robots::Fetch::Configuration qf{0.1f, 0.0f, 0.5f, 0.0f, 1.0f, 0.0f, 1.0f, 0.0f};
+    const robots::Panda_Pair::Configuration qp{};
+    const bool a = robots::Fetch::fkcc(env, qf);
+    const auto b = planning::validate_motions<robots::Fetch>(env, {qf}, {qf});
+    const bool c = planning::validate_motion<robots::Panda_Pair>(env, qp, qp);
+    return (a ? 1u : 0u) + b.size() + (c ? 1u : 0u);
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 3)

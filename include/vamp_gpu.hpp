@@ -118,9 +118,51 @@ namespace vamp_gpu
 
     namespace robots
     {
+        // The batched calls every robot type shares (Derived provides c_robot(), dimension,
+        // n_spheres and Configuration).
+        template <typename Derived>
+        struct RobotOps
+        {
+            // fkcc<rake> of one configuration broadcast to the rake == validate(q) without the
+            // joint-limit check (bindings/common.hh:172-182)
+            template <typename Configuration>
+            static auto fkcc(collision::Environment &env, const Configuration &q) -> bool
+            {
+                return fkcc(env, std::vector<Configuration>{q})[0] != 0;
+            }
+
+            template <typename Configuration>
+            static auto fkcc(collision::Environment &env, const std::vector<Configuration> &q)
+                -> std::vector<uint8_t>
+            {
+                std::vector<uint8_t> out(q.size());
+                const vgpu_robot r = Derived::c_robot();
+                vgpu_ctx *c = env.context().handle();
+                check(vgpu_fkcc_host(c, &r, env.handle(), q.empty() ? nullptr : q[0].data(), q.size(),
+                                     out.data()),
+                      c, "vgpu_fkcc_host");
+                return out;
+            }
+
+            // sphere_fk<1>: world-frame centres of the collision spheres (radii are constants)
+            template <typename Configuration>
+            static auto sphere_fk(Context &ctx, const Configuration &q)
+            {
+                constexpr std::size_t ns = Derived::n_spheres;
+                std::vector<float> soa(3 * ns);
+                const vgpu_robot r = Derived::c_robot();
+                check(vgpu_sphere_fk_host(ctx.handle(), &r, q.data(), 1, soa.data()), ctx.handle(),
+                      "vgpu_sphere_fk_host");
+                std::array<std::array<float, 3>, ns> out{};
+                for (std::size_t s = 0; s < ns; ++s)
+                    for (int c = 0; c < 3; ++c) out[s][c] = soa[c * ns + s];
+                return out;
+            }
+        };
+
         // vamp::robots::PandaBase<X100, Y100, Z100> (robots/panda_base.hh:15-75)
         template <int BaseX100, int BaseY100, int BaseZ100>
-        struct PandaBase
+        struct PandaBase : RobotOps<PandaBase<BaseX100, BaseY100, BaseZ100>>
         {
             static constexpr auto name = "panda";
             static constexpr std::size_t dimension = 7;
@@ -135,39 +177,38 @@ namespace vamp_gpu
 
             static auto c_robot() noexcept -> vgpu_robot
             {
-                return vgpu_robot{VGPU_ROBOT_PANDA, BaseX100, BaseY100, BaseZ100};
+                return vgpu_robot{VGPU_ROBOT_PANDA, BaseX100, BaseY100, BaseZ100, 0, 0, 0};
             }
+        };
 
-            // fkcc<rake> of one configuration broadcast to the rake == validate(q) without the
-            // joint-limit check (bindings/common.hh:172-182)
-            static auto fkcc(collision::Environment &env, const Configuration &q) -> bool
-            {
-                return fkcc(env, std::vector<Configuration>{q})[0] != 0;
-            }
+        // vamp::robots::Fetch (robots/fetch.hh:8-48): 8 dof (prismatic torso first), 111 spheres
+        struct Fetch : RobotOps<Fetch>
+        {
+            static constexpr auto name = "fetch";
+            static constexpr std::size_t dimension = 8;
+            static constexpr std::size_t resolution = 32;
+            static constexpr std::size_t n_spheres = 111;
+            using Configuration = std::array<float, dimension>;
+            using Spheres = std::array<std::array<float, 3>, n_spheres>;
 
-            static auto fkcc(collision::Environment &env, const std::vector<Configuration> &q)
-                -> std::vector<uint8_t>
-            {
-                std::vector<uint8_t> out(q.size());
-                const vgpu_robot r = c_robot();
-                vgpu_ctx *c = env.context().handle();
-                check(vgpu_fkcc_host(c, &r, env.handle(), q.empty() ? nullptr : q[0].data(), q.size(),
-                                     out.data()),
-                      c, "vgpu_fkcc_host");
-                return out;
-            }
+            static auto c_robot() noexcept -> vgpu_robot { return vgpu_robot{VGPU_ROBOT_FETCH, 0, 0, 0, 0, 0, 0}; }
+        };
 
-            // sphere_fk<1> (fk.hh:104-1333): world-frame centres of the 59 collision spheres
-            static auto sphere_fk(Context &ctx, const Configuration &q) -> Spheres
+        // Two Pandas as one 14-dof robot (BASELINE configs[4]; no reference counterpart):
+        // joints 0..6 = PandaBase<A>, 7..13 = PandaBase<B>; valid = fkcc_A && fkcc_B && no A-B
+        // sphere overlap.  fkcc and validate_motions only (sphere_fk: use each arm's type).
+        template <int AX, int AY, int AZ, int BX, int BY, int BZ>
+        struct PandaPair : RobotOps<PandaPair<AX, AY, AZ, BX, BY, BZ>>
+        {
+            static constexpr auto name = "panda_pair";
+            static constexpr std::size_t dimension = 14;
+            static constexpr std::size_t resolution = 32;
+            static constexpr std::size_t n_spheres = 118;
+            using Configuration = std::array<float, dimension>;
+
+            static auto c_robot() noexcept -> vgpu_robot
             {
-                std::vector<float> soa(3 * n_spheres);
-                const vgpu_robot r = c_robot();
-                check(vgpu_sphere_fk_host(ctx.handle(), &r, q.data(), 1, soa.data()), ctx.handle(),
-                      "vgpu_sphere_fk_host");
-                Spheres out{};
-                for (std::size_t s = 0; s < n_spheres; ++s)
-                    for (int c = 0; c < 3; ++c) out[s][c] = soa[c * n_spheres + s];
-                return out;
+                return vgpu_robot{VGPU_ROBOT_PANDA_PAIR, AX, AY, AZ, BX, BY, BZ};
             }
         };
 
@@ -176,6 +217,8 @@ namespace vamp_gpu
         struct Panda_0_0 : PandaBase<0, 0, 0> { static constexpr auto name = "panda_0_0"; };
         struct Panda_1_0 : PandaBase<100, 0, 0> { static constexpr auto name = "panda_1_0"; };
         struct Panda_2_2 : PandaBase<200, 200, 0> { static constexpr auto name = "panda_2_2"; };
+        // the configs[4] composite: arms 1 m apart along x
+        using Panda_Pair = PandaPair<0, 0, 0, 100, 0, 0>;
     }  // namespace robots
 
     namespace planning

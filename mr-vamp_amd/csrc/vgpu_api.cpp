@@ -201,6 +201,8 @@ struct vgpu_ctx {
     std::vector<uint64_t> rounds;  // check sets run in order (staged); empty = chosen per batch
     uint32_t* st_mask = nullptr;
     size_t st_mask_cap = 0;
+    uint32_t* st_q = nullptr;  // staged sampling without a caller buffer: the drawn configurations
+    size_t st_q_cap = 0;
     uint32_t* st_cnt = nullptr;   // per-(check, block) counts, then their exclusive scan, + scan temp
     size_t st_cnt_cap = 0;
     uint32_t* st_host = nullptr;  // pinned: the 33 segment boundaries of the scan
@@ -299,6 +301,7 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->items) (void)hipFree(c->items);
     if (c->aux) (void)hipFree(c->aux);
     if (c->st_mask) (void)hipFree(c->st_mask);
+    if (c->st_q) (void)hipFree(c->st_q);
     if (c->st_cnt) (void)hipFree(c->st_cnt);
     if (c->st_items) (void)hipFree(c->st_items);
     if (c->st_host) (void)hipHostFree(c->st_host);
@@ -1094,6 +1097,12 @@ extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, u
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
     if (r->kind == VGPU_ROBOT_PANDA_PAIR) return fail(c, VGPU_ERR_UNSUPPORTED, "no sampler for the composite");
+    if (c->staged && !q) {  // the children stage reads the bound stage's samples back
+        int32_t dim = 0;
+        vgpu_robot_info(r->kind, &dim, nullptr, nullptr);
+        if ((rc = grow(c, &c->st_q, &c->st_q_cap, n * (size_t)dim))) return rc;
+        q = (float*)c->st_q;
+    }
     if (r->kind == VGPU_ROBOT_FETCH) {
         if (c->staged) return staged_pass(c, kFetchStaged, 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
         HIPCHK(c, vgpu_launch_fetch_sample_fkcc(first, n, &v, q, valid, c->cur));

@@ -120,12 +120,25 @@ __device__ __forceinline__ void halton_index(uint64_t k, uint32_t& idx, uint32_t
     }
 }
 
+// Radical inverse of idx (< 2^24: idx <= 1,000,001 within a cycle) in base b.  The digit
+// division uses a float reciprocal estimate of idx / b (exact float operands; |error| < 1) and one
+// integer correction step, so every quotient and remainder is the exact integer one -- no
+// hardware integer divide (a ~40-instruction sequence on CDNA) per digit.
 __device__ __forceinline__ float halton_coord(uint32_t idx, uint32_t b)
 {
+    const float inv = 1.0f / (float)b;
     uint32_t num = 0, den = 1;
     while (idx) {
-        const uint32_t q = idx / b;
-        num = num * b + (idx - q * b);
+        uint32_t q = (uint32_t)((float)idx * inv);
+        int32_t r = (int32_t)(idx - q * b);
+        if (r < 0) {
+            q -= 1u;
+            r += (int32_t)b;
+        } else if (r >= (int32_t)b) {
+            q += 1u;
+            r -= (int32_t)b;
+        }
+        num = num * b + (uint32_t)r;
         den *= b;
         idx = q;
     }

@@ -61,8 +61,18 @@ struct SrcSamplesT {  // Halton draw first + g, scaled
     static constexpr int G = 1;
     static constexpr bool kInit = true;
     uint64_t first;
-    float* q_out;  // optional copy of the sample (written by the bound stage)
-    __device__ void load(uint32_t g, int, float v[R::D]) const { R::sample(first + g, v); }
+    float* q_out;       // bound stage: copy of the sample (optional)
+    const float* q_in;  // children stage: the bound stage's copy (else the draw is recomputed)
+    __device__ void load(uint32_t g, int, float v[R::D]) const
+    {
+        if (q_in) {
+            const float* p = q_in + R::D * (size_t)g;
+#pragma unroll
+            for (int j = 0; j < R::D; ++j) v[j] = p[j];
+        } else {
+            R::sample(first + g, v);
+        }
+    }
     __device__ uint32_t out(uint32_t g) const { return g; }
 };
 
@@ -349,7 +359,7 @@ struct StagedHost {
         case 0:
             return fn(SrcConfigsT<R>{(const float*)s0});
         case 1:
-            return fn(SrcSamplesT<R>{first, (float*)s0});
+            return fn(SrcSamplesT<R>{first, (float*)s0, nullptr});
         case 2:
             return fn(SrcHeadT<R>{(const float*)s0, (const float*)s1});
         case 3:
@@ -410,7 +420,10 @@ struct StagedHost {
     {                                                                                                                \
         using H = vgpu::StagedHost<R>;                                                                               \
         return H::with_source(kind, s0, s1, s2, s3, first, [&](auto src) {                                          \
-            if constexpr (std::is_same<decltype(src), vgpu::SrcSamplesT<R>>::value) src.q_out = nullptr;            \
+            if constexpr (std::is_same<decltype(src), vgpu::SrcSamplesT<R>>::value) {                                \
+                src.q_in = src.q_out; /* the samples the bound stage wrote */                                         \
+                src.q_out = nullptr;                                                                                 \
+            }                                                                                                        \
             return H::children(src, seg, items, env, bx, by, bz, valid, st);                                         \
         });                                                                                                          \
     }                                                                                                                \
