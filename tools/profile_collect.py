@@ -37,7 +37,7 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
             if "sphere_fk" not in name[d][0]:
                 step_bytes[c] += v
         if c == "FETCH_SIZE":
-            calls = sum(1 for d in byd if name[d][0].startswith("bound_kernel<SrcHead")) or \
+            calls = sum(1 for d in byd if name[d][0].startswith("bound_kernel<") and "SrcHead" in name[d][0]) or \
                 sum(1 for d in byd if name[d][0].startswith("panda_validate_head_kernel"))
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes (tools/profile_round.sh {R}), "
                   "bench.py 2^20-edge cage workload, every validate_motions kernel; "
