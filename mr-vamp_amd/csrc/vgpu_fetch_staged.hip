@@ -17,6 +17,7 @@ struct FetchR {
     static constexpr int kRes = 32;  // robots/fetch.hh:13
     static constexpr int kChecks = fetch_n_checks;
     static constexpr int kWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
+    static constexpr int kChildWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
     using Mask = fetch_mask_t;
     static constexpr Mask kEnvChecks = fetch_env_check_bits;
     __device__ static __forceinline__ void sample(uint64_t k, float v[8]) { sample_d<8>(k, fetch_s_m, fetch_s_a, v); }

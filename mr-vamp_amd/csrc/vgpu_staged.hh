@@ -261,7 +261,7 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
 
 // ---- stage 2: children, one check per wave ------------------------------------------------------
 template <class R, class Src, bool EXT>
-__global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void children_kernel(Src src, SegTableT<R> seg,
+__global__ __launch_bounds__(kStagedBlock, R::kChildWavesPerEU) void children_kernel(Src src, SegTableT<R> seg,
                                                                                 const uint32_t* __restrict__ items,
                                                                                 EnvView env, float bx, float by,
                                                                                 float bz, uint8_t* __restrict__ valid)

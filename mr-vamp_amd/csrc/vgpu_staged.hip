@@ -10,6 +10,11 @@ struct PandaR {
     static constexpr int D = 7;
     static constexpr int kChecks = panda_n_checks;
     static constexpr int kWavesPerEU = VGPU_WAVES_PER_EU;
+#ifdef VGPU_CHILD_WAVES_PER_EU
+    static constexpr int kChildWavesPerEU = VGPU_CHILD_WAVES_PER_EU;
+#else
+    static constexpr int kChildWavesPerEU = VGPU_WAVES_PER_EU;
+#endif
     using Mask = panda_mask_t;
     static constexpr Mask kEnvChecks = panda_env_check_bits;
     __device__ static __forceinline__ void sample(uint64_t k, float v[7]) { panda_sample(k, v); }

@@ -118,6 +118,8 @@ float vo_capt_vol_ball(const float p[3], const float lo[3], const float up[3]);
  * (robots/panda_base.hh:15-75), Fetch (robots/fetch.hh:8-48, 8 dof, no base offset) */
 #define VO_ROBOT_PANDA 1
 #define VO_ROBOT_FETCH 2
+#define VO_ROBOT_UR5 4    /* robots/ur5.hh: 6 dof */
+#define VO_ROBOT_BAXTER 5 /* robots/baxter.hh: 14 dof dual arm, resolution 64 */
 int vo_robot_dim(int robot);
 int vo_robot_nspheres(int robot);
 float vo_l2_norm(const float *v, int dim);                                   /* dim <= 16 */

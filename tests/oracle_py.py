@@ -357,7 +357,8 @@ def validate_flops(env: Env, starts, goals, base100=(0, 0, 0)):
 
 
 # ---- robot-generic views (robot = "panda" | "fetch"; ids match VGPU_ROBOT_*) ----
-ROBOTS = {"panda": (1, 7, 59), "fetch": (2, 8, 111)}
+ROBOTS = {"panda": (1, 7, 59), "fetch": (2, 8, 111), "ur5": (4, 6, 36), "baxter": (5, 14, 75)}
+RESOLUTION = {"panda": 32, "fetch": 32, "ur5": 32, "baxter": 64}  # Robot::resolution
 
 
 def robot_scale(robot, u):

@@ -44,6 +44,10 @@ ROBOTS = {
                   root="panda_link0", resolution=32, has_base=True),
     "fetch": dict(urdf="resources/fetch/fetch_spherized.urdf", fk="src/impl/vamp/robots/fetch/fk.hh",
                   root="base_link", resolution=32, has_base=False),
+    "ur5": dict(urdf="resources/ur5/ur5_spherized.urdf", fk="src/impl/vamp/robots/ur5/fk.hh",
+                root="offset_link", resolution=32, has_base=False),         # robots/ur5.hh:11-12
+    "baxter": dict(urdf="resources/baxter/baxter_spherized.urdf", fk="src/impl/vamp/robots/baxter/fk.hh",
+                   root="base", resolution=64, has_base=False),             # robots/baxter.hh:11-12
 }
 
 
@@ -147,7 +151,10 @@ def extract_robot(ref, robot):
             children.append(dict(sphere=s, base=has_base(i, range(3))))
         b = dict(link=link, frame=fidx, offset=[float(round(v, 6)) for v in loc[0]], radius=r, base=has_base(t, range(3)))
         bounding[link] = b
-        env_checks.append(dict(link=link, bounding_base=b["base"], children=children))
+        ck = dict(link=link, bounding_base=b["base"], children=children)
+        if not kids:  # a labeled single-sphere link tested directly (ur5/fk.hh fts_robotside): leaf
+            ck["leaf"] = True
+        env_checks.append(ck)
 
     def entity(pts, r):
         s = sphere_at(pts, r)

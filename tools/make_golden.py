@@ -123,17 +123,23 @@ def sphere_cage():
     return e, fi.EnvNP(spheres=e.arrays()["spheres"])
 
 
-def interp_validate(cc, starts, goals, base, envnp, rs):
+def interp_validate(cc, starts, goals, base, envnp, rs, res=32):
     """validate_motion (planning/validate.hh:23-75) over E edges, 8-lane groups."""
     E, D = starts.shape
     v = (goals - starts).astype(F)
-    sq = np.zeros((E, 8), F)
-    sq[:, :D] = (v * v).astype(F)
+    if D <= 8:
+        sq = np.zeros((E, 8), F)
+        sq[:, :D] = (v * v).astype(F)
+    else:  # two registers: fma(lo, lo, hi * hi) (ref_probe "l2norm")
+        lo, hi = np.zeros((E, 8), F), np.zeros((E, 8), F)
+        lo[:, :] = v[:, :8]
+        hi[:, :D - 8] = v[:, 8:]
+        sq = fi.fma32(lo, lo, (hi * hi).astype(F))
     dist = np.sqrt((((sq[:, 0] + sq[:, 4]) + (sq[:, 2] + sq[:, 6])) + ((sq[:, 1] + sq[:, 5]) + (sq[:, 3] + sq[:, 7])))
                    .astype(F)).astype(F)
-    n = np.maximum(np.ceil((dist / F(8) * F(32)).astype(F)), F(1)).astype(np.int64)
+    n = np.maximum(np.ceil((dist / F(8) * F(res)).astype(F)), F(1)).astype(np.int64)
     pct = (np.arange(1, 9, dtype=F) / F(8)).astype(F)
-    block = fi.fma32(v[:, None, :], pct[None, :, None], starts[:, None, :])  # (E, 8, 7)
+    block = fi.fma32(v[:, None, :], pct[None, :, None], starts[:, None, :])  # (E, 8, D)
     back = (v / (F(8) * n[:, None].astype(F))).astype(F)
     ok = np.ones(E, bool)
     tmarg = np.full(E, np.inf)
@@ -169,32 +175,33 @@ def envnp_of(env):
                     zcuboids=a["zcuboids"])
 
 
-def make_fetch(rng):
-    """Fetch (robots/fetch.hh, 8 dof): FK centres, per-configuration masks and edges on the
-    empty scene and MotionBenchMaker table_pick_fetch scene0001, from the reference's generated
-    fetch/fk.hh evaluated by tools/fkhh_interp.py."""
-    src = open("/root/reference/src/impl/vamp/robots/fetch/fk.hh").read()
+def make_robot(rng, robot, scene, out_name, n_cfg=16384, n_empty=4096, n_edges=1024):
+    """A generated robot (fetch, ur5, baxter): FK centres, per-configuration masks and edges on
+    the empty scene and one MotionBenchMaker scene, from the reference's generated
+    robots/<robot>/fk.hh evaluated by tools/fkhh_interp.py."""
+    src = open(f"/root/reference/src/impl/vamp/robots/{robot}/fk.hh").read()
     fk = fi.parse_function(src, r"inline void sphere_fk\(")
     cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
+    dim = op.ROBOTS[robot][1]
     lut, kb = op.rsqrt_probe()
     rs = fi.RsqrtHost(lut, kb)
-    q = op.robot_scale("fetch", rng.random((1024, 8), dtype=F))
+    q = op.robot_scale(robot, rng.random((1024, dim), dtype=F))
     xyz, r = fi.run_sphere_fk(fk, q, (0, 0, 0))
-    np.savez_compressed(os.path.join(GOLD, "fk_fetch.npz"), q=q, radii=r.astype(F),
+    np.savez_compressed(os.path.join(GOLD, f"fk_{robot}.npz"), q=q, radii=r.astype(F),
                         xyz=np.ascontiguousarray(np.transpose(xyz, (2, 1, 0))))
-    print("fk_fetch.npz")
-    env = op.mbm_env(mbm_scene("fetch", "table_pick_fetch/scene0001.yaml"))
+    print(f"fk_{robot}.npz")
+    env = op.mbm_env(mbm_scene(robot, scene))
     arr = env.arrays()
     envnp = envnp_of(env)
     empty = fi.EnvNP(spheres=np.zeros((0, 5), F))
-    q = op.robot_scale("fetch", rng.random((16384, 8), dtype=F))
+    q = op.robot_scale(robot, rng.random((n_cfg, dim), dtype=F))
     valid, st = fi.run_fkcc(cc, q, (0, 0, 0), envnp, rs, G=1)
-    qe = op.robot_scale("fetch", rng.random((4096, 8), dtype=F))
+    qe = op.robot_scale(robot, rng.random((n_empty, dim), dtype=F))
     valid_e, st_e = fi.run_fkcc(cc, qe, (0, 0, 0), empty, rs, G=1)
     # edges: raw pairs (short) and valid-endpoint pairs capped at length 1.0
-    E = 1024
-    s = op.robot_scale("fetch", rng.random((E, 8), dtype=F))
-    g = op.robot_scale("fetch", rng.random((E, 8), dtype=F))
+    E = n_edges
+    s = op.robot_scale(robot, rng.random((E, dim), dtype=F))
+    g = op.robot_scale(robot, rng.random((E, dim), dtype=F))
     g = (s + (g - s) * F(0.25)).astype(F)
     vq = q[valid]
     sb, gb = vq[0:2 * E:2][:E], vq[1:2 * E:2][:E]
@@ -204,14 +211,18 @@ def make_fetch(rng):
     starts = np.concatenate([s, sb])
     goals = np.concatenate([g, gb])
     starts[:4] = goals[:4]
-    ok, n, tm, cm = interp_validate(cc, starts, goals, (0, 0, 0), envnp, rs)
-    np.savez_compressed(os.path.join(GOLD, "fetch_table_pick.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
+    ok, n, tm, cm = interp_validate(cc, starts, goals, (0, 0, 0), envnp, rs, op.RESOLUTION[robot])
+    np.savez_compressed(os.path.join(GOLD, out_name), rsqrt_lut=lut, rsqrt_kbits=kb,
                         **{"env_" + k: v for k, v in arr.items()},
                         q=q, valid=valid, test_margin=st.test_margin.astype(F), cull_margin=st.cull_margin.astype(F),
                         q_empty=qe, valid_empty=valid_e, test_margin_empty=st_e.test_margin.astype(F),
                         starts=starts, goals=goals, ok=ok, n=n.astype(np.int32), edge_test_margin=tm.astype(F),
                         edge_cull_margin=cm.astype(F))
-    print("fetch_table_pick.npz", valid.mean(), valid_e.mean(), ok[:E].mean(), ok[E:].mean(), n.max())
+    print(out_name, valid.mean(), valid_e.mean(), ok[:E].mean(), ok[E:].mean(), n.max())
+
+
+def make_fetch(rng):
+    make_robot(rng, "fetch", "table_pick_fetch/scene0001.yaml", "fetch_table_pick.npz")
 
 
 def make_l2_pins(rng):
@@ -331,6 +342,13 @@ def main():
         return
     if "--fetch" in sys.argv:
         make_fetch(np.random.default_rng(20261016))
+        return
+    if "--ur5" in sys.argv:
+        make_robot(np.random.default_rng(20261019), "ur5", "table_pick_ur5/scene0001.yaml", "ur5_table_pick.npz")
+        return
+    if "--baxter" in sys.argv:
+        make_robot(np.random.default_rng(20261020), "baxter", "bookshelf_tall_both_arms_easy_baxter/scene0001.yaml",
+                   "baxter_bookshelf.npz", n_cfg=8192, n_empty=2048, n_edges=512)
         return
     if not os.path.exists(PROBE):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "ref"])

@@ -112,6 +112,8 @@ def build_frames(links, joints, root_link):
     children: Dict[str, List[dict]] = {}
     for j in joints:
         children.setdefault(j["parent"], []).append(j)
+    movable = [j["name"] for j in joints if j["type"] in ("revolute", "continuous", "prismatic")
+               and (links.get(j["child"]) or children.get(j["child"]))]
     frames = [dict(name=root_link, parent=-1, t=[0.0, 0.0, 0.0], qf=[1.0, 0.0, 0.0, 0.0], dof=-1, jtype="root")]
     dof = 0
     order = [root_link]
@@ -132,7 +134,10 @@ def build_frames(links, joints, root_link):
                 # the other two components structurally zero
                 assert sorted(abs(v) for v in j["axis"]) == [0.0, 0.0, 1.0], f"axis {j['axis']} ({j['name']})"
                 axis = [float(v) for v in j["axis"]]
-                d = dof
+                # configuration index = the joint's position among the URDF's movable joints in
+                # document order (the reference generator's q order; BFS order differs for
+                # branching robots such as Baxter's two arms)
+                d = movable.index(j["name"])
                 dof += 1
             frames.append(
                 dict(name=c, parent=idx[ln], t=[float(v) for v in j["xyz"]], qf=qf, dof=d,
