@@ -21,7 +21,10 @@ using namespace vamp_gpu;
     const bool a = robots::Fetch::fkcc(env, qf);
     const auto b = planning::validate_motions<robots::Fetch>(env, {qf}, {qf});
     const bool c = planning::validate_motion<robots::Panda_Pair>(env, qp, qp);
-    return (a ? 1u : 0u) + b.size() + (c ? 1u : 0u);
+    const bool d = robots::UR5::fkcc(env, robots::UR5::Configuration{});
+    const bool e = planning::validate_motion<robots::Baxter>(env, robots::Baxter::Configuration{},
+                                                             robots::Baxter::Configuration{});
+    return (a ? 1u : 0u) + b.size() + (c ? 1u : 0u) + (d ? 1u : 0u) + (e ? 1u : 0u);
 }
 
 int main(int argc, char **argv)

@@ -51,6 +51,11 @@ typedef struct vgpu_env vgpu_env;
  * The reference has no composite robot; validity = fkcc_A && fkcc_B && no A-B sphere overlap
  * (link-bounding pairs first), composed from the reference primitives. */
 #define VGPU_ROBOT_PANDA_PAIR 3
+/* kind = VGPU_ROBOT_UR5: vamp::robots::UR5 (robots/ur5.hh: 6 dof, 36 spheres, resolution 32);
+ * kind = VGPU_ROBOT_BAXTER: vamp::robots::Baxter (robots/baxter.hh: 14-dof dual arm, 75 spheres,
+ * resolution 64).  Neither has a base offset (base_*100 must be 0). */
+#define VGPU_ROBOT_UR5 4
+#define VGPU_ROBOT_BAXTER 5
 typedef struct vgpu_robot {
     int32_t kind;
     int32_t base_x100, base_y100, base_z100;

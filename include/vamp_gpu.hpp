@@ -194,6 +194,28 @@ namespace vamp_gpu
             static auto c_robot() noexcept -> vgpu_robot { return vgpu_robot{VGPU_ROBOT_FETCH, 0, 0, 0, 0, 0, 0}; }
         };
 
+        // vamp::robots::UR5 (robots/ur5.hh): 6 dof, 36 spheres
+        struct UR5 : RobotOps<UR5>
+        {
+            static constexpr auto name = "ur5";
+            static constexpr std::size_t dimension = 6;
+            static constexpr std::size_t resolution = 32;
+            static constexpr std::size_t n_spheres = 36;
+            using Configuration = std::array<float, dimension>;
+            static auto c_robot() noexcept -> vgpu_robot { return vgpu_robot{VGPU_ROBOT_UR5, 0, 0, 0, 0, 0, 0}; }
+        };
+
+        // vamp::robots::Baxter (robots/baxter.hh): 14-dof dual arm, 75 spheres, resolution 64
+        struct Baxter : RobotOps<Baxter>
+        {
+            static constexpr auto name = "baxter";
+            static constexpr std::size_t dimension = 14;
+            static constexpr std::size_t resolution = 64;
+            static constexpr std::size_t n_spheres = 75;
+            using Configuration = std::array<float, dimension>;
+            static auto c_robot() noexcept -> vgpu_robot { return vgpu_robot{VGPU_ROBOT_BAXTER, 0, 0, 0, 0, 0, 0}; }
+        };
+
         // Two Pandas as one 14-dof robot (BASELINE configs[4]; no reference counterpart):
         // joints 0..6 = PandaBase<A>, 7..13 = PandaBase<B>; valid = fkcc_A && fkcc_B && no A-B
         // sphere overlap.  fkcc and validate_motions only (sphere_fk: use each arm's type).

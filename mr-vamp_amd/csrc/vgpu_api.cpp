@@ -20,6 +20,7 @@
 #include "../../include/vamp_gpu.h"
 #include "vgpu_capt.hh"
 #include "vgpu_device.hh"
+#include "vgpu_ops.hh"
 
 extern "C" {
 hipError_t vgpu_launch_panda_sample(uint64_t first, size_t n, float* q, hipStream_t st);
@@ -54,6 +55,9 @@ hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, s
                                              float bz, uint8_t* valid, hipStream_t st);
 VGPU_STAGED_DECL(panda)
 VGPU_STAGED_DECL(fetch)
+VGPU_STAGED_DECL(ur5)
+const RobotOps* vgpu_ur5_ops(void);
+const RobotOps* vgpu_baxter_ops(void);
 hipError_t vgpu_launch_fetch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
                                          int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
 hipError_t vgpu_launch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
@@ -721,8 +725,16 @@ static EnvView make_view(const vgpu_env* e)
 // ---------------------------------------------------------------------------------------
 // batch entry points
 // ---------------------------------------------------------------------------------------
+static const RobotOps* generic_ops(int32_t kind);
+
 extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t* ns)
 {
+    if (const RobotOps* g = generic_ops(kind)) {
+        if (dim) *dim = g->dim;
+        if (res) *res = g->resolution;
+        if (ns) *ns = g->n_spheres;
+        return VGPU_OK;
+    }
     if (kind == VGPU_ROBOT_PANDA_PAIR) {
         if (dim) *dim = kPairDim;
         if (res) *res = kPandaResolution;
@@ -756,9 +768,9 @@ static void pair_bases(const vgpu_robot* r, float pb[6])
 static int check_robot(vgpu_ctx* c, const vgpu_robot* r, float base[3])
 {
     if (!r) return fail(c, VGPU_ERR_INVALID_ARG, "null robot");
-    if (r->kind == VGPU_ROBOT_FETCH) {  // robots/fetch.hh: no base offset
+    if (r->kind == VGPU_ROBOT_FETCH || generic_ops(r->kind)) {  // fetch.hh, ur5.hh, baxter.hh: no base offset
         if (r->base_x100 || r->base_y100 || r->base_z100)
-            return fail(c, VGPU_ERR_INVALID_ARG, "Fetch has no base offset (robots/fetch.hh)");
+            return fail(c, VGPU_ERR_INVALID_ARG, "this robot has no base offset (base_*100 must be 0)");
         base[0] = base[1] = base[2] = 0.0f;
         return VGPU_OK;
     }
@@ -781,6 +793,10 @@ extern "C" int vgpu_sphere_fk(vgpu_ctx* c, const vgpu_robot* r, const float* q, 
     HIPCHK(c, hipSetDevice(c->device));
     if (r->kind == VGPU_ROBOT_FETCH) {
         HIPCHK(c, vgpu_launch_fetch_sphere_fk(q, n, xyz, ld, c->cur));
+        return VGPU_OK;
+    }
+    if (const RobotOps* g = generic_ops(r->kind)) {
+        HIPCHK(c, g->sphere_fk(q, n, xyz, ld, c->cur));
         return VGPU_OK;
     }
     if (r->kind == VGPU_ROBOT_PANDA_PAIR)
@@ -829,6 +845,18 @@ struct StagedOps {
     }
 static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda);
 static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch);
+static const StagedOps kUr5Staged = VGPU_STAGED_OPS(ur5);
+
+// robots built from vgpu_robot.hh (one TU each): their launch table, or NULL
+static const RobotOps* generic_ops(int32_t kind)
+{
+    switch (kind) {
+    case VGPU_ROBOT_UR5: return vgpu_ur5_ops();
+    case VGPU_ROBOT_BAXTER: return vgpu_baxter_ops();
+    default: return nullptr;
+    }
+}
+static const StagedOps* generic_staged(int32_t kind) { return kind == VGPU_ROBOT_UR5 ? &kUr5Staged : nullptr; }
 
 static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* s0, const void* s1, const void* s2,
                        const void* s3, uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid)
@@ -916,6 +944,12 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
+    if (const RobotOps* g = generic_ops(r->kind)) {
+        if (c->staged && g->staged)
+            return staged_pass(c, *generic_staged(r->kind), 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
+        HIPCHK(c, g->fkcc(q, n, &v, valid, c->cur));
+        return VGPU_OK;
+    }
     if (r->kind == VGPU_ROBOT_FETCH) {
         if (c->staged) return staged_pass(c, kFetchStaged, 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
         HIPCHK(c, vgpu_launch_fetch_fkcc(q, n, &v, valid, c->cur));
@@ -973,17 +1007,24 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
     const bool pair = r->kind == VGPU_ROBOT_PANDA_PAIR;  // monolithic head/tail kernels
     const bool fetch = r->kind == VGPU_ROBOT_FETCH && !c->staged;
-    const StagedOps& ops = r->kind == VGPU_ROBOT_FETCH ? kFetchStaged : kPandaStaged;
+    const RobotOps* g = generic_ops(r->kind);
+    const bool g_mono = g && !(c->staged && g->staged);
+    const StagedOps& ops = g ? (g->staged ? *generic_staged(r->kind) : kPandaStaged)
+                             : (r->kind == VGPU_ROBOT_FETCH ? kFetchStaged : kPandaStaged);
     float pb[6];
     pair_bases(r, pb);
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
-    if (pair) {
+    if (g_mono) {
+        HIPCHK(c, g->validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
+    } else if (pair) {
         HIPCHK(c, vgpu_launch_pair_validate_head(starts, goals, n_edges, &v, pb, ok, n_blocks, cnt, c->cur));
     } else if (fetch) {
         HIPCHK(c, vgpu_launch_fetch_validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
     } else if (c->staged) {
         if ((rc = staged_pass(c, ops, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
-        if (r->kind == VGPU_ROBOT_FETCH)
+        if (g)
+            HIPCHK(c, g->tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
+        else if (r->kind == VGPU_ROBOT_FETCH)
             HIPCHK(c, vgpu_launch_fetch_tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
         else
             HIPCHK(c, vgpu_launch_tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
@@ -1005,10 +1046,12 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
         c->items_cap = cap;
     }
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[2], c->cur));
-    if (fetch || pair) {
+    if (fetch || pair || g_mono) {
         if (n_items) {
             HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
-            if (pair)
+            if (g_mono)
+                HIPCHK(c, g->validate_tail(starts, goals, n_items, &v, ok, off, c->items, c->cur));
+            else if (pair)
                 HIPCHK(c, vgpu_launch_pair_validate_tail(starts, goals, n_items, &v, pb, ok, off, c->items, c->cur));
             else
                 HIPCHK(c, vgpu_launch_fetch_validate_tail(starts, goals, n_items, &v, ok, off, c->items, c->cur));
@@ -1076,7 +1119,9 @@ extern "C" int vgpu_sample_configurations(vgpu_ctx* c, const vgpu_robot* r, uint
     if (!q) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
     HIPCHK(c, hipSetDevice(c->device));
     if (r->kind == VGPU_ROBOT_PANDA_PAIR) return fail(c, VGPU_ERR_UNSUPPORTED, "no sampler for the composite");
-    if (r->kind == VGPU_ROBOT_FETCH)
+    if (const RobotOps* g = generic_ops(r->kind))
+        HIPCHK(c, g->sample(first, n, q, c->cur));
+    else if (r->kind == VGPU_ROBOT_FETCH)
         HIPCHK(c, vgpu_launch_fetch_sample(first, n, q, c->cur));
     else
         HIPCHK(c, vgpu_launch_panda_sample(first, n, q, c->cur));
@@ -1102,6 +1147,12 @@ extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, u
         vgpu_robot_info(r->kind, &dim, nullptr, nullptr);
         if ((rc = grow(c, &c->st_q, &c->st_q_cap, n * (size_t)dim))) return rc;
         q = (float*)c->st_q;
+    }
+    if (const RobotOps* g = generic_ops(r->kind)) {
+        if (c->staged && g->staged)
+            return staged_pass(c, *generic_staged(r->kind), 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
+        HIPCHK(c, g->sample_fkcc(first, n, &v, q, valid, c->cur));
+        return VGPU_OK;
     }
     if (r->kind == VGPU_ROBOT_FETCH) {
         if (c->staged) return staged_pass(c, kFetchStaged, 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
@@ -1164,12 +1215,16 @@ static size_t al(size_t b) { return (b + 255) & ~(size_t)255; }
 // configuration width and sphere count of a robot selection (host staging sizes)
 static size_t dim_of(const vgpu_robot* r)
 {
+    if (r)
+        if (const RobotOps* g = generic_ops(r->kind)) return (size_t)g->dim;
     if (r && r->kind == VGPU_ROBOT_FETCH) return kFetchDim;
     if (r && r->kind == VGPU_ROBOT_PANDA_PAIR) return kPairDim;
     return kPandaDim;
 }
 static size_t spheres_of(const vgpu_robot* r)
 {
+    if (r)
+        if (const RobotOps* g = generic_ops(r->kind)) return (size_t)g->n_spheres;
     return (r && r->kind == VGPU_ROBOT_FETCH) ? kFetchSpheres : kPandaSpheres;
 }
 

@@ -339,6 +339,14 @@ class Robot:
             [-2.9671, -1.8326, -2.9671, -3.1416, -2.9671, -0.0873, -2.9671],
             [0.1685147113342995, 0.2728364072901888, 0.1685147113342995, 0.30970299482796, 0.1685147113342995,
              0.25578064252097404, 0.1685147113342995]),
+        _lib.VGPU_ROBOT_UR5: (
+            [6.2831853, 6.2831853, 6.2831853, 6.2831853, 6.2831853, 6.2831853],
+            [-3.14159265, -3.14159265, -3.14159265, -3.14159265, -3.14159265, -3.14159265],
+            [0.15915494327375637, 0.15915494327375637, 0.15915494327375637, 0.15915494327375637, 0.15915494327375637, 0.15915494327375637]),
+        _lib.VGPU_ROBOT_BAXTER: (
+            [3.40335987756, 3.194, 6.10835987756, 2.6679999999999997, 6.118, 3.66479632679, 6.118, 3.40335987756, 3.194, 6.10835987756, 2.6679999999999997, 6.118, 3.66479632679, 6.118],
+            [-1.70167993878, -2.147, -3.05417993878, -0.05, -3.059, -1.57079632679, -3.059, -1.70167993878, -2.147, -3.05417993878, -0.05, -3.059, -1.57079632679, -3.059],
+            [0.2938272871445316, 0.31308703819661865, 0.16371006621166082, 0.37481259370314846, 0.16345210853220005, 0.2728664599148137, 0.16345210853220005, 0.2938272871445316, 0.31308703819661865, 0.16371006621166082, 0.37481259370314846, 0.16345210853220005, 0.2728664599148137, 0.16345210853220005]),
         _lib.VGPU_ROBOT_FETCH: (
             [0.38615, 3.2112, 2.739, 6.28318, 4.502, 6.28318, 4.32, 6.28318],
             [0.0, -1.6056, -1.221, -3.14159, -2.251, -3.14159, -2.16, -3.14159],
@@ -359,7 +367,8 @@ class Robot:
         self.S_M = np.array(sm, np.float32)
         self.S_A = np.array(sa, np.float32)
         self.D_M = np.array(dm, np.float32)
-        self.radii = {_lib.VGPU_ROBOT_PANDA: _PANDA_RADII, _lib.VGPU_ROBOT_FETCH: _FETCH_RADII}.get(
+        self.radii = {_lib.VGPU_ROBOT_PANDA: _PANDA_RADII, _lib.VGPU_ROBOT_FETCH: _FETCH_RADII,
+                      _lib.VGPU_ROBOT_UR5: _UR5_RADII, _lib.VGPU_ROBOT_BAXTER: _BAXTER_RADII}.get(
             kind, np.concatenate([_PANDA_RADII, _PANDA_RADII]))
 
     def _meta(self):
@@ -499,6 +508,11 @@ _FETCH_RADII = np.array(
 assert _FETCH_RADII.shape == (111,)
 
 
+# robots/ur5/fk.hh and robots/baxter/fk.hh sphere radii (reference order)
+_UR5_RADII = np.array([0.08, 0.08, 0.08, 0.08, 0.08, 0.08, 0.08, 0.08, 0.06, 0.06, 0.06, 0.06, 0.04, 0.04, 0.04, 0.04, 0.04, 0.04, 0.04, 0.04, 0.04, 0.04, 0.02, 0.015, 0.015, 0.015, 0.02, 0.02, 0.02, 0.02, 0.02, 0.02, 0.02, 0.015, 0.015, 0.015], np.float32)
+_BAXTER_RADII = np.array([0.25, 0.25, 0.23, 0.2, 0.1, 0.1, 0.1, 0.08, 0.08, 0.08, 0.1, 0.08, 0.08, 0.08, 0.07, 0.07, 0.07, 0.08, 0.05, 0.1, 0.1, 0.1, 0.08, 0.08, 0.08, 0.1, 0.08, 0.08, 0.08, 0.07, 0.07, 0.07, 0.08, 0.05, 0.5, 0.04, 0.04, 0.015, 0.015, 0.012, 0.012, 0.012, 0.014, 0.014, 0.014, 0.014, 0.015, 0.015, 0.012, 0.012, 0.012, 0.014, 0.014, 0.014, 0.014, 0.04, 0.04, 0.015, 0.015, 0.012, 0.012, 0.012, 0.014, 0.014, 0.014, 0.014, 0.015, 0.015, 0.012, 0.012, 0.012, 0.014, 0.014, 0.014, 0.014], np.float32)
+
+
 def PandaBase(base_x100: int, base_y100: int, base_z100: int, name: Optional[str] = None) -> Robot:
     """vamp::robots::PandaBase<X100, Y100, Z100> (robots/panda_base.hh:15)."""
     return Robot(name or f"panda_{base_x100}_{base_y100}_{base_z100}", base_x100, base_y100, base_z100)
@@ -526,3 +540,8 @@ def PandaPair(a100=(0, 0, 0), b100=(100, 0, 0), name: Optional[str] = None) -> R
 
 panda_pair = PandaPair((0, 0, 0), (100, 0, 0), "panda_pair")
 __all__ += ["PandaPair", "panda_pair"]
+
+# robots/ur5.hh (6 dof) and robots/baxter.hh (14-dof dual arm): no base offset
+ur5 = Robot("ur5", 0, 0, 0, kind=_lib.VGPU_ROBOT_UR5)
+baxter = Robot("baxter", 0, 0, 0, kind=_lib.VGPU_ROBOT_BAXTER)
+__all__ += ["ur5", "baxter"]

@@ -17,6 +17,8 @@ VGPU_OK = 0
 VGPU_ROBOT_PANDA = 1
 VGPU_ROBOT_FETCH = 2
 VGPU_ROBOT_PANDA_PAIR = 3
+VGPU_ROBOT_UR5 = 4
+VGPU_ROBOT_BAXTER = 5
 ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of memory", -4: "unsupported", -5: "host rsqrt probe"}
 
 F32P = C.POINTER(C.c_float)

@@ -564,7 +564,8 @@ def main():
         vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model[key])
         consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
     out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
-    out += "\n" + g.gen_staged()  # check masks: 32-bit up to 32 checks, 64-bit up to 64
+    if len(model["check_order"]) <= 64:  # check masks: 32-bit up to 32 checks, 64-bit up to 64
+        out += "\n" + g.gen_staged()
     if "--pair" in sys.argv:  # the composite's inter-robot check, as its own include
         out = g.gen_pair_inter()
     open(sys.argv[2], "w").write(out)
