@@ -28,5 +28,11 @@ typedef struct vo_model {
     const int *env_bound, *env_child_start, *env_child_sphere, *env_child_base, *env_leaf;
     const int *self_a_kind, *self_a_idx, *self_b_kind, *self_b_idx, *self_child_start;
     const int (*self_child)[2];
-    const int *order_kind, *order_idx;
+    const int *order_kind, *order_idx; /* kind 0 env, 1 self, 2 attachment vs link, 3 attachment vs env */
+    /* attachment variant (interleaved_sphere_fk_attachment) only: checks of the attached spheres
+     * against a link entity (kind 0 sphere / 1 bounding) with children [start, end), and the
+     * end-effector frame the attachment is posed at (-1: no attachment checks) */
+    int natt;
+    const int *att_ent_kind, *att_ent_idx, *att_child_start, *att_child_sphere, *att_leaf;
+    int ee_frame;
 } vo_model;

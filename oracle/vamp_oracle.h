@@ -136,6 +136,26 @@ void vo_robot_validate_motions(int robot, const vo_env *env, const float *starts
                                size_t n_edges, int bx100, int by100, int bz100, uint8_t *ok, int32_t *n_out,
                                int threads);
 
+/* Attachment<float> (collision/attachments.hh:14-123): spheres (x y z r) relative to a frame
+ * tf = (x y z, qx qy qz qw) attached to the end effector (bindings/environment.cc:197-249). */
+typedef struct vo_attachment {
+    float tf[7];
+    int n;
+    const float *spheres;
+} vo_attachment;
+/* Robot::fkcc_attach (panda: robots/panda/fk.hh:6278-11397); returns -1 for robots without an
+ * extracted attachment hierarchy */
+int vo_robot_fkcc_attach_block(int robot, const vo_env *env, const vo_attachment *att, const float *q, int G,
+                               int bx100, int by100, int bz100, vo_stats *stats);
+/* validate_motion with env.attachments set: first block fkcc_attach, back-steps fkcc (validate.hh:43) */
+int vo_robot_validate_motion_att(int robot, const vo_env *env, const vo_attachment *att, const float *start,
+                                 const float *goal, int bx100, int by100, int bz100, int *n_out, vo_stats *stats);
+void vo_robot_fkcc_attach_configs(int robot, const vo_env *env, const vo_attachment *att, const float *q, size_t n,
+                                  int bx100, int by100, int bz100, uint8_t *valid, int threads);
+void vo_robot_validate_motions_att(int robot, const vo_env *env, const vo_attachment *att, const float *starts,
+                                   const float *goals, size_t n_edges, int bx100, int by100, int bz100, uint8_t *ok,
+                                   int32_t *n_out, int threads);
+
 /* ---- Panda (robots/panda_base.hh, robots/panda/fk.hh): wrappers of the vo_robot_* calls ---- */
 void vo_panda_scale(float q[7]);                                               /* fk.hh:34-37 */
 void vo_panda_sphere_fk(const float q[7], int bx100, int by100, int bz100,

@@ -41,6 +41,10 @@ class VoEnv(C.Structure):
     ]
 
 
+class VoAttachment(C.Structure):
+    _fields_ = [("tf", C.c_float * 7), ("n", C.c_int), ("spheres", F32P)]
+
+
 class VoStats(C.Structure):
     _fields_ = [("test_margin", C.c_double), ("cull_margin", C.c_double), ("flops", C.c_double)]
 
@@ -128,6 +132,14 @@ def lib():
         L.vo_pair_fkcc_configs.argtypes = [C.POINTER(VoEnv), F32P, C.c_size_t, I3, I3, U8P, C.c_int]
         L.vo_pair_validate_motions.argtypes = [C.POINTER(VoEnv), F32P, F32P, C.c_size_t, I3, I3, U8P, I32P,
                                                C.c_int]
+        AP = C.POINTER(VoAttachment)
+        L.vo_robot_fkcc_attach_block.restype = C.c_int
+        L.vo_robot_fkcc_attach_block.argtypes = [C.c_int, C.POINTER(VoEnv), AP, F32P, C.c_int, C.c_int, C.c_int,
+                                                 C.c_int, C.POINTER(VoStats)]
+        L.vo_robot_fkcc_attach_configs.argtypes = [C.c_int, C.POINTER(VoEnv), AP, F32P, C.c_size_t, C.c_int,
+                                                   C.c_int, C.c_int, U8P, C.c_int]
+        L.vo_robot_validate_motions_att.argtypes = [C.c_int, C.POINTER(VoEnv), AP, F32P, F32P, C.c_size_t,
+                                                    C.c_int, C.c_int, C.c_int, U8P, I32P, C.c_int]
         L.vo_l2_norm.restype = C.c_float
         L.vo_l2_norm.argtypes = [F32P, C.c_int]
         _lib = L
@@ -501,3 +513,58 @@ def pair_validate_flops(env: Env, starts, goals, ba=(0, 0, 0), bb=(100, 0, 0)):
                                       C.byref(st))
         out[i] = st.flops
     return out
+
+
+# ---- attachments (collision/attachments.hh; Robot::fkcc_attach) ----
+class Attachment:
+    """Attachment(center, quaternion_xyzw) + add_sphere (bindings/environment.cc:197-249)."""
+
+    def __init__(self, center, quaternion_xyzw):
+        self.tf = np.array(list(center) + list(quaternion_xyzw), np.float32)
+        self.spheres = []
+
+    def add_sphere(self, center, r):
+        self.spheres.append([float(np.float32(v)) for v in center] + [float(np.float32(r))])
+        return self
+
+    def c(self):
+        self._keep = np.ascontiguousarray(np.array(self.spheres, np.float32).reshape(-1, 4))
+        a = VoAttachment()
+        for i in range(7):
+            a.tf[i] = float(self.tf[i])
+        a.n = len(self.spheres)
+        a.spheres = fp(self._keep)
+        return a
+
+    def as_dict(self):
+        return {"tf": self.tf.copy(), "spheres": np.array(self.spheres, np.float32).reshape(-1, 4)}
+
+
+def held_object():
+    """A bar held 10-25 cm along the hand's z axis (four spheres, r 3 cm), turned 45 degrees."""
+    a = Attachment((0.0, 0.0, 0.1), (0.0, 0.0, 0.38268343, 0.92387953))
+    for z in (0.0, 0.05, 0.1, 0.15):
+        a.add_sphere((0.03, 0.0, z), 0.03)
+    return a
+
+
+def robot_fkcc_attach_threads(robot, env: Env, att: Attachment, q, base100=(0, 0, 0), threads=8):
+    rid, dim, _ = ROBOTS[robot]
+    q = np.ascontiguousarray(q, np.float32).reshape(-1, dim)
+    out = np.zeros(q.shape[0], np.uint8)
+    ce, ca = env.c(), att.c()
+    lib().vo_robot_fkcc_attach_configs(rid, C.byref(ce), C.byref(ca), fp(q), q.shape[0], *base100,
+                                       out.ctypes.data_as(U8P), threads)
+    return out.astype(bool)
+
+
+def robot_validate_motions_att(robot, env: Env, att: Attachment, starts, goals, base100=(0, 0, 0), threads=8):
+    rid, dim, _ = ROBOTS[robot]
+    s = np.ascontiguousarray(starts, np.float32).reshape(-1, dim)
+    g = np.ascontiguousarray(goals, np.float32).reshape(-1, dim)
+    ok = np.zeros(s.shape[0], np.uint8)
+    n = np.zeros(s.shape[0], np.int32)
+    ce, ca = env.c(), att.c()
+    lib().vo_robot_validate_motions_att(rid, C.byref(ce), C.byref(ca), fp(s), fp(g), s.shape[0], *base100,
+                                        ok.ctypes.data_as(U8P), n.ctypes.data_as(I32P), threads)
+    return ok.astype(bool), n

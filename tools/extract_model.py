@@ -56,8 +56,13 @@ def parse_const_array(src, name):
     return [float(v.strip().rstrip("f")) for v in m.group(1).split(",")]
 
 
-def extract_robot(ref, robot):
+def extract_robot(ref, robot, variant=""):
+    """variant "" = interleaved_sphere_fk (Robot::fkcc); "attach" = interleaved_sphere_fk_attachment
+    (Robot::fkcc_attach, planning/validate.hh:43): its own bounding spheres, plus checks of the
+    attached spheres against links ("att") and against the environment ("attenv"), posed at the
+    end-effector frame recorded as ee_frame."""
     cfg = ROBOTS[robot]
+    fn = "interleaved_sphere_fk_attachment" if variant == "attach" else "interleaved_sphere_fk"
     urdf = f"{ref}/{cfg['urdf']}"
     fkhh = f"{ref}/{cfg['fk']}"
     src = open(fkhh).read()
@@ -65,8 +70,8 @@ def extract_robot(ref, robot):
     frames = rm.build_frames(links, joints, cfg["root"])
     fname = [f["name"] for f in frames]
     fk = fi.parse_function(src, r"inline void sphere_fk\(")
-    cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
-    cc_text = fi.function_body(src, r"inline bool interleaved_sphere_fk\(")
+    cc = fi.parse_function(src, rf"inline bool {fn}\(")
+    cc_text = fi.function_body(src, rf"inline bool {fn}\(")
     # top-level checks in text order: the generator's link label, or None for an unlabeled
     # single-sphere link tested directly (a leaf: its hit is a collision, no children)
     labels = [m.group(2) for m in re.finditer(r"^        if \((/\*(.*?)\*/)?", cc_text, re.M)]
@@ -167,17 +172,45 @@ def extract_robot(ref, robot):
                 return dict(bound=link)
         raise RuntimeError("unmatched self-collision entity")
 
+    def entity_or_new(pts, r, link):
+        try:
+            return entity(pts, r)
+        except RuntimeError:  # a link-bounding sphere that no environment check uses
+            fidx = fname.index(link)
+            loc, spread = local_in(fidx, pts)
+            assert spread < 2e-6, (link, spread)
+            key = f"{link}#att"
+            bounding[key] = dict(link=key, frame=fidx, offset=[float(round(v, 6)) for v in loc[0]], radius=r,
+                                 base=False)
+            return dict(bound=key)
+
+    att_checks = []
     order = []
     for t, lab in zip(top, labels):
         c = calls0[t]
+        if c["kind"] == "attenv":  # attached spheres vs the environment (validity.hh:251-266)
+            order.append(dict(kind="attenv", index=0))
+            continue
+        if c["kind"] == "att":  # "attachment vs. <link>" (validity.hh:269-293)
+            link = lab.split("vs.")[1].strip()
+            e = entity_or_new(np.stack(c["args"][:3]).T, float(c["args"][3][0]), link)
+            kids = [i for i, cc_ in enumerate(calls0) if cc_["parent"] == t]
+            ch = [sphere_at(np.stack(calls0[i]["args"][:3]).T, float(calls0[i]["args"][3][0])) for i in kids]
+            assert all(x is not None for x in ch)
+            ck = dict(link=link, ent=e, children=ch)
+            if not kids:
+                ck["leaf"] = True
+            att_checks.append(ck)
+            order.append(dict(kind="att", index=len(att_checks) - 1))
+            continue
         if c["kind"] == "env":
             lk = lab.strip() if lab is not None else spheres[sphere_at(np.stack(c["args"][:3]).T, float(c["args"][3][0]))]["link"]
             order.append(dict(kind="env", index=[e["link"] for e in env_checks].index(lk)))
             continue
         a_link, b_link = [s.strip() for s in lab.split("vs.")]
         pa, pb = np.stack(c["args"][:3]).T, np.stack(c["args"][4:7]).T
-        ea = entity(pa, float(c["args"][3][0]))
-        eb = entity(pb, float(c["args"][7][0]))
+        ea = entity_or_new(pa, float(c["args"][3][0]), a_link)
+        eb = entity_or_new(pb, float(c["args"][7][0]), b_link)
         kids = [i for i, cc_ in enumerate(calls0) if cc_["parent"] == t]
         pairs = []
         for i in kids:
@@ -214,18 +247,49 @@ def extract_robot(ref, robot):
         self_checks=self_checks,
         check_order=order,
     )
+    if variant == "attach":
+        model["robot"] = f"{robot}_attach"
+        model["att_checks"] = att_checks
+        model["ee_frame"] = ee_frame_of(cc, frames, Q, poses, fi)
     return model
+
+
+def ee_frame_of(cc, frames, Q, poses, fi):
+    """The frame whose pose set_attachment_pose receives: position = its origin, orientation =
+    its quaternion (x, y, z, w), checked over the sample configurations."""
+    ev = fi.Evaluator(Q, (0, 0, 0), "exact64")
+    ev.bind_base()
+    vals = None
+    for st in cc:
+        if st[0] in ("decl", "fdecl"):
+            ev.env[st[1]] = ev.ev(st[2])
+        elif st[0] == "setpose":
+            vals = np.array([ev.arg(a) for a in st[1]])
+            break
+    for fidx in range(len(frames)):
+        ok = True
+        for k in range(Q.shape[0]):
+            qf, pf = poses[k][0][fidx], poses[k][1][fidx]
+            w, x, y, z = qf
+            if np.abs(vals[:3, k] - pf).max() > 2e-6 or np.abs(vals[3:, k] - np.array([x, y, z, w])).max() > 2e-6:
+                ok = False
+                break
+        if ok:
+            return fidx
+    raise RuntimeError("end-effector frame not found")
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
     ap.add_argument("--robot", default="panda", choices=sorted(ROBOTS))
+    ap.add_argument("--variant", default="", choices=["", "attach"])
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     if a.out is None:
-        a.out = os.path.join(os.path.dirname(__file__), "..", "model", f"{a.robot}.json")
-    m = extract_robot(a.ref, a.robot)
+        suffix = "_attach" if a.variant else ""
+        a.out = os.path.join(os.path.dirname(__file__), "..", "model", f"{a.robot}{suffix}.json")
+    m = extract_robot(a.ref, a.robot, a.variant)
     with open(a.out, "w") as f:
         json.dump(m, f, indent=1)
     print(f"wrote {a.out}: {len(m['spheres'])} spheres, {len(m['env_checks'])} env checks "

@@ -153,6 +153,17 @@ class Parser:
             body = self.stmts()
             self.take("}")
             return ("if", call, body)
+        if v == "set_attachment_pose":  # set_attachment_pose(environment, tx, ty, tz, rx, ry, rz, rw);
+            self.take()
+            self.take("(")
+            self.take("environment")
+            args = []
+            while self.peek()[1] == ",":
+                self.take()
+                args.append(self.expr())
+            self.take(")")
+            self.take(";")
+            return ("setpose", args)
         if v == "return":
             self.take()
             b = self.take()[1]
@@ -164,6 +175,11 @@ class Parser:
 
     def call(self):
         fn = self.take()[1]
+        if fn == "attachment_environment_collision":  # (environment)
+            self.take("(")
+            self.take("environment")
+            self.take(")")
+            return ("attenv", [])
         if fn.startswith("sphere_sphere_self_collision") or fn.startswith("attachment_sphere_collision"):
             # template args: <decltype(q[0])>
             self.take("<")
@@ -578,8 +594,47 @@ def run_sphere_fk(ast, q, base100, mode="ref32"):
     return xyz, r
 
 
-def run_fkcc(ast, q, base100, env: EnvNP, rs: RsqrtHost, G=1):
-    """Evaluate interleaved_sphere_fk over N lanes grouped by G. Returns (valid[N], stats)."""
+def pose_attachment(att, p):
+    """Attachment::pose (collision/attachments.hh:75-122) in float32, left to right: the
+    end-effector pose p = (tx, ty, tz, rx, ry, rz, rw) (lane vectors) composed with the
+    attachment's relative frame att["tf"] = (tx, ty, tz, rx, ry, rz, rw), then every relative
+    sphere centre att["spheres"][k] = (x, y, z, r) rotated and translated.  Returns (x, y, z)
+    arrays of shape (K, N) and the radii (K,)."""
+    f = F32
+    p_tx, p_ty, p_tz, p_rx, p_ry, p_rz, p_rw = (np.asarray(a, f) for a in p)
+    t_tx, t_ty, t_tz, t_rx, t_ry, t_rz, t_rw = (f(v) for v in att["tf"])
+    two, one = f(2.0), f(1.0)
+    rx = p_rw * t_rx + p_rx * t_rw + p_ry * t_rz - p_rz * t_ry
+    ry = p_rw * t_ry - p_rx * t_rz + p_ry * t_rw + p_rz * t_rx
+    rz = p_rw * t_rz + p_rx * t_ry - p_ry * t_rx + p_rz * t_rw
+    rw = p_rw * t_rw - p_rx * t_rx - p_ry * t_ry - p_rz * t_rz
+    x0 = p_ry * t_tz - p_rz * t_ty
+    x1 = p_rx * t_ty - p_ry * t_tx
+    x2 = p_rx * t_tz - p_rz * t_tx
+    tx = p_tx + two * (p_rw * x0 + p_ry * x1 + p_rz * x2) + t_tx
+    ty = p_ty + two * (-p_rw * x2 - p_rx * x1 + p_rz * x0) + t_ty
+    tz = p_tz + two * (p_rw * x1 - p_rx * x2 - p_ry * x0) + t_tz
+    bx0, bx1, bx2, bx3 = ry * ry, rz * rz, rw * rz, rw * ry
+    bx4, bx5, bx6, bx7, bx8 = rx * rx, rw * rx, rx * ry, rx * rz, ry * rz
+    b_xx = -two * (bx0 + bx1) + one
+    b_xy = two * (bx6 + bx2)
+    b_xz = two * (bx7 - bx3)
+    b_yx = two * (bx6 - bx2)
+    b_yy = -two * (bx1 + bx4) + one
+    b_yz = two * (bx8 + bx5)
+    b_zx = two * (bx7 + bx3)
+    b_zy = two * (bx8 - bx5)
+    b_zz = -two * (bx0 + bx4) + one
+    sp = np.asarray(att["spheres"], f).reshape(-1, 4)
+    X = np.stack([sx * b_xx + sy * b_yx + sz * b_zx + tx for sx, sy, sz, _ in sp]).astype(f)
+    Y = np.stack([sx * b_xy + sy * b_yy + sz * b_zy + ty for sx, sy, sz, _ in sp]).astype(f)
+    Z = np.stack([sx * b_xz + sy * b_yz + sz * b_zz + tz for sx, sy, sz, _ in sp]).astype(f)
+    return X, Y, Z, sp[:, 3].copy()
+
+
+def run_fkcc(ast, q, base100, env: EnvNP, rs: RsqrtHost, G=1, att=None):
+    """Evaluate interleaved_sphere_fk (or interleaved_sphere_fk_attachment, with `att` =
+    {"tf": 7 floats, "spheres": K x 4}) over N lanes grouped by G. Returns (valid[N], stats)."""
     q = np.asarray(q, F32)
     N = q.shape[0]
     assert N % G == 0
@@ -587,6 +642,7 @@ def run_fkcc(ast, q, base100, env: EnvNP, rs: RsqrtHost, G=1):
     ev.bind_base()
     stats = CheckStats(N)
     alive = np.ones(N, bool)
+    posed = {}
 
     def run(stmts, active):
         nonlocal alive
@@ -594,6 +650,8 @@ def run_fkcc(ast, q, base100, env: EnvNP, rs: RsqrtHost, G=1):
             k = st[0]
             if k in ("decl", "fdecl"):
                 ev.env[st[1]] = ev.ev(st[2])
+            elif k == "setpose":
+                posed["s"] = pose_attachment(att, [ev.arg(a) for a in st[1]])
             elif k == "if":
                 call = st[1]
                 act = active & alive
@@ -603,8 +661,20 @@ def run_fkcc(ast, q, base100, env: EnvNP, rs: RsqrtHost, G=1):
                 elif call[0] == "self":
                     a = [ev.arg(x) for x in call[1]]
                     c = self_collision(*a, G, act, stats)
+                elif call[0] == "att":  # attachment_sphere_collision (validity.hh:269-293)
+                    a = [ev.arg(x) for x in call[1]]
+                    X, Y, Z, R = posed["s"]
+                    c = np.zeros(N, bool)
+                    for kk in range(len(R)):
+                        c |= self_collision(a[0], a[1], a[2], F32(a[3][0]), X[kk], Y[kk], Z[kk], F32(R[kk]), G, act,
+                                            stats)
+                elif call[0] == "attenv":  # attachment_environment_collision (validity.hh:251-266)
+                    X, Y, Z, R = posed["s"]
+                    c = np.zeros(N, bool)
+                    for kk in range(len(R)):
+                        c |= env_in_collision(env, rs, X[kk], Y[kk], Z[kk], F32(R[kk]), G, act & ~c, stats)
                 else:
-                    raise NotImplementedError("attachment checks")
+                    raise NotImplementedError(call[0])
                 run(st[2], act & c)
             elif k == "ret":
                 if not st[1]:

@@ -123,8 +123,9 @@ def sphere_cage():
     return e, fi.EnvNP(spheres=e.arrays()["spheres"])
 
 
-def interp_validate(cc, starts, goals, base, envnp, rs, res=32):
-    """validate_motion (planning/validate.hh:23-75) over E edges, 8-lane groups."""
+def interp_validate(cc, starts, goals, base, envnp, rs, res=32, cc_first=None, att=None):
+    """validate_motion (planning/validate.hh:23-75) over E edges, 8-lane groups; with cc_first /
+    att the first block goes through interleaved_sphere_fk_attachment (validate.hh:43)."""
     E, D = starts.shape
     v = (goals - starts).astype(F)
     if D <= 8:
@@ -152,7 +153,10 @@ def interp_validate(cc, starts, goals, base, envnp, rs, res=32):
         if len(idx) == 0:
             break
         q = block[idx].reshape(-1, D)
-        valid, st = fi.run_fkcc(cc, q, base, envnp, rs, G=8)
+        if k == 0 and cc_first is not None:
+            valid, st = fi.run_fkcc(cc_first, q, base, envnp, rs, G=8, att=att)
+        else:
+            valid, st = fi.run_fkcc(cc, q, base, envnp, rs, G=8)
         valid = valid.reshape(-1, 8)[:, 0]
         tmarg[idx] = np.minimum(tmarg[idx], st.test_margin.reshape(-1, 8).min(1))
         cmarg[idx] = np.minimum(cmarg[idx], st.cull_margin.reshape(-1, 8).min(1))
@@ -223,6 +227,40 @@ def make_robot(rng, robot, scene, out_name, n_cfg=16384, n_empty=4096, n_edges=1
 
 def make_fetch(rng):
     make_robot(rng, "fetch", "table_pick_fetch/scene0001.yaml", "fetch_table_pick.npz")
+
+
+def make_attach(rng):
+    """Panda with a held object (tests/oracle_py.py:held_object) on the sphere cage, bases (0,0,0)
+    and (200,200,0): per-configuration fkcc_attach masks (interleaved_sphere_fk_attachment) and
+    edges whose first block goes through it (validate.hh:43)."""
+    src = open("/root/reference/src/impl/vamp/robots/panda/fk.hh").read()
+    cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
+    ca = fi.parse_function(src, r"inline bool interleaved_sphere_fk_attachment\(")
+    lut, kb = op.rsqrt_probe()
+    rs = fi.RsqrtHost(lut, kb)
+    env, envnp = sphere_cage()
+    att = op.held_object()
+    ad = att.as_dict()
+    out = {}
+    for tag, base in (("b000", (0, 0, 0)), ("b220", (200, 200, 0))):
+        q = op.scale(rng.random((8192, 7), dtype=F))
+        valid, st = fi.run_fkcc(ca, q, base, envnp, rs, G=1, att=ad)
+        plain, _ = fi.run_fkcc(cc, q, base, envnp, rs, G=1)
+        out.update({f"q_{tag}": q, f"valid_{tag}": valid, f"plain_{tag}": plain,
+                    f"test_margin_{tag}": st.test_margin.astype(F), f"cull_margin_{tag}": st.cull_margin.astype(F)})
+    E = 1024
+    pool = op.scale(rng.random((20000, 7), dtype=F))
+    pv = op.fkcc_threads(env, pool, (0, 0, 0))
+    vq = pool[pv]
+    s, g = vq[0:2 * E:2][:E], vq[1:2 * E:2][:E]
+    d = np.linalg.norm((g - s).astype(np.float64), axis=1)
+    g = (s + (g - s) * np.minimum(1.0, 1.0 / np.maximum(d, 1e-9)).astype(F)[:, None]).astype(F)
+    ok, n, tm, cm = interp_validate(cc, s, g, (0, 0, 0), envnp, rs, 32, cc_first=ca, att=ad)
+    np.savez_compressed(os.path.join(GOLD, "attach_panda_cage.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
+                        att_tf=ad["tf"], att_spheres=ad["spheres"], starts=s, goals=g, ok=ok, n=n.astype(np.int32),
+                        edge_test_margin=tm.astype(F), edge_cull_margin=cm.astype(F), **out)
+    print("attach_panda_cage.npz", out["valid_b000"].mean(), out["plain_b000"].mean(), out["valid_b220"].mean(),
+          ok.mean())
 
 
 def make_l2_pins(rng):
@@ -342,6 +380,9 @@ def main():
         return
     if "--fetch" in sys.argv:
         make_fetch(np.random.default_rng(20261016))
+        return
+    if "--attach" in sys.argv:
+        make_attach(np.random.default_rng(20261021))
         return
     if "--ur5" in sys.argv:
         make_robot(np.random.default_rng(20261019), "ur5", "table_pick_ur5/scene0001.yaml", "ur5_table_pick.npz")
