@@ -118,6 +118,15 @@ int vgpu_env_pointcloud_info(const vgpu_env *env, int index, int32_t *nlog2, siz
  * aff[n_aff][3][8] (any pointer may be NULL) */
 int vgpu_env_pointcloud_arrays(const vgpu_env *env, int index, float *tests, float *aabbs, uint32_t *aff_starts,
                                float *aff);
+/* Environment::attach(Attachment) (bindings/environment.cc:161-162): one attachment, replacing
+ * any previous one.  tf = relative frame x y z, quaternion x y z w (Attachment(center,
+ * quaternion_xyzw), environment.cc:197-215); spheres[n][4] = x y z r relative to it
+ * (Attachment::add_spheres, :226-233).  validate_motions then checks the first rake block
+ * through Robot::fkcc_attach (planning/validate.hh:43).  Panda only (VGPU_ERR_UNSUPPORTED at
+ * validation time for other robots). */
+int vgpu_env_attach(vgpu_env *env, const float tf[7], const float *spheres, size_t n);
+/* Environment::detach (environment.cc:163) */
+int vgpu_env_detach(vgpu_env *env);
 /* Copy the (sorted) environment to the device.  Called implicitly by the batch functions
  * when the environment changed since the last upload. */
 int vgpu_env_upload(vgpu_env *env);
@@ -129,6 +138,11 @@ int vgpu_sphere_fk(vgpu_ctx *ctx, const vgpu_robot *robot, const float *q, size_
 /* Robot::fkcc<rake> of each configuration broadcast to the whole rake (the per-configuration
  * mask, as used by validate(q) and the PRM sampler): valid[i] = 1 if q[i] is collision-free. */
 int vgpu_fkcc(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n, uint8_t *valid);
+/* Robot::fkcc_attach<rake> (robots/panda_base.hh:61-65, panda/fk.hh:6278-11397) of each
+ * configuration broadcast to the rake, with the environment's attachment posed at the end
+ * effector; requires an attachment (vgpu_env_attach).  Panda only. */
+int vgpu_fkcc_attach(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n,
+                     uint8_t *valid);
 /* validate_motion<Robot, 8, Robot::resolution>(starts[i], goals[i], env) for every edge:
  * ok[i] = 1 if the whole edge is valid.  n_blocks (optional) receives n_e, the rake
  * back-step count of validate.hh:41 (interpolants = 8 * n_e). */
@@ -159,6 +173,8 @@ int vgpu_compact(vgpu_ctx *ctx, const float *rows, const uint8_t *valid, size_t 
 int vgpu_sphere_fk_host(vgpu_ctx *ctx, const vgpu_robot *robot, const float *q, size_t n, float *xyz);
 int vgpu_fkcc_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n,
                    uint8_t *valid);
+int vgpu_fkcc_attach_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n,
+                          uint8_t *valid);
 int vgpu_validate_motions_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *starts,
                                const float *goals, size_t n_edges, uint8_t *ok, int32_t *n_blocks);
 

@@ -90,6 +90,11 @@ hipError_t vgpu_launch_pair_validate_tail(const float* starts, const float* goal
 size_t vgpu_validate_scan_bytes(size_t n_edges);
 hipError_t vgpu_launch_scan(const uint32_t* cnt, uint32_t* off, size_t n_edges, void* scan_tmp, size_t scan_bytes,
                             hipStream_t st);
+hipError_t vgpu_launch_panda_fkcc_attach(const float* q, size_t n, const EnvView* env, float bx, float by, float bz,
+                                         uint8_t* valid, hipStream_t st);
+hipError_t vgpu_launch_panda_validate_head_att(const float* starts, const float* goals, size_t n_edges,
+                                               const EnvView* env, float bx, float by, float bz, uint8_t* ok,
+                                               int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
 hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goals, size_t n_edges,
                                            const EnvView* env, float bx, float by, float bz, uint8_t* ok,
                                            int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
@@ -225,7 +230,10 @@ struct vgpu_env {
     std::vector<std::array<float, 16>> cuboids, zcuboids;
     std::vector<vgpu::Heightfield> heightfields;
     std::vector<vgpu::CaptTree> pointclouds;
-    size_t hf_off = 0, pc_off = 0;
+    bool attached = false;  // Environment::attachments (environment.hh:21)
+    std::array<float, 7> att_tf{};
+    std::vector<std::array<float, 4>> att_spheres;
+    size_t hf_off = 0, pc_off = 0, att_off = 0;
     bool dirty = true;
     float* dev = nullptr;
     size_t dev_floats = 0;
@@ -612,6 +620,30 @@ static void sort_md(std::vector<std::array<float, W>>& v)  // environment.hh:40-
 
 // Device layout of EnvView (vgpu_device.hh): per type, records sorted by min_distance
 // (environment.hh:40-66) followed by kObsPad sentinels with min_distance = +inf.
+extern "C" int vgpu_env_attach(vgpu_env* e, const float tf[7], const float* spheres, size_t n)
+{
+    if (!e || !tf || (n && !spheres)) return VGPU_ERR_INVALID_ARG;
+    if (n > ((size_t)1 << 20)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "too many attached spheres");
+    for (int i = 0; i < 7; ++i)
+        if (!std::isfinite(tf[i])) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "non-finite attachment frame");
+    std::copy(tf, tf + 7, e->att_tf.begin());
+    e->att_spheres.assign(n, {});
+    for (size_t k = 0; k < n; ++k)
+        for (int i = 0; i < 4; ++i) e->att_spheres[k][i] = spheres[4 * k + i];
+    e->attached = true;
+    e->dirty = true;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_detach(vgpu_env* e)
+{
+    if (!e) return VGPU_ERR_INVALID_ARG;
+    e->attached = false;
+    e->att_spheres.clear();
+    e->dirty = true;
+    return VGPU_OK;
+}
+
 extern "C" int vgpu_env_upload(vgpu_env* e)
 {
     if (!e) return VGPU_ERR_INVALID_ARG;
@@ -688,6 +720,12 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
         hd[PC_STARTS] = hdr_u((uint32_t)o_starts);
         hd[PC_AFF] = hdr_u((uint32_t)o_aff);
     }
+    // the attachment: frame (7 floats + pad), then its spheres (16-B aligned)
+    align16();
+    e->att_off = blob.size();
+    blob.resize(blob.size() + kAttHdr, 0.0f);
+    std::copy(e->att_tf.begin(), e->att_tf.end(), blob.begin() + e->att_off);
+    for (const auto& sp : e->att_spheres) blob.insert(blob.end(), sp.begin(), sp.end());
     if (blob.size() >= ((size_t)1 << 32)) return fail(c, VGPU_ERR_INVALID_ARG, "environment larger than 16 GiB");
     HIPCHK(c, hipSetDevice(c->device));
     if (blob.size() > e->dev_floats) {
@@ -719,6 +757,8 @@ static EnvView make_view(const vgpu_env* e)
     v.base = e->dev;
     v.n_hf = (int)e->heightfields.size();
     v.n_pc = (int)e->pointclouds.size();
+    v.att = (const VGPU_CONST float*)(e->dev + e->att_off);
+    v.n_att = e->attached ? (int)e->att_spheres.size() : 0;
     return v;
 }
 
@@ -966,6 +1006,23 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     return VGPU_OK;
 }
 
+extern "C" int vgpu_fkcc_attach(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n,
+                                uint8_t* valid)
+{
+    if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
+    float b[3];
+    int rc = check_robot(c, r, b);
+    if (rc) return rc;
+    if (r->kind != VGPU_ROBOT_PANDA) return fail(c, VGPU_ERR_UNSUPPORTED, "fkcc_attach: Panda only");
+    if (!e->attached) return fail(c, VGPU_ERR_INVALID_ARG, "fkcc_attach: the environment has no attachment");
+    if (n && (!q || !valid)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if ((rc = vgpu_env_upload(e))) return rc;
+    const EnvView v = make_view(e);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_panda_fkcc_attach(q, n, &v, b[0], b[1], b[2], valid, c->cur));
+    return VGPU_OK;
+}
+
 static int ensure_ws(vgpu_ctx* c, size_t n_edges, uint32_t** cnt, uint32_t** off, void** tmp, size_t* tmp_bytes)
 {
     const size_t idx_bytes = ((n_edges + 1) * sizeof(uint32_t) + 255) & ~(size_t)255;
@@ -998,6 +1055,10 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     if (n_edges == 0) return VGPU_OK;
     if (!starts || !goals || !ok) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
     if (n_edges >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many edges in one call (< 2^31)");
+    // validate.hh:43: with an attachment the first block goes through fkcc_attach
+    const bool att = e->attached;
+    if (att && r->kind != VGPU_ROBOT_PANDA)
+        return fail(c, VGPU_ERR_UNSUPPORTED, "attachments: fkcc_attach is built for the Panda only");
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
@@ -1014,7 +1075,10 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     float pb[6];
     pair_bases(r, pb);
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
-    if (g_mono) {
+    if (att) {
+        HIPCHK(c, vgpu_launch_panda_validate_head_att(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, cnt,
+                                                      c->cur));
+    } else if (g_mono) {
         HIPCHK(c, g->validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
     } else if (pair) {
         HIPCHK(c, vgpu_launch_pair_validate_head(starts, goals, n_edges, &v, pb, ok, n_blocks, cnt, c->cur));
@@ -1256,6 +1320,23 @@ extern "C" int vgpu_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, con
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipMemcpyAsync(d, q, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     if ((rc = vgpu_fkcc(c, r, e, (const float*)d, n, (uint8_t*)(d + qb)))) return rc;
+    HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_fkcc_attach_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n,
+                                     uint8_t* valid)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (n == 0) return VGPU_OK;
+    char* d;
+    const size_t qb = al(n * dim_of(r) * 4);
+    int rc = stage(c, qb + n, &d);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(d, q, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
+    if ((rc = vgpu_fkcc_attach(c, r, e, (const float*)d, n, (uint8_t*)(d + qb)))) return rc;
     HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;

@@ -169,7 +169,12 @@ struct EnvView {
     const VGPU_CONST float* pc;
     const float* base;
     int n_hf, n_pc;
+    // the environment's attachment (Environment::attachments, environment.hh:21): frame tf =
+    // x y z qx qy qz qw (+1 pad), then n_att spheres x y z r relative to it (kAttHdr floats in)
+    const VGPU_CONST float* att;
+    int n_att;
 };
+constexpr int kAttHdr = 8;
 constexpr int kExtHdr = 16;
 // heightfield header: x y z xs ys zs xd yd xd2 yd2 (floats) | data_off cells (uint32 bits)
 enum : int { HF_X = 0, HF_Y, HF_Z, HF_XS, HF_YS, HF_ZS, HF_XD, HF_YD, HF_XD2, HF_YD2, HF_OFF, HF_CELLS };
@@ -415,6 +420,52 @@ template <class Grp, bool EXT = false>
 __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, float z, float r)
 {
     return (env_bits<Grp, EXT>(env, x, y, z, r) >> 31) != 0u;
+}
+
+// Attachment::pose (collision/attachments.hh:75-122) at the end-effector pose p (position,
+// quaternion x y z w): the composed rotation's basis and translation, float32 left to right
+// exactly as the oracle's pose_attachment (oracle/vamp_oracle.c).
+struct AttPose {
+    float xx, xy, xz, yx, yy, yz, zx, zy, zz, tx, ty, tz;
+};
+__device__ __forceinline__ AttPose att_pose(const EnvView& env, float p_tx, float p_ty, float p_tz, float p_rx,
+                                            float p_ry, float p_rz, float p_rw)
+{
+    const VGPU_CONST float* tf = env.att;
+    const float t_tx = tf[0], t_ty = tf[1], t_tz = tf[2], t_rx = tf[3], t_ry = tf[4], t_rz = tf[5], t_rw = tf[6];
+    const float rx = p_rw * t_rx + p_rx * t_rw + p_ry * t_rz - p_rz * t_ry;
+    const float ry = p_rw * t_ry - p_rx * t_rz + p_ry * t_rw + p_rz * t_rx;
+    const float rz = p_rw * t_rz + p_rx * t_ry - p_ry * t_rx + p_rz * t_rw;
+    const float rw = p_rw * t_rw - p_rx * t_rx - p_ry * t_ry - p_rz * t_rz;
+    const float x0 = p_ry * t_tz - p_rz * t_ty;
+    const float x1 = p_rx * t_ty - p_ry * t_tx;
+    const float x2 = p_rx * t_tz - p_rz * t_tx;
+    AttPose a;
+    a.tx = p_tx + 2.0f * (p_rw * x0 + p_ry * x1 + p_rz * x2) + t_tx;
+    a.ty = p_ty + 2.0f * (-p_rw * x2 - p_rx * x1 + p_rz * x0) + t_ty;
+    a.tz = p_tz + 2.0f * (p_rw * x1 - p_rx * x2 - p_ry * x0) + t_tz;
+    const float bx0 = ry * ry, bx1 = rz * rz, bx2 = rw * rz, bx3 = rw * ry, bx4 = rx * rx;
+    const float bx5 = rw * rx, bx6 = rx * ry, bx7 = rx * rz, bx8 = ry * rz;
+    a.xx = -2.0f * (bx0 + bx1) + 1.0f;
+    a.xy = 2.0f * (bx6 + bx2);
+    a.xz = 2.0f * (bx7 - bx3);
+    a.yx = 2.0f * (bx6 - bx2);
+    a.yy = -2.0f * (bx1 + bx4) + 1.0f;
+    a.yz = 2.0f * (bx8 + bx5);
+    a.zx = 2.0f * (bx7 + bx3);
+    a.zy = 2.0f * (bx8 - bx5);
+    a.zz = -2.0f * (bx0 + bx4) + 1.0f;
+    return a;
+}
+// posed centre of attached sphere k (attachments.hh:112-120)
+__device__ __forceinline__ void att_sphere(const EnvView& env, const AttPose& a, int k, float& X, float& Y, float& Z,
+                                           float& R)
+{
+    const VGPU_CONST float* c = env.att + kAttHdr + 4 * k;
+    X = c[0] * a.xx + c[1] * a.yx + c[2] * a.zx + a.tx;
+    Y = c[0] * a.xy + c[1] * a.yy + c[2] * a.zy + a.ty;
+    Z = c[0] * a.xz + c[1] * a.yz + c[2] * a.zz + a.tz;
+    R = c[3];
 }
 
 // sphere_sphere_self_collision (collision/validity.hh:13-44)

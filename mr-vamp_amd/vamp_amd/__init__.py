@@ -23,7 +23,7 @@ from . import _lib
 from ._lib import VgpuError, check, load
 
 __all__ = [
-    "Context", "context", "Environment", "Sphere", "Cuboid", "Cylinder", "HeightField", "make_heightfield", "Robot", "halton", "compact_device",
+    "Context", "context", "Environment", "Attachment", "Sphere", "Cuboid", "Cylinder", "HeightField", "make_heightfield", "Robot", "halton", "compact_device",
     "PandaBase", "panda", "panda_0_0", "VgpuError",
 ]
 
@@ -178,6 +178,59 @@ class _PointCloud:
         self.r_min, self.r_max, self.r_point = float(r_min), float(r_max), float(r_point)
 
 
+class Attachment:
+    """collision::Attachment<float> (collision/attachments.hh:14-123; bindings/environment.cc:197-249):
+    spheres rigidly attached at a frame relative to the end effector."""
+
+    def __init__(self, center: Sequence[float], quaternion_xyzw: Sequence[float]):
+        self.tf = np.array(list(center) + list(quaternion_xyzw), np.float32)
+        if self.tf.shape != (7,):
+            raise ValueError("center[3] and quaternion_xyzw[4]")
+        self.spheres: List[Sphere] = []
+        self.posed_spheres: List[Sphere] = []
+
+    @property
+    def relative_frame(self):
+        return (self.tf[:3].tolist(), self.tf[3:].tolist())
+
+    def add_sphere(self, sphere: Sphere):
+        self.spheres.append(sphere)
+
+    def add_spheres(self, spheres: Sequence[Sphere]):
+        self.spheres.extend(spheres)
+
+    def set_ee_pose(self, position: Sequence[float], quaternion_xyzw: Sequence[float]):
+        """Attachment::pose (attachments.hh:75-122) on the host, float32 left to right (the
+        kernels' att_pose / att_sphere): fills posed_spheres."""
+        F = np.float32
+        ptx, pty, ptz = (F(v) for v in position)
+        prx, pry, prz, prw = (F(v) for v in quaternion_xyzw)
+        ttx, tty, ttz, trx, try_, trz, trw = (F(v) for v in self.tf)
+        two, one = F(2.0), F(1.0)
+        with np.errstate(all="ignore"):
+            rx = prw * trx + prx * trw + pry * trz - prz * try_
+            ry = prw * try_ - prx * trz + pry * trw + prz * trx
+            rz = prw * trz + prx * try_ - pry * trx + prz * trw
+            rw = prw * trw - prx * trx - pry * try_ - prz * trz
+            x0, x1, x2 = pry * ttz - prz * tty, prx * tty - pry * ttx, prx * ttz - prz * ttx
+            tx = ptx + two * (prw * x0 + pry * x1 + prz * x2) + ttx
+            ty = pty + two * (-prw * x2 - prx * x1 + prz * x0) + tty
+            tz = ptz + two * (prw * x1 - prx * x2 - pry * x0) + ttz
+            b0, b1, b2, b3, b4 = ry * ry, rz * rz, rw * rz, rw * ry, rx * rx
+            b5, b6, b7, b8 = rw * rx, rx * ry, rx * rz, ry * rz
+            xx, xy, xz = -two * (b0 + b1) + one, two * (b6 + b2), two * (b7 - b3)
+            yx, yy, yz = two * (b6 - b2), -two * (b1 + b4) + one, two * (b8 + b5)
+            zx, zy, zz = two * (b7 + b3), two * (b8 - b5), -two * (b0 + b4) + one
+            self.posed_spheres = []
+            for s in self.spheres:
+                x, y, z = (F(v) for v in s.center)
+                self.posed_spheres.append(Sphere((x * xx + y * yx + z * zx + tx, x * xy + y * yy + z * zy + ty,
+                                                  x * xz + y * yz + z * zz + tz), s.r))
+
+    def _rows(self) -> np.ndarray:
+        return np.array([list(s.center) + [s.r] for s in self.spheres], np.float32).reshape(-1, 4)
+
+
 class Environment:
     """collision::Environment<float> (environment.hh:12-82) realised lazily per Context."""
 
@@ -206,6 +259,21 @@ class Environment:
     def add_heightfield(self, h: HeightField):
         self._ops.append(("heightfield", h))
         self._changed()
+
+    def attach(self, a: Attachment):
+        """Environment.attach (bindings/environment.cc:161-162): validate_motion then checks its
+        first rake block through Robot::fkcc_attach (planning/validate.hh:43)."""
+        self._ops = [op for op in self._ops if op[0] != "attach"] + [("attach", (a.tf.copy(), a._rows()))]
+        self._changed()
+
+    def detach(self):
+        """Environment.detach (bindings/environment.cc:163)."""
+        self._ops = [op for op in self._ops if op[0] != "attach"]
+        self._changed()
+
+    @property
+    def attached(self) -> bool:
+        return any(op[0] == "attach" for op in self._ops)
 
     def add_pointcloud(self, points, r_min: float, r_max: float, r_point: float) -> int:
         """Environment::add_pointcloud (bindings/environment.cc:148-158): builds a CAPT and
@@ -278,6 +346,11 @@ class Environment:
             elif kind == "heightfield":
                 rc = lib.vgpu_env_add_heightfield(h, _f3(s.center), _f3(s.scale), s.xd, s.yd,
                                                   s.data.ctypes.data_as(_lib.F32P))
+            elif kind == "attach":
+                tf, rows = s
+                rows = np.ascontiguousarray(rows, np.float32)
+                rc = lib.vgpu_env_attach(h, tf.ctypes.data_as(_lib.F32P), rows.ctypes.data_as(_lib.F32P),
+                                         rows.shape[0])
             elif kind == "pointcloud":
                 rc = lib.vgpu_env_add_pointcloud(h, s.points.ctypes.data_as(_lib.F32P), s.points.shape[0], s.r_min,
                                                  s.r_max, s.r_point, None)
@@ -441,6 +514,17 @@ class Robot:
         out = np.empty(q.shape[0], np.uint8)
         check(load().vgpu_fkcc_host(ctx.h, C.byref(self.c_robot), environment.handle(ctx),
                                     q.ctypes.data_as(_lib.F32P), q.shape[0], out.ctypes.data_as(_lib.U8P)), ctx.h)
+        return out.astype(bool)
+
+    def fkcc_attach_batch(self, q, environment: Environment, ctx: Optional[Context] = None) -> np.ndarray:
+        """Robot::fkcc_attach per configuration (robots/panda_base.hh:61-65): the environment's
+        attachment posed at each configuration's end effector."""
+        ctx = ctx or context()
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, self.dimension())
+        out = np.empty(q.shape[0], np.uint8)
+        check(load().vgpu_fkcc_attach_host(ctx.h, C.byref(self.c_robot), environment.handle(ctx),
+                                           q.ctypes.data_as(_lib.F32P), q.shape[0], out.ctypes.data_as(_lib.U8P)),
+              ctx.h)
         return out.astype(bool)
 
     def validate_batch(self, starts, goals, environment: Environment, ctx: Optional[Context] = None):

@@ -61,6 +61,10 @@ SIGNATURES = {
     "vgpu_pointcloud_collides": (C.c_int, [VP, VP, C.c_int, VP, VP, C.c_size_t, C.c_int, VP]),
     "vgpu_pointcloud_collides_host": (C.c_int, [VP, VP, C.c_int, F32P, F32P, C.c_size_t, C.c_int, U8P]),
     "vgpu_env_upload": (C.c_int, [VP]),
+    "vgpu_env_attach": (C.c_int, [VP, F32P, F32P, C.c_size_t]),
+    "vgpu_env_detach": (C.c_int, [VP]),
+    "vgpu_fkcc_attach": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, C.c_size_t, VP]),
+    "vgpu_fkcc_attach_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P]),
     "vgpu_sphere_fk": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, C.c_size_t, VP, C.c_size_t]),
     "vgpu_fkcc": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, C.c_size_t, VP]),
     "vgpu_validate_motions": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, VP, C.c_size_t, VP, VP]),

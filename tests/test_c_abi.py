@@ -104,3 +104,21 @@ def test_cpp_mirror_validate_matches_oracle(lib, tmp_path, oracle):
     assert np.array_equal(got, np.asarray(py_ok, bool))
     want, _ = oracle.validate_motions(oracle.sphere_cage_env(), s, g)
     assert (got != want).sum() <= 2  # near-margin edges only; exact masks are tested in test_gpu_parity
+
+
+def test_attachment_host_pose_identity():
+    """Attachment.set_ee_pose (attachments.hh:75-122) at the identity end-effector pose and an
+    identity relative frame leaves the spheres where they are; a pure translation adds."""
+    import numpy as np
+    import vamp_amd
+    a = vamp_amd.Attachment((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))
+    a.add_spheres([vamp_amd.Sphere((0.1, -0.2, 0.3), 0.05), vamp_amd.Sphere((0.0, 0.0, 1.0), 0.01)])
+    a.set_ee_pose((0.0, 0.0, 0.0), (0.0, 0.0, 0.0, 1.0))
+    assert np.array_equal(np.float32([s.center for s in a.posed_spheres]), np.float32([s.center for s in a.spheres]))
+    a.set_ee_pose((1.0, 2.0, 3.0), (0.0, 0.0, 0.0, 1.0))
+    assert np.allclose([s.center for s in a.posed_spheres], [[1.1, 1.8, 3.3], [1.0, 2.0, 4.0]])
+    # a quarter turn about z maps x to y
+    h = np.float32(np.sqrt(0.5))
+    a.set_ee_pose((0.0, 0.0, 0.0), (0.0, 0.0, h, h))
+    assert np.allclose(a.posed_spheres[0].center, [0.2, 0.1, 0.3], atol=1e-6)
+    assert a.relative_frame == ([0.0, 0.0, 0.0], [0.0, 0.0, 0.0, 1.0])

@@ -1,0 +1,104 @@
+"""GPU parity of the attachment path: Robot::fkcc_attach
+(panda/fk.hh:6278-11397) and validate_motion's first-block branch (planning/validate.hh:43),
+through the C ABI, against the C restatement on the same host (bit for bit) and the
+reference-DAG fixture tests/golden/attach_panda_cage.npz (margin-filtered)."""
+import numpy as np
+import pytest
+
+from conftest import golden
+from test_gpu_parity import gpu_env_from_oracle, random_scene
+from test_oracle import same_rsqrt_host, stable
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+
+
+@pytest.fixture(scope="module")
+def vamp():
+    import vamp_amd
+    assert vamp_amd.context(0) is not None
+    return vamp_amd
+
+
+def both(vamp, oracle, fx=None):
+    """The held object as a product Attachment and as an oracle Attachment."""
+    tf = fx["att_tf"] if fx is not None else oracle.held_object().tf
+    rows = fx["att_spheres"] if fx is not None else np.array(oracle.held_object().spheres, F)
+    a = vamp.Attachment(tf[:3], tf[3:])
+    o = oracle.Attachment(tf[:3], tf[3:])
+    for r in rows:
+        a.add_sphere(vamp.Sphere(r[:3], r[3]))
+        o.add_sphere(r[:3], r[3])
+    return a, o
+
+
+def test_fkcc_attach_cage(vamp, oracle):
+    fx = golden("attach_panda_cage.npz")
+    same = same_rsqrt_host(oracle, fx)
+    oenv = oracle.sphere_cage_env()
+    env = gpu_env_from_oracle(vamp, oenv)
+    a, o = both(vamp, oracle, fx)
+    env.attach(a)
+    for tag, base in (("b000", (0, 0, 0)), ("b220", (200, 200, 0))):
+        q = fx["q_" + tag]
+        got = vamp.PandaBase(*base).fkcc_attach_batch(q, env)
+        assert np.array_equal(got, oracle.robot_fkcc_attach_threads("panda", oenv, o, q, base)), tag
+        m = stable(fx["test_margin_" + tag], fx["cull_margin_" + tag], same)
+        assert np.array_equal(got[m], fx["valid_" + tag][m])
+        # validate(q) ignores attachments (bindings: fkcc, not fkcc_attach)
+        assert np.array_equal(vamp.PandaBase(*base).fkcc_batch(q, env), oracle.fkcc_threads(oenv, q, base))
+
+
+def test_validate_attach_cage(vamp, oracle):
+    fx = golden("attach_panda_cage.npz")
+    same = same_rsqrt_host(oracle, fx)
+    oenv = oracle.sphere_cage_env()
+    env = gpu_env_from_oracle(vamp, oenv)
+    a, o = both(vamp, oracle, fx)
+    env.attach(a)
+    ok, n = vamp.panda_0_0.validate_batch(fx["starts"], fx["goals"], env)
+    ook, on = oracle.robot_validate_motions_att("panda", oenv, o, fx["starts"], fx["goals"])
+    assert np.array_equal(n, on) and np.array_equal(n, fx["n"])
+    assert np.array_equal(ok, ook), "GPU != oracle on the same host"
+    m = stable(fx["edge_test_margin"], fx["edge_cull_margin"], same)
+    assert np.array_equal(ok[m], fx["ok"][m])
+    assert (~ok).sum() > 0 and ok.sum() > 0
+    env.detach()
+    ok2, _ = vamp.panda_0_0.validate_batch(fx["starts"], fx["goals"], env)
+    ook2, _ = oracle.validate_motions(oenv, fx["starts"], fx["goals"], (0, 0, 0))
+    assert np.array_equal(ok2, ook2) and (ok2 & ~ok).sum() > 0
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_attach_mixed_primitives(vamp, oracle, seed):
+    """All five primitive types and a larger object (12 spheres)."""
+    rng = np.random.default_rng(seed)
+    oenv = random_scene(oracle, rng)
+    env = gpu_env_from_oracle(vamp, oenv)
+    a = vamp.Attachment(rng.uniform(-0.05, 0.05, 3).astype(F), (0.0, 0.0, 0.0, 1.0))
+    o = oracle.Attachment(a.tf[:3], a.tf[3:])
+    for _ in range(12):
+        c, r = rng.uniform(-0.1, 0.1, 3).astype(F), F(rng.uniform(0.01, 0.05))
+        a.add_sphere(vamp.Sphere(c, r))
+        o.add_sphere(c, r)
+    env.attach(a)
+    q = oracle.scale(rng.random((16384, 7), dtype=F))
+    got = vamp.panda_0_0.fkcc_attach_batch(q, env)
+    assert np.array_equal(got, oracle.robot_fkcc_attach_threads("panda", oenv, o, q))
+    s = oracle.scale(rng.random((3000, 7), dtype=F))
+    g = oracle.scale(rng.random((3000, 7), dtype=F))
+    g[:1500] = s[:1500] + (g[:1500] - s[:1500]) * F(0.1)
+    ook, on = oracle.robot_validate_motions_att("panda", oenv, o, s, g)
+    ok, n = vamp.panda_0_0.validate_batch(s, g, env)
+    assert np.array_equal(n, on) and np.array_equal(ok, ook)
+
+
+def test_attach_other_robot_refused(vamp, oracle):
+    env = vamp.Environment()
+    a, _ = both(vamp, oracle)
+    env.attach(a)
+    q = np.zeros((4, 8), F)
+    with pytest.raises(vamp.VgpuError):
+        vamp.fetch.validate_batch(q, q, env)
+    with pytest.raises(vamp.VgpuError):
+        vamp.fetch.fkcc_attach_batch(q, env)

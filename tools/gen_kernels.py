@@ -463,9 +463,20 @@ class RobotGen:
         E = Emitter()
         fr = self.Frames(self, E)
         m = self.m
+        posed = False
         for o in m["check_order"]:
             if REMAT:
                 fr.R.clear()
+            if o["kind"] in ("att", "attenv"):
+                if not posed:  # Attachment::pose at the end-effector frame (set_attachment_pose)
+                    f = m["ee_frame"]
+                    fr.frame(f)
+                    Qe, Pe = fr.Q[f], fr.P[f]
+                    E.raw(f"const AttPose ap = att_pose(env, {Pe[0].expr()}, {Pe[1].expr()}, {Pe[2].expr()}, "
+                          f"{Qe[1].expr()}, {Qe[2].expr()}, {Qe[3].expr()}, {Qe[0].expr()});")
+                    posed = True
+                self.emit_att_check(E, fr, o)
+                continue
             if o["kind"] == "env":  # children frames first (short bounding->children gap)
                 for kid in m["env_checks"][o["index"]]["children"]:
                     fr.rot(m["spheres"][kid["sphere"]]["frame"])
@@ -492,6 +503,55 @@ class RobotGen:
                "// Monolithic fkcc: checks follow the reference hierarchy (link-bounding sphere first,",
                "// children only when the group's bounding test fires)."] + self.signature("bool", "fkcc")
         return "\n".join(hdr + E.lines + ["}", ""])
+
+    def emit_att_check(self, E, fr, o):
+        """Checks of the attached spheres (interleaved_sphere_fk_attachment only), robot frame:
+        "attenv" = every posed sphere vs the environment (validity.hh:251-266); "att" = the
+        link's entity (its bounding sphere, or its single sphere) vs every posed sphere, then
+        -- unless a leaf -- the link's spheres vs every posed sphere (validity.hh:269-293)."""
+        m = self.m
+        if o["kind"] == "attenv":
+            E.raw("{  // attachment vs environment")
+            E.raw("    uint32_t h = 0u;")
+            E.raw("    for (int k = 0; k < env.n_att; ++k) {")
+            E.raw("        float X, Y, Z, R;")
+            E.raw("        att_sphere(env, ap, k, X, Y, Z, R);")
+            E.raw("        h = env_bits<Grp, EXT>(env, X, Y, Z, R, h);")
+            E.raw("    }")
+            E.raw("    if (Grp::any_bits(h)) return false;")
+            E.raw("}")
+            return
+        ck = m["att_checks"][o["index"]]
+        c, r = self.self_ent(fr, ck["ent"])
+        E.raw(f"{{  // attachment vs {ck['link']} ({len(ck['children'])} children)")
+        E.indent += 1
+        E.raw("uint32_t h = 0u;")
+        E.raw("for (int k = 0; k < env.n_att; ++k) {")
+        E.raw("    float X, Y, Z, R;")
+        E.raw("    att_sphere(env, ap, k, X, Y, Z, R);")
+        E.raw(f"    h |= self_bits({c[0].expr()}, {c[1].expr()}, {c[2].expr()}, {flit(r)}, X, Y, Z, R);")
+        E.raw("}")
+        if ck.get("leaf"):
+            E.raw("if (Grp::any_bits(h)) return false;")
+        else:
+            E.raw("if (Grp::any_bits(h)) {")
+            E.indent += 1
+            E.raw("uint32_t hc = 0u;")
+            spheres = m["spheres"]
+            for sidx in ck["children"]:
+                sp = spheres[sidx]
+                cs = fr.center(sp["frame"], sp["offset"])
+                E.raw("for (int k = 0; k < env.n_att; ++k) {")
+                E.raw("    float X, Y, Z, R;")
+                E.raw("    att_sphere(env, ap, k, X, Y, Z, R);")
+                E.raw(f"    hc |= self_bits({cs[0].expr()}, {cs[1].expr()}, {cs[2].expr()}, {flit(sp['radius'])}, "
+                      "X, Y, Z, R);")
+                E.raw("}")
+            E.raw("if (Grp::any_bits(hc)) return false;")
+            E.indent -= 1
+            E.raw("}")
+        E.indent -= 1
+        E.raw("}")
 
     def gen_staged(self) -> str:
         """Staged fkcc (same result, see DESIGN.md "Staged checks"):
@@ -564,7 +624,9 @@ def main():
         vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model[key])
         consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
     out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
-    if len(model["check_order"]) <= 64:  # check masks: 32-bit up to 32 checks, 64-bit up to 64
+    if "att_checks" in model:  # the attachment variant: its fkcc only (first rake block)
+        out = g.gen_fkcc()
+    elif len(model["check_order"]) <= 64:  # check masks: 32-bit up to 32 checks, 64-bit up to 64
         out += "\n" + g.gen_staged()
     if "--pair" in sys.argv:  # the composite's inter-robot check, as its own include
         out = g.gen_pair_inter()
