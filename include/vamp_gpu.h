@@ -178,6 +178,27 @@ int vgpu_fkcc_attach_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env,
 int vgpu_validate_motions_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *starts,
                                const float *goals, size_t n_edges, uint8_t *ok, int32_t *n_blocks);
 
+/* ---- PRM roadmap edge stage (planning/prm.hh:235-299) ------------------------------------ */
+/* PRMStarNeighborParams(dim, space_measure) with gamma_scale (roadmap.hh:42-77, bindings
+ * settings.cc:38-44): k[i] = max_neighbors(i), r[i] = neighbor_radius(i) for roadmap sizes
+ * i = 0 .. n-1 (k = 0 for i < 2: start and goal are inserted without a query). */
+int vgpu_prm_neighbor_params(int dim, double space_measure, double gamma_scale, size_t n, uint32_t *k, float *r);
+/* The neighbour query build_roadmap runs for every vertex i (prm.hh:264-266, NN::nearest on
+ * the vertices 0 .. i-1): at most k[i] of them within r[i] (distance <= r), nearest first,
+ * distance = Space<dim>::distance (nn.hh:53-57).  Device pointers: V[n][dim] -> nbr[n][kmax],
+ * dist[n][kmax], cnt[n].  dim in {6, 7, 8, 14}, kmax <= 64. */
+int vgpu_roadmap_knn(vgpu_ctx *ctx, int dim, const float *V, size_t n, const uint32_t *k, const float *r,
+                     uint32_t kmax, uint32_t *nbr, float *dist, uint32_t *cnt);
+/* Roadmap::build_roadmap's graph for the vertex sequence V[n][dim] (start, goal, then the valid
+ * samples in draw order -- vgpu_sample_fkcc + vgpu_compact): every vertex's neighbour query,
+ * validate_motion(neighbor, vertex) of every candidate on the GPU, and the adjacency lists in
+ * the reference's append order (prm.hh:270-275, Roadmap::edges): offsets[n+1], adj[*n_adj].
+ * If adj_cap < *n_adj the call fails with VGPU_ERR_INVALID_ARG and *n_adj = the required size.
+ * component (optional) = smallest vertex index of each vertex's connected component. */
+int vgpu_build_roadmap_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *V, size_t n,
+                            double space_measure, double gamma_scale, size_t *offsets, uint32_t *adj,
+                            size_t adj_cap, size_t *n_adj, uint32_t *component);
+
 /* ---- robot metadata ------------------------------------------------------------------------ */
 /* dimension, resolution, n_spheres of a robot kind (robots/panda_base.hh:19-23) */
 int vgpu_pointcloud_collides_host(vgpu_ctx *ctx, vgpu_env *env, int index, const float *centers,

@@ -1412,3 +1412,171 @@ extern "C" int vgpu_sample_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
 }
+
+// ---------------------------------------------------------------------------------------
+// PRM roadmap edge stage (planning/prm.hh:235-299; vgpu_roadmap.hip)
+// ---------------------------------------------------------------------------------------
+extern "C" hipError_t vgpu_launch_roadmap_knn(int dim, const float* V, uint32_t n, const uint32_t* k, const float* r,
+                                              uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt,
+                                              hipStream_t st);
+extern "C" hipError_t vgpu_launch_edge_gather(const float* V, uint32_t n, int dim, const uint32_t* nbr, uint32_t kmax,
+                                              const uint32_t* cnt, const uint32_t* off, float* starts, float* goals,
+                                              hipStream_t st);
+
+// PRMStarNeighborParams (roadmap.hh:42-77) for roadmap sizes 0 .. n-1, in double as the reference
+extern "C" int vgpu_prm_neighbor_params(int dim, double space_measure, double gamma_scale, size_t n, uint32_t* k,
+                                        float* r)
+{
+    if (dim <= 0 || (n && (!k || !r))) return VGPU_ERR_INVALID_ARG;
+    const double E = 2.718281828459045235360287471352662498;  // constants.hh:6
+    const double PI = 3.141592653589793238462643383279502884;
+    const double kc = E + (E / (double)dim);
+    const double inv = 1.0 / (double)dim;
+    const double ball = std::pow(std::sqrt(PI), (double)dim) / std::tgamma((double)dim / 2.0 + 1.0);
+    const double prm = 2.0 * std::pow(1.0 + inv, inv) * std::pow(space_measure / ball, inv);
+    for (size_t i = 0; i < n; ++i) {
+        if (i < 2) {  // start and goal are inserted without a query (prm.hh:228-233)
+            k[i] = 0;
+            r[i] = 0.0f;
+            continue;
+        }
+        const double d = kc * std::log((double)i);
+        const size_t s = (size_t)d;  // c_ceil (utils.hh:28-32)
+        const size_t kk = d > (double)s ? s + 1 : s;
+        k[i] = (uint32_t)std::min<size_t>(kk, 0xFFFFFFFFu);
+        r[i] = (float)(gamma_scale * prm * std::pow(std::log((double)i) / (double)i, inv));
+    }
+    return VGPU_OK;
+}
+
+static bool knn_dim_ok(int dim) { return dim == 6 || dim == 7 || dim == 8 || dim == 14; }
+
+extern "C" int vgpu_roadmap_knn(vgpu_ctx* c, int dim, const float* V, size_t n, const uint32_t* k, const float* r,
+                                uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (!knn_dim_ok(dim)) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap kNN: dimension 6, 7, 8 or 14");
+    if (kmax == 0 || kmax > 64) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap kNN: 1 <= kmax <= 64");
+    if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many vertices");
+    if (n && (!V || !k || !r || !nbr || !dist || !cnt)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_roadmap_knn(dim, V, (uint32_t)n, k, r, kmax, nbr, dist, cnt, c->cur));
+    return VGPU_OK;
+}
+
+namespace {
+struct DevBufs {  // call-scoped device allocations
+    std::vector<void*> p;
+    ~DevBufs()
+    {
+        for (void* q : p) (void)hipFree(q);
+    }
+    template <class T>
+    hipError_t get(T** out, size_t count)
+    {
+        void* q = nullptr;
+        hipError_t e = hipMalloc(&q, std::max<size_t>(count, 1) * sizeof(T));
+        if (e == hipSuccess) p.push_back(q);
+        *out = (T*)q;
+        return e;
+    }
+};
+}  // namespace
+
+extern "C" int vgpu_build_roadmap_host(vgpu_ctx* c, const vgpu_robot* robot, vgpu_env* e, const float* V, size_t n,
+                                       double space_measure, double gamma_scale, size_t* offsets, uint32_t* adj,
+                                       size_t adj_cap, size_t* n_adj, uint32_t* component)
+{
+    if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
+    float b[3];
+    int rc = check_robot(c, robot, b);
+    if (rc) return rc;
+    const int dim = (int)dim_of(robot);
+    if (!knn_dim_ok(dim)) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap: robot dimension");
+    if (n && (!V || !offsets || !n_adj)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many vertices");
+    if (n_adj) *n_adj = 0;
+    if (n == 0) {
+        if (offsets) offsets[0] = 0;
+        return VGPU_OK;
+    }
+    std::vector<uint32_t> k(n);
+    std::vector<float> r(n);
+    if ((rc = vgpu_prm_neighbor_params(dim, space_measure, gamma_scale, n, k.data(), r.data()))) return rc;
+    uint32_t kmax = 1;
+    for (uint32_t v : k) kmax = std::max(kmax, v);
+    kmax = std::min<uint32_t>(kmax, (uint32_t)n);
+    if (kmax > 64) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap kNN: more than 64 neighbours per query");
+    HIPCHK(c, hipSetDevice(c->device));
+    DevBufs db;
+    float *dV, *dr, *dd;
+    uint32_t *dk, *dn, *dc, *doff;
+    HIPCHK(c, db.get(&dV, n * dim));
+    HIPCHK(c, db.get(&dk, n));
+    HIPCHK(c, db.get(&dr, n));
+    HIPCHK(c, db.get(&dn, n * kmax));
+    HIPCHK(c, db.get(&dd, n * kmax));
+    HIPCHK(c, db.get(&dc, n));
+    HIPCHK(c, db.get(&doff, n + 1));
+    HIPCHK(c, hipMemcpyAsync(dV, V, n * dim * sizeof(float), hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipMemcpyAsync(dk, k.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipMemcpyAsync(dr, r.data(), n * sizeof(float), hipMemcpyHostToDevice, c->cur));
+    if ((rc = vgpu_roadmap_knn(c, dim, dV, n, dk, dr, kmax, dn, dd, dc))) return rc;
+    std::vector<uint32_t> cnt(n), off(n + 1);
+    HIPCHK(c, hipMemcpyAsync(cnt.data(), dc, n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    off[0] = 0;
+    for (size_t i = 0; i < n; ++i) off[i + 1] = off[i] + cnt[i];
+    const size_t E = off[n];
+    std::vector<uint32_t> nb(n * (size_t)kmax);
+    std::vector<uint8_t> ok(E);
+    if (E) {
+        float *ds, *dg;
+        uint8_t* dok;
+        HIPCHK(c, db.get(&ds, E * dim));
+        HIPCHK(c, db.get(&dg, E * dim));
+        HIPCHK(c, db.get(&dok, E));
+        HIPCHK(c, hipMemcpyAsync(doff, off.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, c->cur));
+        HIPCHK(c, vgpu_launch_edge_gather(dV, (uint32_t)n, dim, dn, kmax, dc, doff, ds, dg, c->cur));
+        // validate_motion(neighbor, vertex) for every candidate (prm.hh:267-276)
+        if ((rc = vgpu_validate_motions(c, robot, e, ds, dg, E, dok, nullptr))) return rc;
+        HIPCHK(c, hipMemcpyAsync(ok.data(), dok, E, hipMemcpyDeviceToHost, c->cur));
+        HIPCHK(c, hipMemcpyAsync(nb.data(), dn, n * (size_t)kmax * sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
+        HIPCHK(c, hipStreamSynchronize(c->cur));
+    }
+    // adjacency in the reference's append order: vertex i gets its valid neighbours nearest
+    // first when it is inserted, and every neighbour j gets i appended (prm.hh:270-275), so a
+    // vertex's list = its own valid neighbours, then the later vertices that connected to it
+    std::vector<uint32_t> deg(n, 0);
+    for (size_t i = 0; i < n; ++i)
+        for (uint32_t m = 0; m < cnt[i]; ++m)
+            if (ok[off[i] + m]) ++deg[i], ++deg[nb[i * kmax + m]];
+    offsets[0] = 0;
+    for (size_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + deg[i];
+    *n_adj = offsets[n];
+    if (offsets[n] > adj_cap || (offsets[n] && !adj))
+        return fail(c, VGPU_ERR_INVALID_ARG, "adjacency capacity too small (*n_adj = required entries)");
+    std::vector<size_t> fill(offsets, offsets + n);
+    for (size_t i = 0; i < n; ++i)
+        for (uint32_t m = 0; m < cnt[i]; ++m)
+            if (ok[off[i] + m]) {
+                const uint32_t j = nb[i * kmax + m];
+                adj[fill[i]++] = j;
+                adj[fill[j]++] = (uint32_t)i;
+            }
+    if (component) {  // union-find: each vertex's component = its smallest vertex index
+        std::vector<uint32_t> parent(n);
+        for (size_t i = 0; i < n; ++i) parent[i] = (uint32_t)i;
+        auto find = [&](uint32_t a) {
+            while (parent[a] != a) a = parent[a] = parent[parent[a]];
+            return a;
+        };
+        for (size_t i = 0; i < n; ++i)
+            for (size_t p = offsets[i]; p < offsets[i + 1]; ++p) {
+                const uint32_t a = find((uint32_t)i), bb = find(adj[p]);
+                if (a != bb) parent[std::max(a, bb)] = std::min(a, bb);
+            }
+        for (size_t i = 0; i < n; ++i) component[i] = find((uint32_t)i);
+    }
+    return VGPU_OK;
+}

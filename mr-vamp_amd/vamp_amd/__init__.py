@@ -401,6 +401,15 @@ def compact_device(rows_ptr: int, valid_ptr: int, n: int, dim: int, rows_out_ptr
 
 
 # ---- robots -----------------------------------------------------------------------------------
+# Robot::space_measure of each robot: the reference's generated constant returned as float
+# (panda/fk.hh:88-91 "-> float"), values as extracted into model/<robot>.json; the composite is
+# two Pandas (product)
+_SPACE_MEASURE = {k: float(np.float32(v)) for k, v in {
+    _lib.VGPU_ROBOT_PANDA: 878819.1112640093, _lib.VGPU_ROBOT_FETCH: 269832.2635954135,
+    _lib.VGPU_ROBOT_UR5: 700852.7173113511, _lib.VGPU_ROBOT_BAXTER: 89641415145.821,
+    _lib.VGPU_ROBOT_PANDA_PAIR: 878819.1112640093 ** 2}.items()}
+
+
 class Robot:
     """Python face of a vamp::robots robot: PandaBase<X100, Y100, Z100>
     (robots/panda_base.hh:15-75) or Fetch (robots/fetch.hh:8-48)."""
@@ -456,6 +465,11 @@ class Robot:
 
     def resolution(self) -> int:
         return self._meta()[1]
+
+    def space_measure(self) -> float:
+        """Robot::space_measure (robots/panda_base.hh:22 -> panda/fk.hh; fetch.hh:14): the product
+        of the joint ranges, the PRMNeighborParams input (src/vamp/__init__.py:91)."""
+        return _SPACE_MEASURE[self.kind]
 
     def n_spheres(self) -> int:
         return self._meta()[2]

@@ -78,6 +78,10 @@ SIGNATURES = {
     "vgpu_halton_host": (C.c_int, [VP, C.c_int, C.c_uint64, C.c_size_t, F32P]),
     "vgpu_sample_fkcc_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, C.c_uint64, C.c_size_t, F32P, U8P]),
     "vgpu_robot_info": (C.c_int, [C.c_int32, I32P, I32P, I32P]),
+    "vgpu_prm_neighbor_params": (C.c_int, [C.c_int, C.c_double, C.c_double, C.c_size_t, U32P, F32P]),
+    "vgpu_roadmap_knn": (C.c_int, [VP, C.c_int, VP, C.c_size_t, VP, VP, C.c_uint32, VP, VP, VP]),
+    "vgpu_build_roadmap_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, C.c_double, C.c_double,
+                                          C.POINTER(C.c_size_t), U32P, C.c_size_t, C.POINTER(C.c_size_t), U32P]),
 }
 
 _lib = None

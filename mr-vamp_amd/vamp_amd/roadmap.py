@@ -18,7 +18,9 @@ without the HIP library the calls raise.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
+
+import numpy as np
 
 
 def shard_range(n_draws: int, rank: int, world: int, first: int = 1) -> Tuple[int, int]:
@@ -108,3 +110,70 @@ def roadmap_vertices(robot, environment, n_draws: int, first: int = 1, start=Non
     if max_samples is not None:
         rows, draws = rows[:max_samples], draws[:max_samples]
     return rows, draws
+
+
+# ---- edge stage (prm.hh:255-299) ----------------------------------------------------------------
+def prm_neighbor_params(dim: int, space_measure: float, n: int, gamma_scale: float = 2.0):
+    """PRMStarNeighborParams (roadmap.hh:42-77) for roadmap sizes 0 .. n-1: (k[n], r[n])."""
+    from . import _lib
+    from ._lib import check, load
+    k = np.zeros(n, np.uint32)
+    r = np.zeros(n, np.float32)
+    check(load().vgpu_prm_neighbor_params(dim, float(space_measure), float(gamma_scale), n,
+                                          k.ctypes.data_as(_lib.U32P), r.ctypes.data_as(_lib.F32P)))
+    return k, r
+
+
+class Roadmap:
+    """Roadmap<dim> (prm.hh:285-299): vertices [n, dim] and, per vertex, the indices of its
+    neighbours in the order build_roadmap appended them; plus the connected components."""
+
+    def __init__(self, vertices, offsets, adj, component):
+        self.vertices = vertices
+        self.offsets = offsets
+        self.adj = adj
+        self.component = component
+
+    @property
+    def edges(self) -> List[List[int]]:
+        o = self.offsets
+        return [self.adj[o[i]:o[i + 1]].tolist() for i in range(len(o) - 1)]
+
+    def n_edges(self) -> int:
+        return int(self.offsets[-1]) // 2
+
+
+def build_roadmap_edges(robot, environment, vertices, gamma_scale: float = 2.0, space_measure=None,
+                        ctx=None) -> Roadmap:
+    """The graph of Roadmap::build_roadmap over a given vertex sequence (start, goal, valid samples
+    in draw order): every vertex's PRM* neighbour query and validate_motion of every candidate
+    edge on the GPU (vgpu_build_roadmap_host), adjacency in the reference's append order."""
+    import ctypes as C
+
+    from . import _lib, context
+    from ._lib import check, load
+    ctx = ctx or context()
+    V = np.ascontiguousarray(vertices, np.float32).reshape(-1, robot.dimension())
+    n = V.shape[0]
+    sm = robot.space_measure() if space_measure is None else float(space_measure)
+    k, _ = prm_neighbor_params(robot.dimension(), sm, n, gamma_scale)
+    cap = 2 * int(k.astype(np.int64).sum())
+    offsets = np.zeros(n + 1, np.uint64)
+    adj = np.zeros(max(cap, 1), np.uint32)
+    comp = np.zeros(max(n, 1), np.uint32)
+    n_adj = C.c_size_t()
+    check(load().vgpu_build_roadmap_host(ctx.h, C.byref(robot.c_robot), environment.handle(ctx),
+                                         V.ctypes.data_as(_lib.F32P), n, sm, float(gamma_scale),
+                                         offsets.ctypes.data_as(C.POINTER(C.c_size_t)),
+                                         adj.ctypes.data_as(_lib.U32P), adj.shape[0], C.byref(n_adj),
+                                         comp.ctypes.data_as(_lib.U32P)), ctx.h)
+    return Roadmap(V, offsets.astype(np.int64), adj[:n_adj.value], comp[:n])
+
+
+def build_roadmap(robot, start, goal, environment, max_iterations: int = 100000, max_samples: int = 100000,
+                  gamma_scale: float = 2.0, ctx=None, group=None) -> Roadmap:
+    """Roadmap::build_roadmap (prm.hh:197-299) with the Halton sampler: vertices = start, goal and
+    the valid samples of draws 1..max_iterations, at most max_samples vertices (the sampling
+    stage sharded over ranks when torch.distributed is initialised), then the edge stage."""
+    rows, _ = roadmap_vertices(robot, environment, max_iterations, 1, start, goal, max_samples, ctx, group)
+    return build_roadmap_edges(robot, environment, rows.cpu().numpy(), gamma_scale, None, ctx)

@@ -196,6 +196,13 @@ void vo_pair_validate_motions(const vo_env *env, const float *starts, const floa
 /* Sample with 1-based draw index k (k-th call to next()) of Halton<dim>, dim <= 16. */
 void vo_halton(int dim, uint64_t k, float *out);
 
+/* ---- PRM roadmap edge stage (planning/prm.hh:235-283, roadmap.hh:42-77, nn.hh:53-57) ---- */
+size_t vo_prm_max_neighbors(int dim, size_t num_states);
+float vo_prm_neighbor_radius(int dim, double space_measure, double gamma_scale, size_t num_states);
+float vo_config_distance(const float *a, const float *b, int dim);
+void vo_roadmap_knn(int dim, const float *V, size_t n, double space_measure, double gamma_scale, uint32_t kmax,
+                    uint32_t *nbr, float *dist, uint32_t *cnt, int threads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -6,6 +6,7 @@ cpu_baseline leg, as the checker.  Never part of the product path.
 from __future__ import annotations
 
 import ctypes as C
+import json
 import os
 import subprocess
 
@@ -568,3 +569,78 @@ def robot_validate_motions_att(robot, env: Env, att: Attachment, starts, goals, 
     lib().vo_robot_validate_motions_att(rid, C.byref(ce), C.byref(ca), fp(s), fp(g), s.shape[0], *base100,
                                         ok.ctypes.data_as(U8P), n.ctypes.data_as(I32P), threads)
     return ok.astype(bool), n
+
+
+# ---- PRM roadmap edge stage (planning/prm.hh:235-283) ----
+# Robot::space_measure() returns float (panda/fk.hh:88-91)
+SPACE_MEASURE = {r: float(np.float32(json.load(open(os.path.join(ROOT, "model", f"{r}.json")))["space_measure"]))
+                 for r in ("panda", "fetch", "ur5", "baxter")}
+
+
+def prm_max_neighbors(dim, n):
+    L = lib()
+    L.vo_prm_max_neighbors.restype = C.c_size_t
+    L.vo_prm_max_neighbors.argtypes = [C.c_int, C.c_size_t]
+    return int(L.vo_prm_max_neighbors(dim, n))
+
+
+def prm_neighbor_radius(dim, space_measure, gamma, n):
+    L = lib()
+    L.vo_prm_neighbor_radius.restype = C.c_float
+    L.vo_prm_neighbor_radius.argtypes = [C.c_int, C.c_double, C.c_double, C.c_size_t]
+    return np.float32(L.vo_prm_neighbor_radius(dim, space_measure, gamma, n))
+
+
+def roadmap_knn(V, space_measure, gamma=2.0, kmax=None, threads=8):
+    """The neighbour lists build_roadmap queries for each vertex (nearest first)."""
+    V = np.ascontiguousarray(V, np.float32)
+    n, dim = V.shape
+    kmax = kmax or max(1, prm_max_neighbors(dim, max(n - 1, 2)))
+    nbr = np.zeros((n, kmax), np.uint32)
+    dist = np.zeros((n, kmax), np.float32)
+    cnt = np.zeros(n, np.uint32)
+    L = lib()
+    L.vo_roadmap_knn.argtypes = [C.c_int, F32P, C.c_size_t, C.c_double, C.c_double, C.c_uint32,
+                                 C.POINTER(C.c_uint32), F32P, C.POINTER(C.c_uint32), C.c_int]
+    U32P_ = C.POINTER(C.c_uint32)
+    L.vo_roadmap_knn(dim, fp(V), n, space_measure, gamma, kmax, nbr.ctypes.data_as(U32P_), fp(dist),
+                     cnt.ctypes.data_as(U32P_), threads)
+    return nbr, dist, cnt
+
+
+def build_roadmap_edges(robot, env: Env, V, base100=(0, 0, 0), gamma=2.0, threads=8):
+    """Roadmap::build_roadmap's graph (prm.hh:235-299) for the vertex sequence V (start, goal,
+    valid samples in draw order): per vertex, its valid neighbours in query order (nearest
+    first), then the later vertices that connected to it, ascending -- the order the reference
+    appends them (prm.hh:268-276).  The kNN does not depend on edge validity, so every candidate
+    edge is validated in one parallel batch (validate_motion(neighbor, new vertex))."""
+    V = np.ascontiguousarray(V, np.float32)
+    n, dim = V.shape
+    nbr, dist, cnt = roadmap_knn(V, SPACE_MEASURE[robot], gamma, threads=threads)
+    qi = np.repeat(np.arange(n), cnt.astype(np.int64))
+    qm = np.concatenate([np.arange(c) for c in cnt]) if n else np.zeros(0, np.int64)
+    cand = nbr[qi, qm].astype(np.int64)
+    ok, _ = robot_validate_motions(robot, env, V[cand], V[qi], base100, threads)
+    edges = [[] for _ in range(n)]
+    for i, j, good in zip(qi.tolist(), cand.tolist(), ok.tolist()):
+        if good:
+            edges[i].append(j)
+            edges[j].append(i)
+    return edges, (nbr, dist, cnt, ok)
+
+
+def components(n, edges):
+    """Connected components by union-find: the smallest vertex index of each vertex's component."""
+    parent = list(range(n))
+
+    def find(a):
+        while parent[a] != a:
+            parent[a] = parent[parent[a]]
+            a = parent[a]
+        return a
+    for i, lst in enumerate(edges):
+        for j in lst:
+            a, b = find(i), find(j)
+            if a != b:
+                parent[max(a, b)] = min(a, b)
+    return np.array([find(i) for i in range(n)], np.uint32)

@@ -1,0 +1,93 @@
+"""GPU parity of the PRM roadmap edge stage: the causal kNN kernel and
+vgpu_build_roadmap_host (neighbour queries + batched validate_motion + append-order adjacency +
+union-find) against the oracle's build_roadmap restatement on the same host: identical
+neighbour lists, distances, edge lists and components."""
+import numpy as np
+import pytest
+
+from test_gpu_parity import gpu_env_from_oracle, random_scene
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+
+
+@pytest.fixture(scope="module")
+def vamp():
+    import vamp_amd
+    assert vamp_amd.context(0) is not None
+    return vamp_amd
+
+
+def knn_gpu(vamp, V, sm, kmax=None):
+    import torch
+    from vamp_amd import roadmap
+    n, dim = V.shape
+    k, r = roadmap.prm_neighbor_params(dim, sm, n)
+    kmax = kmax or int(max(1, k.max()))
+    dev = torch.device("cuda", 0)
+    tV = torch.from_numpy(V).to(dev)
+    tk = torch.from_numpy(k.view(np.int32)).to(dev)
+    tr = torch.from_numpy(r).to(dev)
+    nbr = torch.zeros((n, kmax), dtype=torch.int32, device=dev)
+    dist = torch.zeros((n, kmax), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    ctx = vamp.context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    from vamp_amd._lib import check, load
+    check(load().vgpu_roadmap_knn(ctx.h, dim, tV.data_ptr(), n, tk.data_ptr(), tr.data_ptr(), kmax,
+                                  nbr.data_ptr(), dist.data_ptr(), cnt.data_ptr()), ctx.h)
+    torch.cuda.synchronize()
+    return nbr.cpu().numpy().view(np.uint32), dist.cpu().numpy(), cnt.cpu().numpy().view(np.uint32)
+
+
+@pytest.mark.parametrize("robot,dim,n", [("panda", 7, 20000), ("fetch", 8, 6000), ("ur5", 6, 3000),
+                                         ("baxter", 14, 3000)])
+def test_knn_equals_oracle(vamp, oracle, robot, dim, n):
+    rng = np.random.default_rng(21)
+    V = oracle.robot_scale(robot, rng.random((n, dim), dtype=F))
+    V[n // 2] = V[n // 3]  # duplicate vertex (distance 0)
+    sm = oracle.SPACE_MEASURE[robot]
+    onb, od, oc = oracle.roadmap_knn(V, sm)
+    gnb, gd, gc = knn_gpu(vamp, V, sm, onb.shape[1])
+    assert np.array_equal(gc, oc)
+    mask = np.arange(onb.shape[1])[None, :] < oc[:, None]
+    assert np.array_equal(gnb[mask], onb[mask]) and np.array_equal(gd[mask], od[mask])
+    assert oc[2:].min() >= 1
+
+
+def test_build_roadmap_equals_oracle(vamp, oracle):
+    """Vertices = start, goal, valid Halton samples (the GPU sampling stage); edges and
+    components of build_roadmap on the sphere cage."""
+    oenv = oracle.sphere_cage_env()
+    env = gpu_env_from_oracle(vamp, oenv)
+    robot = vamp.panda_0_0
+    draws = vamp.halton(7, 1, 6000)
+    q = robot.scale_configuration(draws)
+    valid = robot.fkcc_batch(q, env)
+    start, goal = q[valid][0], q[valid][1]
+    V = np.concatenate([start[None], goal[None], q[valid][2:2500]]).astype(F)
+    from vamp_amd import roadmap
+    rm = roadmap.build_roadmap_edges(robot, env, V)
+    edges, _ = oracle.build_roadmap_edges("panda", oenv, V)
+    assert rm.edges == edges
+    assert np.array_equal(rm.component, oracle.components(len(V), edges))
+    assert rm.n_edges() > len(V)
+
+
+def test_build_roadmap_end_to_end(vamp, oracle):
+    """Roadmap::build_roadmap with max_iterations draws and max_samples vertices on a mixed
+    primitive scene: vertex sequence and graph equal the oracle's."""
+    rng = np.random.default_rng(22)
+    oenv = random_scene(oracle, rng, 3, 3, 2)
+    env = gpu_env_from_oracle(vamp, oenv)
+    robot = vamp.panda_0_0
+    s = oracle.scale(rng.random((1, 7), dtype=F))[0]
+    g = oracle.scale(rng.random((1, 7), dtype=F))[0]
+    from vamp_amd import roadmap
+    rm = roadmap.build_roadmap(robot, s, g, env, max_iterations=4000, max_samples=1500)
+    V = rm.vertices
+    q = oracle.scale(oracle.halton(7, range(1, 4001)))
+    want = np.concatenate([s[None], g[None], q[oracle.fkcc_threads(oenv, q)]])[:1500]
+    assert np.array_equal(V, want)
+    edges, _ = oracle.build_roadmap_edges("panda", oenv, V)
+    assert rm.edges == edges
