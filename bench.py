@@ -51,9 +51,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
     ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", default="validate", choices=["validate", "capt", "fetch_prm", "pair"],
+    ap.add_argument("--workload", default="validate", choices=["validate", "capt", "fetch_prm", "prm_edges", "pair"],
                     help="validate: BASELINE configs[1] (the headline); capt: configs[2]; fetch_prm: configs[3] "
-                         "vertex stage; pair: configs[4] two-Panda composite edges")
+                         "vertex stage; prm_edges: configs[3] edge stage; pair: configs[4] two-Panda composite edges")
+    ap.add_argument("--vertices", type=int, default=100_000,
+                    help="prm_edges: roadmap vertices (RoadmapSettings::max_samples default, roadmap.hh:170)")
     ap.add_argument("--draws", type=int, default=4_000_000, help="fetch_prm: Halton draws per step (whole job)")
     return ap.parse_args()
 
@@ -280,6 +282,112 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     print(json.dumps(line))
 
 
+def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
+    """BASELINE configs[3] edge stage (SURVEY §8f rank 1): Roadmap::build_roadmap's graph over the
+    first V vertices of the Fetch vertex sequence (two valid draws as start and goal, then the
+    valid Halton<8> draws in order; MBM table_pick scene): every vertex's PRM* neighbour query
+    (causal kNN kernel), validate_motion of every candidate edge, the exchange of valid pairs and
+    the host adjacency/component assembly.  Queries split over ranks by equal prefix work; total
+    vertices fixed (strong scaling).  One step = the whole edge stage."""
+    from vamp_amd import roadmap
+
+    env, fx = fetch_scene(vamp)
+    robot = vamp.fetch
+    dim = 8
+    draws = int(a.vertices / 0.6) + 4096
+    rows, _, cnt = roadmap.sample_valid_shard(torch, robot, env, 1, draws, ctx, dev)
+    n = min(a.vertices, cnt)
+    V = rows[:n].contiguous()
+    k_np, r_np = roadmap.prm_neighbor_params(dim, robot.space_measure(), n)
+    kmax = int(max(1, min(int(k_np.max()), n)))
+    k = torch.from_numpy(k_np.view(np.int32)).to(dev)
+    r = torch.from_numpy(r_np).to(dev)
+    qf, qc = roadmap.query_split(n, rank, world)
+    info = {}
+
+    def step():
+        pairs = roadmap.edges_shard(torch, robot, env, V, k, r, kmax, qf, qc, ctx)
+        if world > 1:
+            pairs = roadmap.allgather_pairs(torch, dist, pairs)
+        off, adj, comp = roadmap.assemble(n, pairs.cpu().numpy())
+        info.update(pairs=int(pairs.shape[0]), components=int(len(np.unique(comp))))
+
+    wall = timed_steps(a, torch, dist, dev, world, step)
+    wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(n) / world, dev, world)
+    # the kNN kernel alone (this rank's queries), HIP events on the launch stream
+    nbr = torch.empty((max(qc, 1), kmax), dtype=torch.int32, device=dev)
+    dd = torch.empty((max(qc, 1), kmax), dtype=torch.float32, device=dev)
+    cc = torch.empty(max(qc, 1), dtype=torch.int32, device=dev)
+    from vamp_amd._lib import check, load
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(a.steps):
+        check(load().vgpu_roadmap_knn_range(ctx.h, dim, V.data_ptr(), n, qf, qc, k.data_ptr(), r.data_ptr(), kmax,
+                                            nbr.data_ptr(), dd.data_ptr(), cc.data_ptr()), ctx.h)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    knn_ms = e0.elapsed_time(e1) / a.steps
+    candidates = int(cc[:qc].long().sum())
+    if rank != 0:
+        return
+    # algorithmic work of the query kernel: one Space<8>::distance per (vertex, earlier vertex)
+    # pair = 8 sub + 8 mul + 7 add + 1 sqrt (nn.hh:53-57)
+    pairs_scanned = sum(range(qf, qf + qc))
+    flops = 24.0 * pairs_scanned
+    achieved = flops / (knn_ms * 1e-3) / 1e12
+    cpu = None
+    if not a.no_cpu and world == 1:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_py as op
+        from test_oracle_fetch import fetch_env
+
+        oenv = fetch_env(op, fx)
+        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        Vh = V.cpu().numpy()
+        m = 4000
+        while True:  # grow the prefix until the restated stage takes ~cpu_seconds
+            t = time.perf_counter()
+            nb_, _, cn_ = op.roadmap_knn(Vh[:m], op.SPACE_MEASURE["fetch"], threads=threads)
+            qi = np.repeat(np.arange(m), cn_.astype(np.int64))
+            qm = np.concatenate([np.arange(c) for c in cn_]).astype(np.int64)
+            qj = nb_[qi, qm].astype(np.int64)
+            op.robot_validate_motions("fetch", oenv, Vh[qj], Vh[qi], threads=threads)
+            dt = time.perf_counter() - t
+            if dt >= a.cpu_seconds / 3 or m >= n:
+                break
+            m = min(n, int(m * min(4.0, max(1.3, (a.cpu_seconds / max(dt, 1e-3)) ** 0.5))))
+        cpu = {"value": m / dt, "unit": "vertices/s", "cores": threads, "kind": "port",
+               "sample": f"the first {m} vertices of the same sequence: oracle/vamp_oracle.c brute-force neighbour "
+                         f"queries + validate_motion of the {len(qi)} candidates, {threads} threads, {dt:.1f} s "
+                         f"(the stage is superlinear in the vertex count: the rate at {n} is lower)",
+               "cpu_model": cpu_model()}
+    line = {
+        "metric": "PRM edge-stage roadmap vertices/sec (Fetch 8-DOF build_roadmap: neighbour queries + edge validation)",
+        "value": units_all * a.steps / wall_max,
+        "unit": "vertices/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": wall_max / a.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (the Halton<8> vertex sequence of configs[3] on MBM table_pick_fetch scene0001)",
+        "config": {"workload": f"BASELINE configs[3] edge stage: build_roadmap graph over {n} Fetch vertices, queries "
+                               f"split over {world} GPU(s), one exchange of valid pairs",
+                   "robot": "Fetch", "vertices": n, "kmax": kmax, "candidate_edges_rank0": candidates,
+                   "valid_edges": info.get("pairs"), "components": info.get("components"),
+                   "parallelism": f"dp{world} (query ranges of equal prefix work, one all-gather)"},
+        "roofline": {"kernel": "knn_kernel<8, K> (causal neighbour queries)", "bound": "valu", "achieved": achieved,
+                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+                     "traffic": None, "kernel_ms": knn_ms, "algorithmic_flops_per_vertex_pair": 24,
+                     "vertex_pairs_rank0": pairs_scanned},
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line))
+
+
 def timed_steps(a, torch, dist, dev, world, step):
     """warmup, then exactly `steps` steps between barrier + synchronize; returns wall seconds"""
     for _ in range(a.warmup):
@@ -472,7 +580,7 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     if a.workload != "validate":
-        {"fetch_prm": run_fetch_prm, "pair": run_pair, "capt": run_capt}[a.workload](
+        {"fetch_prm": run_fetch_prm, "prm_edges": run_prm_edges, "pair": run_pair, "capt": run_capt}[a.workload](
             a, torch, dist, rank, world, dev, stream, ctx, vamp)
         if world > 1:
             dist.destroy_process_group()

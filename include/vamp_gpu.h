@@ -189,6 +189,23 @@ int vgpu_prm_neighbor_params(int dim, double space_measure, double gamma_scale, 
  * dist[n][kmax], cnt[n].  dim in {6, 7, 8, 14}, kmax <= 64. */
 int vgpu_roadmap_knn(vgpu_ctx *ctx, int dim, const float *V, size_t n, const uint32_t *k, const float *r,
                      uint32_t kmax, uint32_t *nbr, float *dist, uint32_t *cnt);
+/* The same for the queries q_first .. q_first+q_count-1 only (one rank's share of the edge
+ * stage); nbr/dist/cnt are indexed from q_first, V holds all n vertices. */
+int vgpu_roadmap_knn_range(vgpu_ctx *ctx, int dim, const float *V, size_t n, size_t q_first, size_t q_count,
+                           const uint32_t *k, const float *r, uint32_t kmax, uint32_t *nbr, float *dist,
+                           uint32_t *cnt);
+/* Candidate edges of queries q_first .. +q_count (device): edge off[i] + m = (nbr[i][m] -> vertex
+ * q_first + i) for m < cnt[i], as starts[e][dim] = V[nbr], goals[e][dim] = V[vertex] -- the
+ * arguments of validate_motion(neighbor, vertex) (prm.hh:268). */
+int vgpu_roadmap_edge_gather(vgpu_ctx *ctx, int dim, const float *V, size_t q_first, size_t q_count,
+                             const uint32_t *nbr, uint32_t kmax, const uint32_t *cnt, const uint32_t *off,
+                             float *starts, float *goals);
+/* Host: the adjacency build_roadmap appends (prm.hh:270-275) from the valid (vertex i, neighbour
+ * j) pairs[m][2] listed in query order (i ascending, nearest first): offsets[n+1], adj[2m] (each
+ * vertex: its own neighbours, then the later vertices that connected to it, ascending);
+ * component (optional) = smallest vertex index of each vertex's connected component. */
+int vgpu_roadmap_assemble(size_t n, const uint32_t *pairs, size_t m, size_t *offsets, uint32_t *adj,
+                          uint32_t *component);
 /* Roadmap::build_roadmap's graph for the vertex sequence V[n][dim] (start, goal, then the valid
  * samples in draw order -- vgpu_sample_fkcc + vgpu_compact): every vertex's neighbour query,
  * validate_motion(neighbor, vertex) of every candidate on the GPU, and the adjacency lists in

@@ -1416,12 +1416,12 @@ extern "C" int vgpu_sample_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
 // ---------------------------------------------------------------------------------------
 // PRM roadmap edge stage (planning/prm.hh:235-299; vgpu_roadmap.hip)
 // ---------------------------------------------------------------------------------------
-extern "C" hipError_t vgpu_launch_roadmap_knn(int dim, const float* V, uint32_t n, const uint32_t* k, const float* r,
-                                              uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt,
-                                              hipStream_t st);
-extern "C" hipError_t vgpu_launch_edge_gather(const float* V, uint32_t n, int dim, const uint32_t* nbr, uint32_t kmax,
-                                              const uint32_t* cnt, const uint32_t* off, float* starts, float* goals,
-                                              hipStream_t st);
+extern "C" hipError_t vgpu_launch_roadmap_knn(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
+                                              const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr,
+                                              float* dist, uint32_t* cnt, hipStream_t st);
+extern "C" hipError_t vgpu_launch_edge_gather(const float* V, uint32_t q_first, uint32_t q_count, int dim,
+                                              const uint32_t* nbr, uint32_t kmax, const uint32_t* cnt,
+                                              const uint32_t* off, float* starts, float* goals, hipStream_t st);
 
 // PRMStarNeighborParams (roadmap.hh:42-77) for roadmap sizes 0 .. n-1, in double as the reference
 extern "C" int vgpu_prm_neighbor_params(int dim, double space_measure, double gamma_scale, size_t n, uint32_t* k,
@@ -1451,16 +1451,38 @@ extern "C" int vgpu_prm_neighbor_params(int dim, double space_measure, double ga
 
 static bool knn_dim_ok(int dim) { return dim == 6 || dim == 7 || dim == 8 || dim == 14; }
 
-extern "C" int vgpu_roadmap_knn(vgpu_ctx* c, int dim, const float* V, size_t n, const uint32_t* k, const float* r,
-                                uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt)
+extern "C" int vgpu_roadmap_knn_range(vgpu_ctx* c, int dim, const float* V, size_t n, size_t q_first, size_t q_count,
+                                      const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr, float* dist,
+                                      uint32_t* cnt)
 {
     if (!c) return VGPU_ERR_INVALID_ARG;
+    if (q_first > n || q_count > n - q_first) return fail(c, VGPU_ERR_INVALID_ARG, "query range outside the vertices");
     if (!knn_dim_ok(dim)) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap kNN: dimension 6, 7, 8 or 14");
     if (kmax == 0 || kmax > 64) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap kNN: 1 <= kmax <= 64");
     if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many vertices");
     if (n && (!V || !k || !r || !nbr || !dist || !cnt)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, vgpu_launch_roadmap_knn(dim, V, (uint32_t)n, k, r, kmax, nbr, dist, cnt, c->cur));
+    HIPCHK(c, vgpu_launch_roadmap_knn(dim, V, (uint32_t)n, (uint32_t)q_first, (uint32_t)q_count, k, r, kmax, nbr, dist,
+                                      cnt, c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_roadmap_knn(vgpu_ctx* c, int dim, const float* V, size_t n, const uint32_t* k, const float* r,
+                                uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt)
+{
+    return vgpu_roadmap_knn_range(c, dim, V, n, 0, n, k, r, kmax, nbr, dist, cnt);
+}
+
+extern "C" int vgpu_roadmap_edge_gather(vgpu_ctx* c, int dim, const float* V, size_t q_first, size_t q_count,
+                                        const uint32_t* nbr, uint32_t kmax, const uint32_t* cnt, const uint32_t* off,
+                                        float* starts, float* goals)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (q_count && (!V || !nbr || !cnt || !off || !starts || !goals))
+        return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_launch_edge_gather(V, (uint32_t)q_first, (uint32_t)q_count, dim, nbr, kmax, cnt, off, starts, goals,
+                                      c->cur));
     return VGPU_OK;
 }
 
@@ -1482,6 +1504,42 @@ struct DevBufs {  // call-scoped device allocations
     }
 };
 }  // namespace
+
+// Roadmap adjacency in build_roadmap's append order (prm.hh:270-275): when vertex i is inserted
+// it gets its valid neighbours nearest first and each neighbour j < i gets i appended.  Replaying
+// the valid pairs in query order therefore reproduces every list: a vertex's own neighbours,
+// then the later vertices that connected to it, ascending.  Union-find for the components.
+extern "C" int vgpu_roadmap_assemble(size_t n, const uint32_t* pairs, size_t m, size_t* offsets, uint32_t* adj,
+                                     uint32_t* component)
+{
+    if (!offsets || (m && (!pairs || !adj))) return VGPU_ERR_INVALID_ARG;
+    for (size_t p = 0; p < 2 * m; ++p)
+        if (pairs[p] >= n) return VGPU_ERR_INVALID_ARG;
+    std::vector<size_t> fill(n + 1, 0);
+    for (size_t p = 0; p < 2 * m; ++p) ++fill[pairs[p] + 1];
+    offsets[0] = 0;
+    for (size_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + fill[i + 1];
+    std::copy(offsets, offsets + n, fill.begin());
+    for (size_t p = 0; p < m; ++p) {
+        const uint32_t i = pairs[2 * p], j = pairs[2 * p + 1];
+        adj[fill[i]++] = j;
+        adj[fill[j]++] = i;
+    }
+    if (component) {  // each vertex's component = its smallest vertex index
+        std::vector<uint32_t> parent(n);
+        for (size_t i = 0; i < n; ++i) parent[i] = (uint32_t)i;
+        auto find = [&](uint32_t a) {
+            while (parent[a] != a) a = parent[a] = parent[parent[a]];
+            return a;
+        };
+        for (size_t p = 0; p < m; ++p) {
+            const uint32_t a = find(pairs[2 * p]), b = find(pairs[2 * p + 1]);
+            if (a != b) parent[std::max(a, b)] = std::min(a, b);
+        }
+        for (size_t i = 0; i < n; ++i) component[i] = find((uint32_t)i);
+    }
+    return VGPU_OK;
+}
 
 extern "C" int vgpu_build_roadmap_host(vgpu_ctx* c, const vgpu_robot* robot, vgpu_env* e, const float* V, size_t n,
                                        double space_measure, double gamma_scale, size_t* offsets, uint32_t* adj,
@@ -1537,46 +1595,26 @@ extern "C" int vgpu_build_roadmap_host(vgpu_ctx* c, const vgpu_robot* robot, vgp
         HIPCHK(c, db.get(&dg, E * dim));
         HIPCHK(c, db.get(&dok, E));
         HIPCHK(c, hipMemcpyAsync(doff, off.data(), (n + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, c->cur));
-        HIPCHK(c, vgpu_launch_edge_gather(dV, (uint32_t)n, dim, dn, kmax, dc, doff, ds, dg, c->cur));
+        HIPCHK(c, vgpu_launch_edge_gather(dV, 0, (uint32_t)n, dim, dn, kmax, dc, doff, ds, dg, c->cur));
         // validate_motion(neighbor, vertex) for every candidate (prm.hh:267-276)
         if ((rc = vgpu_validate_motions(c, robot, e, ds, dg, E, dok, nullptr))) return rc;
         HIPCHK(c, hipMemcpyAsync(ok.data(), dok, E, hipMemcpyDeviceToHost, c->cur));
         HIPCHK(c, hipMemcpyAsync(nb.data(), dn, n * (size_t)kmax * sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
         HIPCHK(c, hipStreamSynchronize(c->cur));
     }
-    // adjacency in the reference's append order: vertex i gets its valid neighbours nearest
-    // first when it is inserted, and every neighbour j gets i appended (prm.hh:270-275), so a
-    // vertex's list = its own valid neighbours, then the later vertices that connected to it
-    std::vector<uint32_t> deg(n, 0);
-    for (size_t i = 0; i < n; ++i)
-        for (uint32_t m = 0; m < cnt[i]; ++m)
-            if (ok[off[i] + m]) ++deg[i], ++deg[nb[i * kmax + m]];
-    offsets[0] = 0;
-    for (size_t i = 0; i < n; ++i) offsets[i + 1] = offsets[i] + deg[i];
-    *n_adj = offsets[n];
-    if (offsets[n] > adj_cap || (offsets[n] && !adj))
-        return fail(c, VGPU_ERR_INVALID_ARG, "adjacency capacity too small (*n_adj = required entries)");
-    std::vector<size_t> fill(offsets, offsets + n);
+    // the valid pairs in query order, nearest first
+    std::vector<uint32_t> pairs;
+    pairs.reserve(2 * E);
     for (size_t i = 0; i < n; ++i)
         for (uint32_t m = 0; m < cnt[i]; ++m)
             if (ok[off[i] + m]) {
-                const uint32_t j = nb[i * kmax + m];
-                adj[fill[i]++] = j;
-                adj[fill[j]++] = (uint32_t)i;
+                pairs.push_back((uint32_t)i);
+                pairs.push_back(nb[i * kmax + m]);
             }
-    if (component) {  // union-find: each vertex's component = its smallest vertex index
-        std::vector<uint32_t> parent(n);
-        for (size_t i = 0; i < n; ++i) parent[i] = (uint32_t)i;
-        auto find = [&](uint32_t a) {
-            while (parent[a] != a) a = parent[a] = parent[parent[a]];
-            return a;
-        };
-        for (size_t i = 0; i < n; ++i)
-            for (size_t p = offsets[i]; p < offsets[i + 1]; ++p) {
-                const uint32_t a = find((uint32_t)i), bb = find(adj[p]);
-                if (a != bb) parent[std::max(a, bb)] = std::min(a, bb);
-            }
-        for (size_t i = 0; i < n; ++i) component[i] = find((uint32_t)i);
-    }
+    *n_adj = pairs.size();
+    if (pairs.size() > adj_cap || (!pairs.empty() && !adj))
+        return fail(c, VGPU_ERR_INVALID_ARG, "adjacency capacity too small (*n_adj = required entries)");
+    if ((rc = vgpu_roadmap_assemble(n, pairs.data(), pairs.size() / 2, offsets, adj, component)))
+        return fail(c, rc, "roadmap assembly");
     return VGPU_OK;
 }

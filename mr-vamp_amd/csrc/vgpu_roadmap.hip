@@ -45,8 +45,8 @@ __device__ __forceinline__ float config_distance(const float* a, const float* b)
 }
 
 template <int D, int K>
-__global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict__ V, uint32_t n,
-                                                         const uint32_t* __restrict__ kq,
+__global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict__ V, uint32_t n, uint32_t q_first,
+                                                         uint32_t q_count, const uint32_t* __restrict__ kq,
                                                          const float* __restrict__ rq, uint32_t kmax,
                                                          uint32_t* __restrict__ nbr, float* __restrict__ dist,
                                                          uint32_t* __restrict__ cnt)
@@ -54,13 +54,14 @@ __global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict_
     __shared__ float tile[kKnnBlock * D];
     // heaviest blocks (largest prefixes) first
     const uint32_t blk = gridDim.x - 1 - blockIdx.x;
-    const uint32_t q0 = blk * kKnnBlock;
+    const uint32_t q_end = min(n, q_first + q_count);  // this call's queries: q_first .. q_end-1
+    const uint32_t q0 = q_first + blk * kKnnBlock;
     const uint32_t i = q0 + threadIdx.x;
-    const bool live = i < n && i >= 2;  // vertices 0, 1 (start, goal) query nothing (prm.hh:228-233)
+    const bool live = i < q_end && i >= 2;  // vertices 0, 1 (start, goal) query nothing (prm.hh:228-233)
     float me[D];
 #pragma unroll
-    for (int j = 0; j < D; ++j) me[j] = (i < n) ? V[(size_t)i * D + j] : 0.0f;
-    const uint32_t k = live ? min(kq[i], (uint32_t)K) : 0u;
+    for (int j = 0; j < D; ++j) me[j] = (i < q_end) ? V[(size_t)i * D + j] : 0.0f;
+    const uint32_t k = live ? min(kq[i], (uint32_t)K) : 0u;  // k, r indexed by vertex
     const float r = live ? rq[i] : -1.0f;
     float bd[K];
     uint32_t bi[K];
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict_
     uint32_t c = 0;
     // a candidate must be within r and closer than the current k-th (when k are held)
     float worst = r;
-    const uint32_t last = min(n, q0 + kKnnBlock);  // candidates 0 .. last-2 matter to this block
+    const uint32_t last = min(q_end, q0 + kKnnBlock);  // candidates 0 .. last-2 matter to this block
     for (uint32_t t0 = 0; t0 + 1 < last; t0 += kKnnBlock) {
         __syncthreads();
         for (uint32_t e = threadIdx.x; e < kKnnBlock * D; e += kKnnBlock) {
@@ -112,13 +113,14 @@ __global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict_
             }
         }
     }
-    if (i < n) {
-        cnt[i] = c;
+    if (i < q_end) {  // outputs indexed from q_first
+        const size_t o = i - q_first;
+        cnt[o] = c;
 #pragma unroll
         for (int m = 0; m < K; ++m) {
             if ((uint32_t)m < c) {
-                nbr[(size_t)i * kmax + m] = bi[m];
-                dist[(size_t)i * kmax + m] = bd[m];
+                nbr[o * kmax + m] = bi[m];
+                dist[o * kmax + m] = bd[m];
             }
         }
     }
@@ -126,7 +128,8 @@ __global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict_
 
 // candidate edge e = (query i, its m-th neighbour): starts[e] = V[nbr], goals[e] = V[i]
 // (validate_motion(neighbor.as_vector(), temp, ...), prm.hh:268)
-__global__ __launch_bounds__(256) void edge_gather_kernel(const float* __restrict__ V, uint32_t n, int dim,
+__global__ __launch_bounds__(256) void edge_gather_kernel(const float* __restrict__ V, uint32_t q_first, uint32_t n,
+                                                          int dim,
                                                           const uint32_t* __restrict__ nbr, uint32_t kmax,
                                                           const uint32_t* __restrict__ cnt,
                                                           const uint32_t* __restrict__ off,
@@ -138,62 +141,64 @@ __global__ __launch_bounds__(256) void edge_gather_kernel(const float* __restric
     if (i >= n || m >= cnt[i]) return;
     const size_t e = (size_t)off[i] + m;
     const uint32_t j = nbr[i * kmax + m];
+    const size_t v = q_first + i;  // query vertex
     for (int d = 0; d < dim; ++d) {
         starts[e * dim + d] = V[(size_t)j * dim + d];
-        goals[e * dim + d] = V[i * dim + d];
+        goals[e * dim + d] = V[v * dim + d];
     }
 }
 
 }  // namespace vgpu
 
 template <int D, int K>
-static void launch_knn(const float* V, uint32_t n, const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr,
-                       float* dist, uint32_t* cnt, hipStream_t st)
+static void launch_knn(const float* V, uint32_t n, uint32_t qf, uint32_t qc, const uint32_t* k, const float* r,
+                       uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, hipStream_t st)
 {
-    const unsigned grid = (n + vgpu::kKnnBlock - 1) / vgpu::kKnnBlock;
-    hipLaunchKernelGGL((vgpu::knn_kernel<D, K>), dim3(grid), dim3(vgpu::kKnnBlock), 0, st, V, n, k, r, kmax, nbr,
-                       dist, cnt);
+    const unsigned grid = (qc + vgpu::kKnnBlock - 1) / vgpu::kKnnBlock;
+    hipLaunchKernelGGL((vgpu::knn_kernel<D, K>), dim3(grid), dim3(vgpu::kKnnBlock), 0, st, V, n, qf, qc, k, r, kmax,
+                       nbr, dist, cnt);
 }
 
 template <int D>
-static hipError_t knn_dim(const float* V, uint32_t n, const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr,
-                          float* dist, uint32_t* cnt, hipStream_t st)
+static hipError_t knn_dim(const float* V, uint32_t n, uint32_t qf, uint32_t qc, const uint32_t* k, const float* r,
+                          uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, hipStream_t st)
 {
     if (kmax <= 16)
-        launch_knn<D, 16>(V, n, k, r, kmax, nbr, dist, cnt, st);
+        launch_knn<D, 16>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, st);
     else if (kmax <= 32)
-        launch_knn<D, 32>(V, n, k, r, kmax, nbr, dist, cnt, st);
+        launch_knn<D, 32>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, st);
     else if (kmax <= 48)
-        launch_knn<D, 48>(V, n, k, r, kmax, nbr, dist, cnt, st);
+        launch_knn<D, 48>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, st);
     else
-        launch_knn<D, 64>(V, n, k, r, kmax, nbr, dist, cnt, st);
+        launch_knn<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, st);
     return hipGetLastError();
 }
 
 extern "C" {
 
 // kmax <= 64 and dim in {6, 7, 8, 14} (the robots built here) are checked by the caller
-hipError_t vgpu_launch_roadmap_knn(int dim, const float* V, uint32_t n, const uint32_t* k, const float* r,
-                                   uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, hipStream_t st)
+hipError_t vgpu_launch_roadmap_knn(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
+                                   const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr, float* dist,
+                                   uint32_t* cnt, hipStream_t st)
 {
-    if (n == 0) return hipSuccess;
+    if (q_count == 0) return hipSuccess;
     switch (dim) {
-    case 6: return knn_dim<6>(V, n, k, r, kmax, nbr, dist, cnt, st);
-    case 7: return knn_dim<7>(V, n, k, r, kmax, nbr, dist, cnt, st);
-    case 8: return knn_dim<8>(V, n, k, r, kmax, nbr, dist, cnt, st);
-    case 14: return knn_dim<14>(V, n, k, r, kmax, nbr, dist, cnt, st);
+    case 6: return knn_dim<6>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, st);
+    case 7: return knn_dim<7>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, st);
+    case 8: return knn_dim<8>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, st);
+    case 14: return knn_dim<14>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, st);
     default: return hipErrorInvalidValue;
     }
 }
 
-hipError_t vgpu_launch_edge_gather(const float* V, uint32_t n, int dim, const uint32_t* nbr, uint32_t kmax,
-                                   const uint32_t* cnt, const uint32_t* off, float* starts, float* goals,
-                                   hipStream_t st)
+hipError_t vgpu_launch_edge_gather(const float* V, uint32_t q_first, uint32_t q_count, int dim, const uint32_t* nbr,
+                                   uint32_t kmax, const uint32_t* cnt, const uint32_t* off, float* starts,
+                                   float* goals, hipStream_t st)
 {
-    const size_t threads = (size_t)n * kmax;
+    const size_t threads = (size_t)q_count * kmax;
     if (threads == 0) return hipSuccess;
-    hipLaunchKernelGGL(vgpu::edge_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, V, n, dim,
-                       nbr, kmax, cnt, off, starts, goals);
+    hipLaunchKernelGGL(vgpu::edge_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, V, q_first,
+                       q_count, dim, nbr, kmax, cnt, off, starts, goals);
     return hipGetLastError();
 }
 

@@ -80,6 +80,11 @@ SIGNATURES = {
     "vgpu_robot_info": (C.c_int, [C.c_int32, I32P, I32P, I32P]),
     "vgpu_prm_neighbor_params": (C.c_int, [C.c_int, C.c_double, C.c_double, C.c_size_t, U32P, F32P]),
     "vgpu_roadmap_knn": (C.c_int, [VP, C.c_int, VP, C.c_size_t, VP, VP, C.c_uint32, VP, VP, VP]),
+    "vgpu_roadmap_knn_range": (C.c_int, [VP, C.c_int, VP, C.c_size_t, C.c_size_t, C.c_size_t, VP, VP, C.c_uint32,
+                                         VP, VP, VP]),
+    "vgpu_roadmap_edge_gather": (C.c_int, [VP, C.c_int, VP, C.c_size_t, C.c_size_t, VP, C.c_uint32, VP, VP, VP,
+                                           VP]),
+    "vgpu_roadmap_assemble": (C.c_int, [C.c_size_t, U32P, C.c_size_t, C.POINTER(C.c_size_t), U32P, U32P]),
     "vgpu_build_roadmap_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, C.c_double, C.c_double,
                                           C.POINTER(C.c_size_t), U32P, C.c_size_t, C.POINTER(C.c_size_t), U32P]),
 }

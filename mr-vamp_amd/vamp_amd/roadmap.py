@@ -177,3 +177,108 @@ def build_roadmap(robot, start, goal, environment, max_iterations: int = 100000,
     stage sharded over ranks when torch.distributed is initialised), then the edge stage."""
     rows, _ = roadmap_vertices(robot, environment, max_iterations, 1, start, goal, max_samples, ctx, group)
     return build_roadmap_edges(robot, environment, rows.cpu().numpy(), gamma_scale, None, ctx)
+
+
+# ---- the edge stage sharded over ranks (every rank holds all vertices after the all-gather) ----
+def query_split(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """(first, count) of this rank's queries: contiguous ranges with equal sum of prefix lengths
+    (query i scans i candidates), boundaries at n * sqrt(r / world)."""
+    b = [0] + [min(n, int(round(n * (r / world) ** 0.5))) for r in range(1, world)] + [n]
+    return b[rank], b[rank + 1] - b[rank]
+
+
+def edges_shard(torch, robot, environment, V, k, r, kmax: int, q_first: int, q_count: int, ctx):
+    """This rank's share of build_roadmap's edge stage on the GPU: neighbour queries of vertices
+    q_first .. q_first+q_count-1, then validate_motion(neighbor, vertex) of their candidates.
+    V [n, dim], k [n], r [n] are device tensors (all vertices).  Returns the valid (vertex,
+    neighbour) pairs in query order, nearest first: int64 tensor [m, 2]."""
+    from ._lib import check, load
+    dev = V.device
+    n, dim = V.shape
+    nbr = torch.empty((max(q_count, 1), kmax), dtype=torch.int32, device=dev)
+    dist_ = torch.empty((max(q_count, 1), kmax), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(max(q_count, 1), dtype=torch.int32, device=dev)
+    if q_count == 0:
+        return torch.zeros((0, 2), dtype=torch.int64, device=dev)
+    check(load().vgpu_roadmap_knn_range(ctx.h, dim, V.data_ptr(), n, q_first, q_count, k.data_ptr(), r.data_ptr(),
+                                        kmax, nbr.data_ptr(), dist_.data_ptr(), cnt.data_ptr()), ctx.h)
+    cnt = cnt[:q_count]
+    off = torch.zeros(q_count + 1, dtype=torch.int32, device=dev)
+    off[1:] = torch.cumsum(cnt, 0)
+    E = int(off[-1])
+    if E == 0:
+        return torch.zeros((0, 2), dtype=torch.int64, device=dev)
+    starts = torch.empty((E, dim), dtype=torch.float32, device=dev)
+    goals = torch.empty_like(starts)
+    check(load().vgpu_roadmap_edge_gather(ctx.h, dim, V.data_ptr(), q_first, q_count, nbr.data_ptr(), kmax,
+                                          cnt.data_ptr(), off.data_ptr(), starts.data_ptr(), goals.data_ptr()), ctx.h)
+    ok = torch.empty(E, dtype=torch.uint8, device=dev)
+    robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, environment, ok.data_ptr(), ctx=ctx)
+    qi = torch.repeat_interleave(torch.arange(q_first, q_first + q_count, device=dev), cnt.long())
+    m = torch.arange(E, device=dev) - off[:-1].long().repeat_interleave(cnt.long())
+    qj = nbr[:q_count].long()[qi - q_first, m]
+    keep = ok.bool()
+    return torch.stack([qi[keep], qj[keep]], 1)
+
+
+def allgather_pairs(torch, dist, pairs, group=None):
+    """Concatenate the ranks' valid pairs in rank order (= query order): counts, then count-padded
+    pairs, one all_gather_into_tensor each (RCCL on CUDA tensors, gloo on CPU tensors)."""
+    world = dist.get_world_size(group)
+    dev = pairs.device
+    cnt = torch.tensor([pairs.shape[0]], dtype=torch.int64, device=dev)
+    cnts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(cnts, cnt, group=group)
+    counts = [int(c) for c in cnts.tolist()]
+    mx = max(counts)
+    send = torch.zeros((mx, 2), dtype=torch.int64, device=dev)
+    send[:pairs.shape[0]] = pairs
+    recv = torch.empty((world * mx, 2), dtype=torch.int64, device=dev)
+    if mx:
+        dist.all_gather_into_tensor(recv, send, group=group)
+    return torch.cat([recv[r * mx:r * mx + c] for r, c in enumerate(counts)])
+
+
+def assemble(n: int, pairs: np.ndarray):
+    """Adjacency in build_roadmap's append order from the valid (vertex i, neighbour j) pairs
+    listed in query order (i ascending, nearest first): vertex v's list = its own pairs' j, then
+    every later i whose pair names v, ascending (prm.hh:270-275).  Host C++ (vgpu_roadmap_assemble).
+    Returns (offsets [n+1], adj, component [n] = smallest vertex index of each vertex's
+    connected component)."""
+    import ctypes as C
+
+    from . import _lib
+    from ._lib import check, load
+    p = np.ascontiguousarray(np.asarray(pairs).reshape(-1, 2), np.uint32)
+    offsets = np.zeros(n + 1, np.uint64)
+    adj = np.zeros(max(2 * len(p), 1), np.uint32)
+    comp = np.zeros(max(n, 1), np.uint32)
+    check(load().vgpu_roadmap_assemble(n, p.ctypes.data_as(_lib.U32P), len(p),
+                                       offsets.ctypes.data_as(C.POINTER(C.c_size_t)), adj.ctypes.data_as(_lib.U32P),
+                                       comp.ctypes.data_as(_lib.U32P)))
+    return offsets.astype(np.int64), adj[:2 * len(p)], comp[:n]
+
+
+def build_roadmap_edges_sharded(torch, dist, robot, environment, V, gamma_scale: float = 2.0, ctx=None,
+                                group=None) -> Roadmap:
+    """The edge stage with the queries split over the ranks (query_split), each rank validating its
+    own candidates on its GPU, then one exchange of the valid pairs; every rank returns the whole
+    graph.  V: [n, dim] tensor on this rank's device, identical on all ranks."""
+    from . import context
+    ctx = ctx or context()
+    dev = V.device
+    if dev.type == "cuda":  # the kernels run on the context stream: make it torch's
+        ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    n, dim = V.shape
+    k_np, r_np = prm_neighbor_params(dim, robot.space_measure(), n, gamma_scale)
+    kmax = int(max(1, min(int(k_np.max()) if n else 1, n)))
+    k = torch.from_numpy(k_np.view(np.int32)).to(dev)
+    r = torch.from_numpy(r_np).to(dev)
+    sharded = dist is not None and dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1
+    rank, world = (dist.get_rank(group), dist.get_world_size(group)) if sharded else (0, 1)
+    qf, qc = query_split(n, rank, world)
+    pairs = edges_shard(torch, robot, environment, V, k, r, kmax, qf, qc, ctx)
+    if sharded:
+        pairs = allgather_pairs(torch, dist, pairs, group)
+    offsets, adj, comp = assemble(n, pairs.cpu().numpy())
+    return Roadmap(V.cpu().numpy(), offsets, adj, comp)

@@ -91,3 +91,18 @@ def test_build_roadmap_end_to_end(vamp, oracle):
     assert np.array_equal(V, want)
     edges, _ = oracle.build_roadmap_edges("panda", oenv, V)
     assert rm.edges == edges
+
+
+def test_sharded_edges_single_process_equals_oracle(vamp, oracle):
+    """build_roadmap_edges_sharded (queries -> device pairs -> assemble) at world size 1."""
+    import torch
+    from vamp_amd import roadmap
+    rng = np.random.default_rng(23)
+    oenv = random_scene(oracle, rng, 4, 4, 2)
+    env = gpu_env_from_oracle(vamp, oenv)
+    q = oracle.robot_scale("fetch", rng.random((5000, 8), dtype=F))
+    V = q[oracle.robot_fkcc_threads("fetch", oenv, q)][:2000]
+    rm = roadmap.build_roadmap_edges_sharded(torch, None, vamp.fetch, env, torch.from_numpy(V).cuda())
+    edges, _ = oracle.build_roadmap_edges("fetch", oenv, V)
+    assert rm.edges == edges
+    assert np.array_equal(rm.component, oracle.components(len(V), edges))
