@@ -217,6 +217,9 @@ struct vgpu_ctx {
     uint32_t* st_host = nullptr;  // pinned: the 33 segment boundaries of the scan
     uint32_t* st_items = nullptr;
     size_t st_items_cap = 0;
+    // roadmap kNN chunk lists (vgpu_roadmap.hip)
+    uint32_t* knn_part = nullptr;
+    size_t knn_part_cap = 0;
     // optional phase timing
     bool prof = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -316,6 +319,7 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->st_q) (void)hipFree(c->st_q);
     if (c->st_cnt) (void)hipFree(c->st_cnt);
     if (c->st_items) (void)hipFree(c->st_items);
+    if (c->knn_part) (void)hipFree(c->knn_part);
     if (c->st_host) (void)hipHostFree(c->st_host);
     if (c->total_host) (void)hipHostFree(c->total_host);
     for (auto& ev : c->ev)
@@ -1416,8 +1420,10 @@ extern "C" int vgpu_sample_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
 // ---------------------------------------------------------------------------------------
 // PRM roadmap edge stage (planning/prm.hh:235-299; vgpu_roadmap.hip)
 // ---------------------------------------------------------------------------------------
+extern "C" size_t vgpu_knn_chunks(size_t n, uint32_t* S);
 extern "C" hipError_t vgpu_launch_roadmap_knn(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
-                                              const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr,
+                                              const uint32_t* k, const float* r, uint32_t kmax, uint32_t S,
+                                              uint32_t C, float* pd, uint32_t* pi, uint32_t* pc, uint32_t* nbr,
                                               float* dist, uint32_t* cnt, hipStream_t st);
 extern "C" hipError_t vgpu_launch_edge_gather(const float* V, uint32_t q_first, uint32_t q_count, int dim,
                                               const uint32_t* nbr, uint32_t kmax, const uint32_t* cnt,
@@ -1462,8 +1468,18 @@ extern "C" int vgpu_roadmap_knn_range(vgpu_ctx* c, int dim, const float* V, size
     if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many vertices");
     if (n && (!V || !k || !r || !nbr || !dist || !cnt)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, vgpu_launch_roadmap_knn(dim, V, (uint32_t)n, (uint32_t)q_first, (uint32_t)q_count, k, r, kmax, nbr, dist,
-                                      cnt, c->cur));
+    if (q_count == 0) return VGPU_OK;
+    uint32_t S = 0;
+    const size_t C = vgpu_knn_chunks(n, &S);
+    // chunk lists (context-owned, grown on demand): distances, indices, counts
+    const size_t cells = q_count * C, need = cells * (2 * (size_t)kmax + 1);
+    int rc;
+    if ((rc = grow(c, &c->knn_part, &c->knn_part_cap, need))) return rc;
+    float* pd = (float*)c->knn_part;
+    uint32_t* pi = c->knn_part + cells * kmax;
+    uint32_t* pc = c->knn_part + 2 * cells * kmax;
+    HIPCHK(c, vgpu_launch_roadmap_knn(dim, V, (uint32_t)n, (uint32_t)q_first, (uint32_t)q_count, k, r, kmax, S,
+                                      (uint32_t)C, pd, pi, pc, nbr, dist, cnt, c->cur));
     return VGPU_OK;
 }
 

@@ -7,24 +7,30 @@
 // (roadmap.hh:49-67).  The query set never depends on which edges were valid, so the queries of
 // all vertices are independent: "causal" kNN, vertex i against its prefix.
 //
-// knn_kernel: one lane per query vertex, 256 queries per block; the candidate prefix streams
-// through LDS in tiles of 256 rows (every lane reads the same row: LDS broadcast).  Each lane
-// keeps its K best (distance, index) pairs sorted in registers; a candidate enters by one
-// unrolled compare-exchange pass (no dynamic register indexing), executed only when some lane
-// of the wave has a candidate closer than its current K-th (order = (distance, index), so
-// ties keep the lower index first).  Distance = Space<dim>::distance
-// (nn.hh:53-57): the lane-wise difference's l2_norm in the AVX hsum order (pinned by ref_probe
-// "l2norm").  Ties keep the lower index first (nigh's tie order is not pinned: DESIGN.md).
+// knn_kernel: one lane per query vertex, 256 queries per block, and the candidate prefix split
+// into chunks along grid y (the work of query i grows with i: without the split a few blocks
+// scan 1e5 candidates serially).  Candidates stream through LDS in tiles of 256 rows (every lane
+// reads the same row: LDS broadcast).  Each lane keeps its K best (distance, index) keys sorted in
+// registers; a candidate enters by one unrolled compare-exchange pass (no dynamic register
+// indexing), run only when some lane of the wave takes a candidate; the correctly rounded sqrt
+// runs only when some lane's squared sum is below its bound.  knn_merge_kernel combines a
+// query's chunk lists into the k smallest keys.  Distance = Space<dim>::distance (nn.hh:53-57):
+// the lane-wise difference's l2_norm in the AVX hsum order (pinned by ref_probe "l2norm").  Ties
+// keep the lower index first (nigh's tie order is not pinned: DESIGN.md).
+#include <algorithm>
+
 #include "vgpu_device.hh"
 
 namespace vgpu {
 
 constexpr int kKnnBlock = 256;
+constexpr int kKnnBuf = 8;  // buffered candidates per lane between insertion passes
 
 // FloatVector<D>::l2_norm of a - b (vector/avx.hh:441-452; two registers contract to
-// fma(lo, lo, hi * hi), pinned by ref_probe "l2norm")
+// fma(lo, lo, hi * hi), pinned by ref_probe "l2norm") before its sqrt: the squared sum in the
+// AVX hsum lane order
 template <int D>
-__device__ __forceinline__ float config_distance(const float* a, const float* b)
+__device__ __forceinline__ float config_sumsq(const float* a, const float* b)
 {
     float v[D];
 #pragma unroll
@@ -40,23 +46,55 @@ __device__ __forceinline__ float config_distance(const float* a, const float* b)
             sq[j] = __builtin_fmaf(lo, lo, hi * hi);
         }
     }
-    const float s = ((sq[0] + sq[4]) + (sq[2] + sq[6])) + ((sq[1] + sq[5]) + (sq[3] + sq[7]));
-    return __builtin_sqrtf(s);
+    return ((sq[0] + sq[4]) + (sq[2] + sq[6])) + ((sq[1] + sq[5]) + (sq[3] + sq[7]));
 }
 
+// Insert (cd, ci) into the register list (bd, bi) of K entries sorted by the key (distance,
+// index), by one unrolled compare-exchange pass: the carried element displaced from an earlier
+// slot passes equal distances with larger indices.  No dynamic register indexing.
+template <int K>
+__device__ __forceinline__ void list_insert(float (&bd)[K], uint32_t (&bi)[K], float cd, uint32_t ci)
+{
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        const bool lt = cd < bd[m] || (cd == bd[m] && ci < bi[m]);
+        const float td = bd[m];
+        const uint32_t ti = bi[m];
+        bd[m] = lt ? cd : td;
+        bi[m] = lt ? ci : ti;
+        cd = lt ? td : cd;
+        ci = lt ? ti : ci;
+    }
+}
+
+// Partial queries: block (x, y) = queries q0 .. q0+255 against the candidate chunk
+// [y * S, (y + 1) * S) of their prefixes; each query's chunk list = its k smallest keys
+// (distance, index) with distance <= r within the chunk.  The exact result is the k smallest keys
+// over all chunks (knn_merge_kernel): the same set and order as one sequential scan.
 template <int D, int K>
 __global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict__ V, uint32_t n, uint32_t q_first,
                                                          uint32_t q_count, const uint32_t* __restrict__ kq,
-                                                         const float* __restrict__ rq, uint32_t kmax,
-                                                         uint32_t* __restrict__ nbr, float* __restrict__ dist,
-                                                         uint32_t* __restrict__ cnt)
+                                                         const float* __restrict__ rq, uint32_t kmax, uint32_t S,
+                                                         uint32_t C, float* __restrict__ pd,
+                                                         uint32_t* __restrict__ pi, uint32_t* __restrict__ pc)
 {
     __shared__ float tile[kKnnBlock * D];
-    // heaviest blocks (largest prefixes) first
+    // per-lane buffers of taken candidates: inserted into the register lists in batches, so the
+    // wave runs the K-slot insertion pass max-over-lanes times per batch instead of once for
+    // every candidate some lane takes
+    __shared__ float buf_d[kKnnBuf][kKnnBlock];
+    __shared__ uint32_t buf_i[kKnnBuf][kKnnBlock];
+    // heaviest query blocks (largest prefixes) first
     const uint32_t blk = gridDim.x - 1 - blockIdx.x;
+    const uint32_t chunk = blockIdx.y;
     const uint32_t q_end = min(n, q_first + q_count);  // this call's queries: q_first .. q_end-1
     const uint32_t q0 = q_first + blk * kKnnBlock;
-    const uint32_t i = q0 + threadIdx.x;
+    const uint32_t last = min(q_end, q0 + kKnnBlock);  // candidates 0 .. last-2 matter to this block
+    const uint32_t c_lo = chunk * S;
+    if (c_lo + 1 >= last) return;  // no query of the block reaches this chunk (the merge skips it)
+    const uint32_t c_hi = min(c_lo + S, last - 1);
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = q0 + lane;
     const bool live = i < q_end && i >= 2;  // vertices 0, 1 (start, goal) query nothing (prm.hh:228-233)
     float me[D];
 #pragma unroll
@@ -70,58 +108,102 @@ __global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict_
         bd[m] = __builtin_inff();
         bi[m] = 0xFFFFFFFFu;
     }
-    uint32_t c = 0;
-    // a candidate must be within r and closer than the current k-th (when k are held)
+    uint32_t c = 0, nb = 0;
+    // a candidate must be within r and closer than the current k-th (when k are held); thr is a
+    // bound on the squared distance below which sqrt_rn(s) <= worst is possible (w^2 (1 + 2^-20)
+    // > (w + ulp(w)/2)^2), so the correctly rounded sqrt runs only for plausible candidates.
+    // worst may be stale while candidates wait in the buffer: it only admits more of them, and
+    // the list keeps the K smallest keys of everything inserted.
     float worst = r;
-    const uint32_t last = min(q_end, q0 + kKnnBlock);  // candidates 0 .. last-2 matter to this block
-    for (uint32_t t0 = 0; t0 + 1 < last; t0 += kKnnBlock) {
+    float thr = live ? r * r * 1.000001f : -1.0f;
+    auto flush = [&]() {
+        for (uint32_t m = 0; __builtin_amdgcn_ballot_w64(m < nb) != 0ull; ++m) {
+            const bool has = m < nb;
+            list_insert<K>(bd, bi, has ? buf_d[has ? m : 0][lane] : __builtin_inff(),
+                           has ? buf_i[has ? m : 0][lane] : 0xFFFFFFFFu);
+        }
+        c = min(c + nb, k);  // every buffered candidate is within r
+        nb = 0;
+        float kth = r;
+#pragma unroll
+        for (int m = 0; m < K; ++m)
+            if ((uint32_t)m + 1 == k) kth = bd[m];
+        worst = (c == k) ? kth : r;
+        thr = live ? worst * worst * 1.000001f : -1.0f;
+    };
+    for (uint32_t t0 = c_lo; t0 < c_hi; t0 += kKnnBlock) {
         __syncthreads();
         for (uint32_t e = threadIdx.x; e < kKnnBlock * D; e += kKnnBlock) {
             const size_t g = (size_t)t0 * D + e;
             tile[e] = (g < (size_t)n * D) ? V[g] : 0.0f;
         }
         __syncthreads();
-        const uint32_t tn = min((uint32_t)kKnnBlock, last - 1 - t0);
+        const uint32_t tn = min((uint32_t)kKnnBlock, c_hi - t0);
         for (uint32_t u = 0; u < tn; ++u) {
             const uint32_t j = t0 + u;
-            const float d = config_distance<D>(tile + u * D, me);
+            const float s = config_sumsq<D>(tile + u * D, me);
+            const bool pre = j < i && s <= thr;
+            if (__builtin_amdgcn_ballot_w64(pre) == 0ull) continue;
+            const float d = __builtin_sqrtf(s);
             // nn query semantics: distance <= r, strictly closer than the k-th to displace it
-            const bool take = live && j < i && (c < k ? d <= worst : d < worst);
-            if (__builtin_amdgcn_ballot_w64(take) == 0ull) continue;
-            float cd = take ? d : __builtin_inff();
-            uint32_t ci = take ? j : 0xFFFFFFFFu;
-#pragma unroll
-            for (int m = 0; m < K; ++m) {
-                // insertion by compare-exchange on the key (distance, index): the carried element
-                // displaced from an earlier slot must pass equal distances with larger indices
-                const bool lt = cd < bd[m] || (cd == bd[m] && ci < bi[m]);
-                const float td = bd[m];
-                const uint32_t ti = bi[m];
-                bd[m] = lt ? cd : td;
-                bi[m] = lt ? ci : ti;
-                cd = lt ? td : cd;
-                ci = lt ? ti : ci;
-            }
+            const bool take = pre && (c < k ? d <= worst : d < worst);
             if (take) {
-                c = c < k ? c + 1 : c;
-                // worst = the k-th distance once k are held (bd[k-1]), else r
-                float kth = r;
-#pragma unroll
-                for (int m = 0; m < K; ++m)
-                    if ((uint32_t)m + 1 == k) kth = bd[m];
-                worst = (c == k) ? kth : r;
+                buf_d[nb][lane] = d;
+                buf_i[nb][lane] = j;
+                ++nb;
             }
+            if (__builtin_amdgcn_ballot_w64(nb == kKnnBuf) != 0ull) flush();
         }
+        if (__builtin_amdgcn_ballot_w64(nb != 0) != 0ull) flush();
     }
-    if (i < q_end) {  // outputs indexed from q_first
-        const size_t o = i - q_first;
-        cnt[o] = c;
+    if (i < q_end) {
+        const size_t o = ((size_t)(i - q_first) * C + chunk);
+        pc[o] = c;
 #pragma unroll
         for (int m = 0; m < K; ++m) {
             if ((uint32_t)m < c) {
-                nbr[o * kmax + m] = bi[m];
-                dist[o * kmax + m] = bd[m];
+                pd[o * kmax + m] = bd[m];
+                pi[o * kmax + m] = bi[m];
             }
+        }
+    }
+}
+
+// Final lists: the k smallest keys over the chunk lists of query i (chunks c with c * S < i)
+template <int K>
+__global__ __launch_bounds__(256) void knn_merge_kernel(uint32_t n, uint32_t q_first, uint32_t q_count,
+                                                         const uint32_t* __restrict__ kq, uint32_t kmax, uint32_t S,
+                                                         uint32_t C, const float* __restrict__ pd,
+                                                         const uint32_t* __restrict__ pi,
+                                                         const uint32_t* __restrict__ pc, uint32_t* __restrict__ nbr,
+                                                         float* __restrict__ dist, uint32_t* __restrict__ cnt)
+{
+    const uint32_t o = blockIdx.x * 256 + threadIdx.x;
+    if (o >= q_count) return;
+    const uint32_t i = q_first + o;
+    const uint32_t k = i >= 2 ? min(kq[i], (uint32_t)K) : 0u;
+    float bd[K];
+    uint32_t bi[K];
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        bd[m] = __builtin_inff();
+        bi[m] = 0xFFFFFFFFu;
+    }
+    uint32_t total = 0;
+    const uint32_t nch = k ? min(C, (i + S - 1) / S) : 0u;
+    for (uint32_t ch = 0; ch < nch; ++ch) {
+        const size_t b = (size_t)o * C + ch;
+        const uint32_t pn = pc[b];
+        total += pn;
+        for (uint32_t m = 0; m < pn; ++m) list_insert<K>(bd, bi, pd[b * kmax + m], pi[b * kmax + m]);
+    }
+    const uint32_t c = min(total, k);
+    cnt[o] = c;
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        if ((uint32_t)m < c) {
+            nbr[(size_t)o * kmax + m] = bi[m];
+            dist[(size_t)o * kmax + m] = bd[m];
         }
     }
 }
@@ -151,42 +233,55 @@ __global__ __launch_bounds__(256) void edge_gather_kernel(const float* __restric
 }  // namespace vgpu
 
 template <int D, int K>
-static void launch_knn(const float* V, uint32_t n, uint32_t qf, uint32_t qc, const uint32_t* k, const float* r,
-                       uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, hipStream_t st)
+static hipError_t launch_knn(const float* V, uint32_t n, uint32_t qf, uint32_t qc, const uint32_t* k, const float* r,
+                             uint32_t kmax, uint32_t S, uint32_t C, float* pd, uint32_t* pi, uint32_t* pc,
+                             uint32_t* nbr, float* dist, uint32_t* cnt, hipStream_t st)
 {
-    const unsigned grid = (qc + vgpu::kKnnBlock - 1) / vgpu::kKnnBlock;
-    hipLaunchKernelGGL((vgpu::knn_kernel<D, K>), dim3(grid), dim3(vgpu::kKnnBlock), 0, st, V, n, qf, qc, k, r, kmax,
-                       nbr, dist, cnt);
+    const unsigned qb = (qc + vgpu::kKnnBlock - 1) / vgpu::kKnnBlock;
+    hipLaunchKernelGGL((vgpu::knn_kernel<D, K>), dim3(qb, C), dim3(vgpu::kKnnBlock), 0, st, V, n, qf, qc, k, r, kmax,
+                       S, C, pd, pi, pc);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((vgpu::knn_merge_kernel<K>), dim3((qc + 255) / 256), dim3(256), 0, st, n, qf, qc, k, kmax, S, C,
+                       pd, pi, pc, nbr, dist, cnt);
+    return hipGetLastError();
 }
 
 template <int D>
 static hipError_t knn_dim(const float* V, uint32_t n, uint32_t qf, uint32_t qc, const uint32_t* k, const float* r,
-                          uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, hipStream_t st)
+                          uint32_t kmax, uint32_t S, uint32_t C, float* pd, uint32_t* pi, uint32_t* pc, uint32_t* nbr,
+                          float* dist, uint32_t* cnt, hipStream_t st)
 {
-    if (kmax <= 16)
-        launch_knn<D, 16>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, st);
-    else if (kmax <= 32)
-        launch_knn<D, 32>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, st);
-    else if (kmax <= 48)
-        launch_knn<D, 48>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, st);
-    else
-        launch_knn<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, st);
-    return hipGetLastError();
+    if (kmax <= 16) return launch_knn<D, 16>(V, n, qf, qc, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
+    if (kmax <= 32) return launch_knn<D, 32>(V, n, qf, qc, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
+    if (kmax <= 40) return launch_knn<D, 40>(V, n, qf, qc, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
+    if (kmax <= 48) return launch_knn<D, 48>(V, n, qf, qc, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
+    return launch_knn<D, 64>(V, n, qf, qc, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
 }
 
 extern "C" {
 
+// Chunking of the candidate prefixes: S candidates per chunk (a multiple of the block), at most
+// 4 chunks; the partial lists need q_count * C * kmax (float + u32) + q_count * C u32.
+size_t vgpu_knn_chunks(size_t n, uint32_t* S)
+{
+    const size_t s = std::max<size_t>(8192, (n + 3) / 4);
+    *S = (uint32_t)((s + vgpu::kKnnBlock - 1) / vgpu::kKnnBlock * vgpu::kKnnBlock);
+    return std::max<size_t>(1, (n + *S - 1) / *S);
+}
+
 // kmax <= 64 and dim in {6, 7, 8, 14} (the robots built here) are checked by the caller
 hipError_t vgpu_launch_roadmap_knn(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
-                                   const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr, float* dist,
-                                   uint32_t* cnt, hipStream_t st)
+                                   const uint32_t* k, const float* r, uint32_t kmax, uint32_t S, uint32_t C, float* pd,
+                                   uint32_t* pi, uint32_t* pc, uint32_t* nbr, float* dist, uint32_t* cnt,
+                                   hipStream_t st)
 {
     if (q_count == 0) return hipSuccess;
     switch (dim) {
-    case 6: return knn_dim<6>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, st);
-    case 7: return knn_dim<7>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, st);
-    case 8: return knn_dim<8>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, st);
-    case 14: return knn_dim<14>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, st);
+    case 6: return knn_dim<6>(V, n, q_first, q_count, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
+    case 7: return knn_dim<7>(V, n, q_first, q_count, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
+    case 8: return knn_dim<8>(V, n, q_first, q_count, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
+    case 14: return knn_dim<14>(V, n, q_first, q_count, k, r, kmax, S, C, pd, pi, pc, nbr, dist, cnt, st);
     default: return hipErrorInvalidValue;
     }
 }
