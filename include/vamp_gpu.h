@@ -122,8 +122,9 @@ int vgpu_env_pointcloud_arrays(const vgpu_env *env, int index, float *tests, flo
  * any previous one.  tf = relative frame x y z, quaternion x y z w (Attachment(center,
  * quaternion_xyzw), environment.cc:197-215); spheres[n][4] = x y z r relative to it
  * (Attachment::add_spheres, :226-233).  validate_motions then checks the first rake block
- * through Robot::fkcc_attach (planning/validate.hh:43).  Panda only (VGPU_ERR_UNSUPPORTED at
- * validation time for other robots). */
+ * through Robot::fkcc_attach (planning/validate.hh:43): Panda, Fetch and UR5 have generated
+ * attachment checks; the Baxter's fkcc_attach is its plain fkcc (baxter.hh:44); the composite
+ * has none (VGPU_ERR_UNSUPPORTED). */
 int vgpu_env_attach(vgpu_env *env, const float tf[7], const float *spheres, size_t n);
 /* Environment::detach (environment.cc:163) */
 int vgpu_env_detach(vgpu_env *env);
@@ -138,9 +139,9 @@ int vgpu_sphere_fk(vgpu_ctx *ctx, const vgpu_robot *robot, const float *q, size_
 /* Robot::fkcc<rake> of each configuration broadcast to the whole rake (the per-configuration
  * mask, as used by validate(q) and the PRM sampler): valid[i] = 1 if q[i] is collision-free. */
 int vgpu_fkcc(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n, uint8_t *valid);
-/* Robot::fkcc_attach<rake> (robots/panda_base.hh:61-65, panda/fk.hh:6278-11397) of each
+/* Robot::fkcc_attach<rake> (robots/panda_base.hh:61-65, fetch.hh:42, ur5.hh:43) of each
  * configuration broadcast to the rake, with the environment's attachment posed at the end
- * effector; requires an attachment (vgpu_env_attach).  Panda only. */
+ * effector; requires an attachment (vgpu_env_attach).  Panda, Fetch, UR5 (Baxter: = vgpu_fkcc). */
 int vgpu_fkcc_attach(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n,
                      uint8_t *valid);
 /* validate_motion<Robot, 8, Robot::resolution>(starts[i], goals[i], env) for every edge:

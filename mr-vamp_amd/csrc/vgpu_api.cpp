@@ -95,6 +95,14 @@ hipError_t vgpu_launch_panda_fkcc_attach(const float* q, size_t n, const EnvView
 hipError_t vgpu_launch_panda_validate_head_att(const float* starts, const float* goals, size_t n_edges,
                                                const EnvView* env, float bx, float by, float bz, uint8_t* ok,
                                                int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
+hipError_t vgpu_launch_fetch_fkcc_attach(const float* q, size_t n, const EnvView* env, uint8_t* valid, hipStream_t st);
+hipError_t vgpu_launch_fetch_validate_head_att(const float* starts, const float* goals, size_t n_edges,
+                                               const EnvView* env, uint8_t* ok, int32_t* n_blocks, uint32_t* cnt,
+                                               hipStream_t st);
+hipError_t vgpu_launch_ur5_fkcc_attach(const float* q, size_t n, const EnvView* env, uint8_t* valid, hipStream_t st);
+hipError_t vgpu_launch_ur5_validate_head_att(const float* starts, const float* goals, size_t n_edges,
+                                             const EnvView* env, uint8_t* ok, int32_t* n_blocks, uint32_t* cnt,
+                                             hipStream_t st);
 hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goals, size_t n_edges,
                                            const EnvView* env, float bx, float by, float bz, uint8_t* ok,
                                            int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
@@ -1017,13 +1025,19 @@ extern "C" int vgpu_fkcc_attach(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, c
     float b[3];
     int rc = check_robot(c, r, b);
     if (rc) return rc;
-    if (r->kind != VGPU_ROBOT_PANDA) return fail(c, VGPU_ERR_UNSUPPORTED, "fkcc_attach: Panda only");
+    if (r->kind == VGPU_ROBOT_PANDA_PAIR) return fail(c, VGPU_ERR_UNSUPPORTED, "fkcc_attach: not for the composite");
     if (!e->attached) return fail(c, VGPU_ERR_INVALID_ARG, "fkcc_attach: the environment has no attachment");
     if (n && (!q || !valid)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if (r->kind == VGPU_ROBOT_BAXTER) return vgpu_fkcc(c, r, e, q, n, valid);  // Baxter::fkcc_attach = fkcc
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, vgpu_launch_panda_fkcc_attach(q, n, &v, b[0], b[1], b[2], valid, c->cur));
+    if (r->kind == VGPU_ROBOT_FETCH)
+        HIPCHK(c, vgpu_launch_fetch_fkcc_attach(q, n, &v, valid, c->cur));
+    else if (r->kind == VGPU_ROBOT_UR5)
+        HIPCHK(c, vgpu_launch_ur5_fkcc_attach(q, n, &v, valid, c->cur));
+    else
+        HIPCHK(c, vgpu_launch_panda_fkcc_attach(q, n, &v, b[0], b[1], b[2], valid, c->cur));
     return VGPU_OK;
 }
 
@@ -1059,10 +1073,11 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     if (n_edges == 0) return VGPU_OK;
     if (!starts || !goals || !ok) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
     if (n_edges >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many edges in one call (< 2^31)");
-    // validate.hh:43: with an attachment the first block goes through fkcc_attach
-    const bool att = e->attached;
-    if (att && r->kind != VGPU_ROBOT_PANDA)
-        return fail(c, VGPU_ERR_UNSUPPORTED, "attachments: fkcc_attach is built for the Panda only");
+    // validate.hh:43: with an attachment the first block goes through fkcc_attach; the Baxter's
+    // fkcc_attach is its plain fkcc (baxter.hh:44), so its attachment changes nothing
+    const bool att = e->attached && r->kind != VGPU_ROBOT_BAXTER;
+    if (att && r->kind == VGPU_ROBOT_PANDA_PAIR)
+        return fail(c, VGPU_ERR_UNSUPPORTED, "attachments: no fkcc_attach for the composite");
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
     HIPCHK(c, hipSetDevice(c->device));
@@ -1080,8 +1095,13 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     pair_bases(r, pb);
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
     if (att) {
-        HIPCHK(c, vgpu_launch_panda_validate_head_att(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks, cnt,
-                                                      c->cur));
+        if (r->kind == VGPU_ROBOT_FETCH)
+            HIPCHK(c, vgpu_launch_fetch_validate_head_att(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
+        else if (r->kind == VGPU_ROBOT_UR5)
+            HIPCHK(c, vgpu_launch_ur5_validate_head_att(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
+        else
+            HIPCHK(c, vgpu_launch_panda_validate_head_att(starts, goals, n_edges, &v, b[0], b[1], b[2], ok, n_blocks,
+                                                          cnt, c->cur));
     } else if (g_mono) {
         HIPCHK(c, g->validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
     } else if (pair) {

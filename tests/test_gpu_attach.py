@@ -93,12 +93,53 @@ def test_attach_mixed_primitives(vamp, oracle, seed):
     assert np.array_equal(n, on) and np.array_equal(ok, ook)
 
 
-def test_attach_other_robot_refused(vamp, oracle):
+def _mbm_env(vamp, oracle, fx):
+    o = oracle.Env()
+    for k in ("spheres", "capsules", "zcapsules", "cuboids", "zcuboids"):
+        setattr(o, k, [list(r) for r in fx["env_" + k]])
+    return o, gpu_env_from_oracle(vamp, o)
+
+
+@pytest.mark.parametrize("robot", ["fetch", "ur5"])
+def test_robot_attach(vamp, oracle, robot):
+    """Fetch / UR5 fkcc_attach and the attached rake on their MBM scene: GPU == oracle on the
+    same host, and == the reference-DAG fixture on the margin-filtered set."""
+    fx = golden(f"attach_{robot}.npz")
+    same = same_rsqrt_host(oracle, fx)
+    oenv, env = _mbm_env(vamp, oracle, fx)
+    a, o = both(vamp, oracle, fx)
+    env.attach(a)
+    r = getattr(vamp, robot)
+    got = r.fkcc_attach_batch(fx["q"], env)
+    assert np.array_equal(got, oracle.robot_fkcc_attach_threads(robot, oenv, o, fx["q"]))
+    m = stable(fx["test_margin"], fx["cull_margin"], same)
+    assert np.array_equal(got[m], fx["valid"][m])
+    ok, n = r.validate_batch(fx["starts"], fx["goals"], env)
+    ook, on = oracle.robot_validate_motions_att(robot, oenv, o, fx["starts"], fx["goals"])
+    assert np.array_equal(n, on) and np.array_equal(ok, ook)
+    me = stable(fx["edge_test_margin"], fx["edge_cull_margin"], same)
+    assert np.array_equal(ok[me], fx["ok"][me])
+
+
+def test_baxter_attach_is_plain(vamp, oracle):
+    """Baxter::fkcc_attach = interleaved_sphere_fk (baxter.hh:44): an attachment changes nothing."""
+    rng = np.random.default_rng(8)
+    oenv = oracle.sphere_cage_env()
+    env = gpu_env_from_oracle(vamp, oenv)
+    q = oracle.robot_scale("baxter", rng.random((2048, 14), dtype=F))
+    s, g = q[:1024], q[1024:]
+    plain_ok, plain_n = vamp.baxter.validate_batch(s, g, env)
+    a, _ = both(vamp, oracle)
+    env.attach(a)
+    ok, n = vamp.baxter.validate_batch(s, g, env)
+    assert np.array_equal(ok, plain_ok) and np.array_equal(n, plain_n)
+    assert np.array_equal(vamp.baxter.fkcc_attach_batch(q, env), oracle.robot_fkcc_threads("baxter", oenv, q))
+
+
+def test_attach_composite_refused(vamp, oracle):
     env = vamp.Environment()
     a, _ = both(vamp, oracle)
     env.attach(a)
-    q = np.zeros((4, 8), F)
+    q = np.zeros((4, 14), F)
     with pytest.raises(vamp.VgpuError):
-        vamp.fetch.validate_batch(q, q, env)
-    with pytest.raises(vamp.VgpuError):
-        vamp.fetch.fkcc_attach_batch(q, env)
+        vamp.panda_pair.validate_batch(q, q, env)

@@ -7,6 +7,7 @@ Object: tests/oracle_py.py:held_object (four spheres of r 3 cm along the hand's 
 turned 45 degrees).  Scene: the sphere cage.  Same tolerances as tests/test_oracle.py.
 """
 import numpy as np
+import pytest
 
 from conftest import golden
 from test_oracle import stable, same_rsqrt_host
@@ -62,3 +63,46 @@ def test_attach_without_spheres_equals_fkcc(oracle):
     a = oracle.robot_fkcc_attach_threads("panda", env, empty, q)
     b = oracle.fkcc_threads(env, q)
     assert np.array_equal(a, b)
+
+
+def _mbm_env(oracle, fx):
+    e = oracle.Env()
+    for k in ("spheres", "capsules", "zcapsules", "cuboids", "zcuboids"):
+        setattr(e, k, [list(r) for r in fx["env_" + k]])
+    return e
+
+
+@pytest.mark.parametrize("robot", ["ur5", "fetch"])
+def test_robot_fkcc_attach_vs_reference_dag(oracle, robot):
+    """Fetch (fetch.hh:42) and UR5 (ur5.hh:43) fkcc_attach = their generated
+    interleaved_sphere_fk_attachment, on their MBM table_pick scene; edges with the first block
+    through it."""
+    import os
+    from conftest import GOLD
+    if not os.path.exists(os.path.join(GOLD, f"attach_{robot}.npz")):
+        pytest.skip("fixture not generated")
+    fx = golden(f"attach_{robot}.npz")
+    same = same_rsqrt_host(oracle, fx)
+    env = _mbm_env(oracle, fx)
+    att = _att(oracle, fx)
+    got = oracle.robot_fkcc_attach_threads(robot, env, att, fx["q"])
+    m = stable(fx["test_margin"], fx["cull_margin"], same)
+    assert m.mean() > 0.9
+    assert np.array_equal(got[m], fx["valid"][m])
+    assert int((got != fx["valid"]).sum()) <= max(2, int(2e-4 * len(got)))
+    assert (fx["plain"] & ~fx["valid"]).sum() > 0
+    ok, n = oracle.robot_validate_motions_att(robot, env, att, fx["starts"], fx["goals"])
+    assert np.array_equal(n, fx["n"])
+    me = stable(fx["edge_test_margin"], fx["edge_cull_margin"], same)
+    assert np.array_equal(ok[me], fx["ok"][me])
+
+
+def test_baxter_fkcc_attach_is_fkcc(oracle):
+    """Baxter's fkcc_attach is its plain interleaved_sphere_fk (baxter.hh:44): the attachment is
+    not checked."""
+    rng = np.random.default_rng(6)
+    q = oracle.robot_scale("baxter", rng.random((1024, 14), dtype=np.float32))
+    env = oracle.sphere_cage_env()
+    att = oracle.held_object()
+    assert np.array_equal(oracle.robot_fkcc_attach_threads("baxter", env, att, q),
+                          oracle.robot_fkcc_threads("baxter", env, q))

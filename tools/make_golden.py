@@ -263,6 +263,39 @@ def make_attach(rng):
           ok.mean())
 
 
+def make_attach_robot(rng, robot, scene, n_cfg=8192, n_edges=1024):
+    """Fetch / UR5 with the held object on one MotionBenchMaker scene: per-configuration
+    fkcc_attach masks (the robot's interleaved_sphere_fk_attachment) next to plain fkcc, and
+    valid-endpoint edges capped at 1.0 whose first block goes through it (validate.hh:43)."""
+    src = open(f"/root/reference/src/impl/vamp/robots/{robot}/fk.hh").read()
+    cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
+    ca = fi.parse_function(src, r"inline bool interleaved_sphere_fk_attachment\(")
+    dim = op.ROBOTS[robot][1]
+    lut, kb = op.rsqrt_probe()
+    rs = fi.RsqrtHost(lut, kb)
+    env = op.mbm_env(mbm_scene(robot, scene))
+    envnp = envnp_of(env)
+    ad = op.held_object().as_dict()
+    q = op.robot_scale(robot, rng.random((n_cfg, dim), dtype=F))
+    valid, st = fi.run_fkcc(ca, q, (0, 0, 0), envnp, rs, G=1, att=ad)
+    plain, _ = fi.run_fkcc(cc, q, (0, 0, 0), envnp, rs, G=1)
+    pool = op.robot_scale(robot, rng.random((8 * n_edges, dim), dtype=F))
+    pv = op.robot_fkcc_threads(robot, env, pool)
+    vq = pool[pv]
+    E = min(n_edges, len(vq) // 2)
+    s, g = vq[0:2 * E:2], vq[1:2 * E:2]
+    d = np.linalg.norm((g - s).astype(np.float64), axis=1)
+    g = (s + (g - s) * np.minimum(1.0, 1.0 / np.maximum(d, 1e-9)).astype(F)[:, None]).astype(F)
+    ok, n, tm, cm = interp_validate(cc, s, g, (0, 0, 0), envnp, rs, op.RESOLUTION[robot], cc_first=ca, att=ad)
+    arr = env.arrays()
+    np.savez_compressed(os.path.join(GOLD, f"attach_{robot}.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
+                        att_tf=ad["tf"], att_spheres=ad["spheres"], q=q, valid=valid, plain=plain,
+                        test_margin=st.test_margin.astype(F), cull_margin=st.cull_margin.astype(F), starts=s, goals=g,
+                        ok=ok, n=n.astype(np.int32), edge_test_margin=tm.astype(F), edge_cull_margin=cm.astype(F),
+                        **{"env_" + k: v for k, v in arr.items()})
+    print(f"attach_{robot}.npz", valid.mean(), plain.mean(), ok.mean())
+
+
 def make_l2_pins(rng):
     """FloatVector<dim>::l2_norm for dim 7, 8 and 14 (ref_probe "l2norm"): the 14-lane form is
     two registers contracted as fma(lo, lo, hi * hi) before the hsum."""
@@ -380,6 +413,12 @@ def main():
         return
     if "--fetch" in sys.argv:
         make_fetch(np.random.default_rng(20261016))
+        return
+    if "--attach-fetch" in sys.argv:
+        make_attach_robot(np.random.default_rng(20261022), "fetch", "table_pick_fetch/scene0001.yaml")
+        return
+    if "--attach-ur5" in sys.argv:
+        make_attach_robot(np.random.default_rng(20261023), "ur5", "table_pick_ur5/scene0001.yaml")
         return
     if "--attach" in sys.argv:
         make_attach(np.random.default_rng(20261021))
