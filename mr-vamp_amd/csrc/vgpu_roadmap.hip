@@ -139,11 +139,9 @@ __global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict_
         }
         __syncthreads();
         const uint32_t tn = min((uint32_t)kKnnBlock, c_hi - t0);
-        for (uint32_t u = 0; u < tn; ++u) {
-            const uint32_t j = t0 + u;
-            const float s = config_sumsq<D>(tile + u * D, me);
+        auto consider = [&](uint32_t j, float s) {
             const bool pre = j < i && s <= thr;
-            if (__builtin_amdgcn_ballot_w64(pre) == 0ull) continue;
+            if (__builtin_amdgcn_ballot_w64(pre) == 0ull) return;
             const float d = __builtin_sqrtf(s);
             // nn query semantics: distance <= r, strictly closer than the k-th to displace it
             const bool take = pre && (c < k ? d <= worst : d < worst);
@@ -152,7 +150,29 @@ __global__ __launch_bounds__(kKnnBlock) void knn_kernel(const float* __restrict_
                 buf_i[nb][lane] = j;
                 ++nb;
             }
-            if (__builtin_amdgcn_ballot_w64(nb == kKnnBuf) != 0ull) flush();
+        };
+        // a step appends at most 4 per lane: flush while the buffers still have room for that
+        auto maybe_flush = [&]() {
+            if (__builtin_amdgcn_ballot_w64(nb > kKnnBuf - 4) != 0ull) flush();
+        };
+        uint32_t u = 0;
+        // four candidates per step: independent LDS reads and sums in flight, one ballot when
+        // none of them is plausible for any lane (the common case)
+        for (; u + 4 <= tn; u += 4) {
+            float s4[4];
+#pragma unroll
+            for (int h = 0; h < 4; ++h) s4[h] = config_sumsq<D>(tile + (u + h) * D, me);
+            bool any = false;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) any |= (t0 + u + h < i) && s4[h] <= thr;
+            if (__builtin_amdgcn_ballot_w64(any) == 0ull) continue;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) consider(t0 + u + h, s4[h]);
+            maybe_flush();
+        }
+        for (; u < tn; ++u) {
+            consider(t0 + u, config_sumsq<D>(tile + u * D, me));
+            maybe_flush();
         }
         if (__builtin_amdgcn_ballot_w64(nb != 0) != 0ull) flush();
     }
