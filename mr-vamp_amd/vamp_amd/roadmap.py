@@ -191,7 +191,7 @@ def edges_shard(torch, robot, environment, V, k, r, kmax: int, q_first: int, q_c
     """This rank's share of build_roadmap's edge stage on the GPU: neighbour queries of vertices
     q_first .. q_first+q_count-1, then validate_motion(neighbor, vertex) of their candidates.
     V [n, dim], k [n], r [n] are device tensors (all vertices).  Returns the valid (vertex,
-    neighbour) pairs in query order, nearest first: int64 tensor [m, 2]."""
+    neighbour) pairs in query order, nearest first: int32 tensor [m, 2]."""
     from ._lib import check, load
     dev = V.device
     n, dim = V.shape
@@ -199,7 +199,7 @@ def edges_shard(torch, robot, environment, V, k, r, kmax: int, q_first: int, q_c
     dist_ = torch.empty((max(q_count, 1), kmax), dtype=torch.float32, device=dev)
     cnt = torch.zeros(max(q_count, 1), dtype=torch.int32, device=dev)
     if q_count == 0:
-        return torch.zeros((0, 2), dtype=torch.int64, device=dev)
+        return torch.zeros((0, 2), dtype=torch.int32, device=dev)
     check(load().vgpu_roadmap_knn_range(ctx.h, dim, V.data_ptr(), n, q_first, q_count, k.data_ptr(), r.data_ptr(),
                                         kmax, nbr.data_ptr(), dist_.data_ptr(), cnt.data_ptr()), ctx.h)
     cnt = cnt[:q_count]
@@ -207,7 +207,7 @@ def edges_shard(torch, robot, environment, V, k, r, kmax: int, q_first: int, q_c
     off[1:] = torch.cumsum(cnt, 0)
     E = int(off[-1])
     if E == 0:
-        return torch.zeros((0, 2), dtype=torch.int64, device=dev)
+        return torch.zeros((0, 2), dtype=torch.int32, device=dev)
     starts = torch.empty((E, dim), dtype=torch.float32, device=dev)
     goals = torch.empty_like(starts)
     check(load().vgpu_roadmap_edge_gather(ctx.h, dim, V.data_ptr(), q_first, q_count, nbr.data_ptr(), kmax,
@@ -218,7 +218,7 @@ def edges_shard(torch, robot, environment, V, k, r, kmax: int, q_first: int, q_c
     m = torch.arange(E, device=dev) - off[:-1].long().repeat_interleave(cnt.long())
     qj = nbr[:q_count].long()[qi - q_first, m]
     keep = ok.bool()
-    return torch.stack([qi[keep], qj[keep]], 1)
+    return torch.stack([qi[keep], qj[keep]], 1).to(torch.int32)  # vertex indices < 2^31
 
 
 def allgather_pairs(torch, dist, pairs, group=None):
@@ -231,9 +231,9 @@ def allgather_pairs(torch, dist, pairs, group=None):
     dist.all_gather_into_tensor(cnts, cnt, group=group)
     counts = [int(c) for c in cnts.tolist()]
     mx = max(counts)
-    send = torch.zeros((mx, 2), dtype=torch.int64, device=dev)
+    send = torch.zeros((mx, 2), dtype=pairs.dtype, device=dev)
     send[:pairs.shape[0]] = pairs
-    recv = torch.empty((world * mx, 2), dtype=torch.int64, device=dev)
+    recv = torch.empty((world * mx, 2), dtype=pairs.dtype, device=dev)
     if mx:
         dist.all_gather_into_tensor(recv, send, group=group)
     return torch.cat([recv[r * mx:r * mx + c] for r, c in enumerate(counts)])
@@ -249,7 +249,8 @@ def assemble(n: int, pairs: np.ndarray):
 
     from . import _lib
     from ._lib import check, load
-    p = np.ascontiguousarray(np.asarray(pairs).reshape(-1, 2), np.uint32)
+    p = np.asarray(pairs).reshape(-1, 2)
+    p = p.view(np.uint32) if p.dtype == np.int32 and p.flags.c_contiguous else np.ascontiguousarray(p, np.uint32)
     offsets = np.zeros(n + 1, np.uint64)
     adj = np.zeros(max(2 * len(p), 1), np.uint32)
     comp = np.zeros(max(n, 1), np.uint32)

@@ -122,3 +122,25 @@ def test_attachment_host_pose_identity():
     a.set_ee_pose((0.0, 0.0, 0.0), (0.0, 0.0, h, h))
     assert np.allclose(a.posed_spheres[0].center, [0.2, 0.1, 0.3], atol=1e-6)
     assert a.relative_frame == ([0.0, 0.0, 0.0], [0.0, 0.0, 0.0, 1.0])
+
+
+def test_roadmap_host_functions_errors_and_order():
+    """vgpu_prm_neighbor_params / vgpu_roadmap_assemble are host code (no GPU): argument errors
+    come back as VGPU_ERR_INVALID_ARG, and the assembly replays pairs in the reference's append
+    order (prm.hh:270-275)."""
+    import ctypes as C
+    import numpy as np
+    from vamp_amd import _lib, roadmap
+    lib = _lib.load()
+    k = np.zeros(4, np.uint32)
+    r = np.zeros(4, np.float32)
+    assert lib.vgpu_prm_neighbor_params(0, 1.0, 2.0, 4, k.ctypes.data_as(_lib.U32P), r.ctypes.data_as(_lib.F32P)) == -1
+    off = np.zeros(4, np.uint64)
+    adj = np.zeros(8, np.uint32)
+    bad = np.array([[2, 7]], np.uint32)  # neighbour index outside the 3 vertices
+    assert lib.vgpu_roadmap_assemble(3, bad.ctypes.data_as(_lib.U32P), 1, off.ctypes.data_as(C.POINTER(C.c_size_t)),
+                                     adj.ctypes.data_as(_lib.U32P), None) == -1
+    # vertex 2 connects to 0 then 1; vertex 3 to 1: lists 0:[2] 1:[2,3] 2:[0,1] 3:[1]
+    o, a, comp = roadmap.assemble(5, np.array([[2, 0], [2, 1], [3, 1]], np.int32))
+    assert [a[o[i]:o[i + 1]].tolist() for i in range(5)] == [[2], [2, 3], [0, 1], [1], []]
+    assert comp.tolist() == [0, 0, 0, 0, 4]
