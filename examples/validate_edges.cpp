@@ -27,6 +27,19 @@ using namespace vamp_gpu;
     return (a ? 1u : 0u) + b.size() + (c ? 1u : 0u) + (d ? 1u : 0u) + (e ? 1u : 0u);
 }
 
+// An attached object (Environment::attach) and the PRM edge stage (build_roadmap's graph).
+[[maybe_unused]] static auto attach_and_roadmap(collision::Environment &env) -> std::size_t
+{
+    collision::Attachment held({0.0f, 0.0f, 0.1f}, {0.0f, 0.0f, 0.0f, 1.0f});
+    held.add_sphere({0.0f, 0.0f, 0.05f}, 0.03f);
+    env.attach(held);
+    const auto m = robots::Panda_0_0::fkcc_attach(env, std::vector<robots::Panda_0_0::Configuration>(4));
+    env.detach();
+    const auto rm = planning::build_roadmap_edges<robots::Fetch>(
+        env, std::vector<robots::Fetch::Configuration>(16), 269832.265625);
+    return m.size() + rm.edges.size();
+}
+
 int main(int argc, char **argv)
 {
     if (argc < 3)

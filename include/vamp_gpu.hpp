@@ -63,6 +63,23 @@ namespace vamp_gpu
     {
         using Point = std::array<float, 3>;
 
+        // vamp::collision::Attachment<float> (collision/attachments.hh:14-123): spheres (x y z r)
+        // relative to a frame (x y z, quaternion x y z w) held at the end effector
+        struct Attachment
+        {
+            Attachment(const Point &center, const std::array<float, 4> &quaternion_xyzw)
+              : frame{center[0], center[1], center[2], quaternion_xyzw[0], quaternion_xyzw[1],
+                      quaternion_xyzw[2], quaternion_xyzw[3]}
+            {
+            }
+            void add_sphere(const Point &center, float radius)
+            {
+                spheres.push_back({center[0], center[1], center[2], radius});
+            }
+            std::array<float, 7> frame;
+            std::vector<std::array<float, 4>> spheres;
+        };
+
         // vamp::collision::Environment<float>: obstacles are routed and sorted exactly like the
         // reference (axis_3_z == 1 -> z-aligned cuboid, xv == yv == 0 -> z-aligned capsule,
         // each list by min_distance); the device copy is made lazily on first use.
@@ -107,6 +124,15 @@ namespace vamp_gpu
                 check(vgpu_env_add_capsule_euler(h_, center.data(), euler_xyz.data(), radius, length),
                       ctx_.handle(), "add_capsule");
             }
+            // Environment::attach(Attachment) / detach (bindings/environment.cc:161-163):
+            // validate_motion then runs its first rake block through Robot::fkcc_attach
+            void attach(const Attachment &a)
+            {
+                check(vgpu_env_attach(h_, a.frame.data(), a.spheres.empty() ? nullptr : a.spheres[0].data(),
+                                      a.spheres.size()),
+                      ctx_.handle(), "attach");
+            }
+            void detach() { check(vgpu_env_detach(h_), ctx_.handle(), "detach"); }
             auto handle() const noexcept -> vgpu_env * { return h_; }
             auto context() const noexcept -> Context & { return ctx_; }
 
@@ -141,6 +167,22 @@ namespace vamp_gpu
                 check(vgpu_fkcc_host(c, &r, env.handle(), q.empty() ? nullptr : q[0].data(), q.size(),
                                      out.data()),
                       c, "vgpu_fkcc_host");
+                return out;
+            }
+
+            // fkcc_attach<rake> of each configuration (robots/panda_base.hh:61-65, fetch.hh:42,
+            // ur5.hh:43; the Baxter's is its fkcc): the environment's attachment posed at the
+            // end effector
+            template <typename Configuration>
+            static auto fkcc_attach(collision::Environment &env, const std::vector<Configuration> &q)
+                -> std::vector<uint8_t>
+            {
+                std::vector<uint8_t> out(q.size());
+                const vgpu_robot r = Derived::c_robot();
+                vgpu_ctx *c = env.context().handle();
+                check(vgpu_fkcc_attach_host(c, &r, env.handle(), q.empty() ? nullptr : q[0].data(), q.size(),
+                                            out.data()),
+                      c, "vgpu_fkcc_attach_host");
                 return out;
             }
 
@@ -275,6 +317,47 @@ namespace vamp_gpu
                                     const typename Robot::Configuration &goal) -> bool
         {
             return validate_motions<Robot>(env, {start}, {goal})[0] != 0;
+        }
+
+        // Roadmap<dim> (prm.hh:285-299): vertices and, per vertex, its neighbours in the order
+        // build_roadmap appended them; component = smallest vertex index of its component
+        template <typename Robot>
+        struct Roadmap
+        {
+            std::vector<typename Robot::Configuration> vertices;
+            std::vector<std::vector<std::size_t>> edges;
+            std::vector<uint32_t> component;
+        };
+
+        // Roadmap::build_roadmap's graph (prm.hh:197-299) over a vertex sequence (start, goal,
+        // then the valid samples in draw order): every vertex's PRM* neighbour query
+        // (PRMStarNeighborParams(dim, space_measure) with gamma_scale, roadmap.hh:42-77) and
+        // validate_motion of every candidate edge on the GPU
+        template <typename Robot>
+        inline auto build_roadmap_edges(collision::Environment &env,
+                                        const std::vector<typename Robot::Configuration> &vertices,
+                                        double space_measure, double gamma_scale = 2.0) -> Roadmap<Robot>
+        {
+            const std::size_t n = vertices.size();
+            std::vector<uint32_t> k(n);
+            std::vector<float> r(n);
+            check(vgpu_prm_neighbor_params(static_cast<int>(Robot::dimension), space_measure, gamma_scale, n, k.data(),
+                                           r.data()),
+                  nullptr, "vgpu_prm_neighbor_params");
+            std::size_t cap = 0;
+            for (uint32_t v : k) cap += 2 * static_cast<std::size_t>(v);
+            std::vector<std::size_t> offsets(n + 1, 0);
+            std::vector<uint32_t> adj(cap > 0 ? cap : 1);
+            Roadmap<Robot> out{vertices, std::vector<std::vector<std::size_t>>(n), std::vector<uint32_t>(n)};
+            std::size_t n_adj = 0;
+            const vgpu_robot rb = Robot::c_robot();
+            vgpu_ctx *c = env.context().handle();
+            check(vgpu_build_roadmap_host(c, &rb, env.handle(), n ? vertices[0].data() : nullptr, n, space_measure,
+                                          gamma_scale, offsets.data(), adj.data(), adj.size(), &n_adj,
+                                          out.component.data()),
+                  c, "vgpu_build_roadmap_host");
+            for (std::size_t i = 0; i < n; ++i) out.edges[i].assign(adj.begin() + offsets[i], adj.begin() + offsets[i + 1]);
+            return out;
         }
     }  // namespace planning
 }  // namespace vamp_gpu
