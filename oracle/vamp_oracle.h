@@ -203,6 +203,22 @@ float vo_config_distance(const float *a, const float *b, int dim);
 void vo_roadmap_knn(int dim, const float *V, size_t n, double space_measure, double gamma_scale, uint32_t kmax,
                     uint32_t *nbr, float *dist, uint32_t *cnt, int threads);
 
+/* ---- Point-cloud filter (collision/filter.hh:101-121,175-268) ---- */
+/* remap_point (filter.hh:101-104): float quotient * 1000 converted to uint32 the way GCC's x86-64
+ * codegen does it (cvttss2si to 64 bits, low 32 bits kept), so out-of-range inputs wrap. */
+uint32_t vo_remap_point(float x, float mn, float mx);
+/* morton_pdep (filter.hh:124-127): x -> bits 0,3,..,30; y -> 1,4,..,31; z -> 2,5,..,29. */
+uint32_t vo_morton_encode(uint32_t x, uint32_t y, uint32_t z);
+/* filter_pointcloud (filter.hh:175-268). pc: n x 3 f32. Writes the kept point indices (in the
+ * final sort order) to out_idx (capacity n) and returns their count. Ties among equal Morton
+ * codes are ordered by position in the previous pass (a stable sort); the reference uses
+ * pdqsort_branchless (unstable), so results on tied codes are parity unpinned. Reproduces the
+ * reference's quirks: the upper bound starts as min(origin + max_range) over axes (filter.hh:192),
+ * and with cull the Morton list keeps its full length n, its unfilled tail naming point 0
+ * (filter.hh:194-214). */
+size_t vo_filter_pointcloud(const float *pc, size_t n, float min_dist, float max_range, const float origin[3],
+                            const float ws_min[3], const float ws_max[3], int cull, uint32_t *out_idx);
+
 #ifdef __cplusplus
 }
 #endif

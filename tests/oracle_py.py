@@ -644,3 +644,30 @@ def components(n, edges):
             if a != b:
                 parent[max(a, b)] = min(a, b)
     return np.array([find(i) for i in range(n)], np.uint32)
+
+
+def morton_encode(x, y, z):
+    L = lib()
+    L.vo_morton_encode.restype = C.c_uint32
+    L.vo_morton_encode.argtypes = [C.c_uint32] * 3
+    return L.vo_morton_encode(x, y, z)
+
+
+def remap_point(x, mn, mx):
+    L = lib()
+    L.vo_remap_point.restype = C.c_uint32
+    L.vo_remap_point.argtypes = [C.c_float] * 3
+    return L.vo_remap_point(x, mn, mx)
+
+
+def filter_pointcloud(pc, min_dist, max_range, origin, ws_min, ws_max, cull=True):
+    """filter_pointcloud (collision/filter.hh:175-268): kept point indices in the final order."""
+    L = lib()
+    L.vo_filter_pointcloud.restype = C.c_size_t
+    L.vo_filter_pointcloud.argtypes = [F32P, C.c_size_t, C.c_float, C.c_float, F32P, F32P, F32P, C.c_int, U32P]
+    pc = np.ascontiguousarray(pc, np.float32).reshape(-1, 3)
+    out = np.zeros(max(pc.shape[0], 1), np.uint32)
+    o, a, b = (np.ascontiguousarray(v, np.float32) for v in (origin, ws_min, ws_max))
+    k = L.vo_filter_pointcloud(fp(pc), pc.shape[0], min_dist, max_range, fp(o), fp(a), fp(b), int(cull),
+                               out.ctypes.data_as(U32P))
+    return out[:k].copy()
