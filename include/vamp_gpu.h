@@ -219,6 +219,18 @@ int vgpu_build_roadmap_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *en
 
 /* ---- robot metadata ------------------------------------------------------------------------ */
 /* dimension, resolution, n_spheres of a robot kind (robots/panda_base.hh:19-23) */
+/* Point-cloud filter (replaces vamp::collision::filter_pointcloud, collision/filter.hh:175-268,
+ * bound as vamp.filter_pointcloud in bindings/common.hh). pc: n x 3 f32 (device for the first,
+ * host for the _host variant). Writes the kept point indices, in the final space-filling-curve
+ * order, to out_idx (capacity n) and their number to *count. Equal Morton codes keep their
+ * previous order (stable sort; the reference's pdqsort leaves it unspecified). */
+int vgpu_filter_pointcloud(vgpu_ctx *ctx, const float *pc, size_t n, float min_dist, float max_range,
+                           const float origin[3], const float ws_min[3], const float ws_max[3], int cull,
+                           uint32_t *out_idx, size_t *count);
+int vgpu_filter_pointcloud_host(vgpu_ctx *ctx, const float *pc, size_t n, float min_dist, float max_range,
+                                const float origin[3], const float ws_min[3], const float ws_max[3], int cull,
+                                uint32_t *out_idx, size_t *count);
+
 int vgpu_pointcloud_collides_host(vgpu_ctx *ctx, vgpu_env *env, int index, const float *centers,
                                   const float *radii, size_t n, int simd, uint8_t *out);
 int vgpu_halton_host(vgpu_ctx *ctx, int dim, uint64_t first, size_t n, float *out);

@@ -27,6 +27,9 @@ hipError_t vgpu_launch_panda_sample(uint64_t first, size_t n, float* q, hipStrea
 hipError_t vgpu_launch_panda_sample_fkcc(uint64_t first, size_t n, const EnvView* env, float bx, float by, float bz,
                                          float* q, uint8_t* valid, hipStream_t st);
 hipError_t vgpu_launch_halton(int dim, uint64_t first, size_t n, float* out, hipStream_t st);
+hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, float min_dist, float max_range,
+                                      const float origin[3], const float ws_min[3], const float ws_max[3], int cull,
+                                      uint32_t* d_out, size_t* count, hipStream_t s);
 size_t vgpu_compact_bytes(size_t n);
 hipError_t vgpu_launch_compact(const uint8_t* valid, size_t n, uint32_t* idx_out, uint32_t* count, void* tmp,
                                size_t tmp_bytes, hipStream_t st);
@@ -1185,6 +1188,22 @@ extern "C" int vgpu_pointcloud_collides(vgpu_ctx* c, vgpu_env* e, int index, con
     return VGPU_OK;
 }
 
+// filter_pointcloud (collision/filter.hh:175-268) on the device (vgpu_filter.hip)
+extern "C" int vgpu_filter_pointcloud(vgpu_ctx* c, const float* pc, size_t n, float min_dist, float max_range,
+                                      const float origin[3], const float ws_min[3], const float ws_max[3], int cull,
+                                      uint32_t* out_idx, size_t* count)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (!count || !origin || !ws_min || !ws_max) return fail(c, VGPU_ERR_INVALID_ARG, "null argument");
+    *count = 0;
+    if (n == 0) return VGPU_OK;
+    if (!pc || !out_idx || n > 0x7fffffffu) return fail(c, VGPU_ERR_INVALID_ARG, "bad filter_pointcloud arguments");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, vgpu_filter_pointcloud_run(pc, n, min_dist, max_range, origin, ws_min, ws_max, cull, out_idx, count,
+                                         c->cur));
+    return VGPU_OK;
+}
+
 // ---- sampling (rng::Halton, Robot::scale_configuration) and compaction --------------------------
 extern "C" int vgpu_halton(vgpu_ctx* c, int dim, uint64_t first, size_t n, float* out)
 {
@@ -1384,6 +1403,29 @@ extern "C" int vgpu_validate_motions_host(vgpu_ctx* c, const vgpu_robot* r, vgpu
     if ((rc = vgpu_validate_motions(c, r, e, (const float*)d, (const float*)(d + qb), n, okd, nbd))) return rc;
     HIPCHK(c, hipMemcpyAsync(ok, okd, n, hipMemcpyDeviceToHost, c->cur));
     if (n_blocks) HIPCHK(c, hipMemcpyAsync(n_blocks, nbd, n * 4, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_filter_pointcloud_host(vgpu_ctx* c, const float* pc, size_t n, float min_dist, float max_range,
+                                           const float origin[3], const float ws_min[3], const float ws_max[3],
+                                           int cull, uint32_t* out_idx, size_t* count)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (!count) return fail(c, VGPU_ERR_INVALID_ARG, "null count");
+    *count = 0;
+    if (n == 0) return VGPU_OK;
+    if (!pc || !out_idx) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
+    char* d;
+    const size_t pb = al(n * 12);
+    int rc = stage(c, pb + n * 4, &d);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(d, pc, n * 12, hipMemcpyHostToDevice, c->cur));
+    if ((rc = vgpu_filter_pointcloud(c, (const float*)d, n, min_dist, max_range, origin, ws_min, ws_max, cull,
+                                     (uint32_t*)(d + pb), count)))
+        return rc;
+    HIPCHK(c, hipMemcpyAsync(out_idx, d + pb, *count * 4, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
 }

@@ -1,0 +1,243 @@
+// vgpu_filter.hip -- the point-cloud filter (reference collision/filter.hh:175-268) on the GPU.
+//
+// The reference runs six space-filling-curve passes on one core: Morton-key every surviving
+// point, pdqsort by key, then a sequential scan that keeps a point only if it lies farther than
+// min_dist from the LAST KEPT point.  That scan is a chain (kept_{k+1} = next(kept_k) with
+// next(i) = first j > i farther than min_dist from i), so per pass the GPU
+//   1. keys every point (remap_point + morton_pdep, filter.hh:101-127) and reduces the pass's
+//      coordinate min/max for the next pass's bounds,
+//   2. radix-sorts (key, index) pairs (stable: ties keep the previous pass's order),
+//   3. computes next(i) for every sorted position in parallel (a short forward scan in Morton
+//      order, where close points are adjacent),
+//   4. marks the chain from position 0 by pointer doubling (ceil(log2 len) rounds),
+//   5. compacts the marked positions in order.
+// The result equals the sequential scan for every input; the order among equal keys follows
+// the stable sort (the reference's pdqsort is unstable there: parity unpinned on ties).
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+
+#include <cstdint>
+#include <vector>
+
+namespace {
+
+struct Bounds {
+    float mn, mx;    // the pass's remap range
+    float nmn, nmx;  // running min/max of coordinates over the pass (filter.hh:225-233)
+};
+
+__device__ inline float sql2_3(float ax, float ay, float az, float bx, float by, float bz)
+{
+    // sql2_3 as the oracle restates it for the reference's compiled code (math.hh:17-42 under
+    // -ffp-contract=fast, oracle/vamp_oracle.c sumsq_vec): fmaf(dx, dx, fmaf(dz, dz, dy*dy))
+    const float dx = ax - bx, dy = ay - by, dz = az - bz;
+    return __builtin_fmaf(dx, dx, __builtin_fmaf(dz, dz, dy * dy));
+}
+
+__device__ inline uint32_t remap_point(float x, float mn, float mx)
+{
+    const float q = __fmul_rn(__fdiv_rn(x - mn, mx - mn), 1000.0f);
+    if (!(q > -9.2233715e18f && q < 9.2233715e18f)) return 0u;
+    return (uint32_t)(uint64_t)(int64_t)q;  // GCC x86-64 float -> uint32 (low word of cvttss2si)
+}
+
+__device__ inline uint32_t spread3(uint32_t v, int nbits, int lane)
+{
+    uint32_t out = 0;
+    for (int i = 0; i < nbits; ++i) out |= ((v >> i) & 1u) << (3 * i + lane);
+    return out;
+}
+
+__device__ inline uint32_t morton(uint32_t x, uint32_t y, uint32_t z)
+{
+    // _pdep_u32 with MORTON_X/Y/Z_MASK: 11, 11 and 10 low bits deposited
+    return spread3(x, 11, 0) | spread3(y, 11, 1) | spread3(z, 10, 2);
+}
+
+__device__ inline int f2ord(float f)
+{
+    const int i = __float_as_int(f);
+    return i >= 0 ? i : i ^ 0x7fffffff;
+}
+__device__ inline float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
+
+__global__ void cull_kernel(const float* __restrict__ pc, uint32_t n, float sqrange, float ox, float oy, float oz,
+                            float lx, float ly, float lz, float ux, float uy, float uz, int cull,
+                            uint8_t* __restrict__ flag)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float x = pc[3 * i], y = pc[3 * i + 1], z = pc[3 * i + 2];
+    flag[i] = !cull || (sql2_3(x, y, z, ox, oy, oz) < sqrange && lx <= x && x <= ux && ly <= y && y <= uy &&
+                        lz <= z && z <= uz);
+}
+
+__global__ void iota_kernel(uint32_t* __restrict__ v, uint32_t n)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) v[i] = i;
+}
+
+// keys of the current list under coordinate permutation (c0, c1, c2); min/max into b->nmn/nmx
+__global__ void key_kernel(const float* __restrict__ pc, const uint32_t* __restrict__ idx, uint32_t len, int c0,
+                           int c1, int c2, Bounds* b, int* ordmm, uint32_t* __restrict__ key)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const float mn = b->mn, mx = b->mx;
+    float lo = 3.4e38f, up = -3.4e38f;
+    if (i < len) {
+        const float* p = pc + 3 * (size_t)idx[i];
+        key[i] = morton(remap_point(p[c0], mn, mx), remap_point(p[c1], mn, mx), remap_point(p[c2], mn, mx));
+        lo = fminf(p[0], fminf(p[1], p[2]));
+        up = fmaxf(p[0], fmaxf(p[1], p[2]));
+    }
+    // wave reduction, one atomic per wave
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, off));
+        up = fmaxf(up, __shfl_xor(up, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        atomicMin(&ordmm[0], f2ord(lo));
+        atomicMax(&ordmm[1], f2ord(up));
+    }
+}
+
+// the next pass's bounds (filter.hh:262-263): start from nmn = mx, nmx = mn
+__global__ void bounds_kernel(Bounds* b, int* ordmm)
+{
+    const float nmn = fminf(b->mx, ord2f(ordmm[0])), nmx = fmaxf(b->mn, ord2f(ordmm[1]));
+    const float mx = (float)((double)(nmx + b->mx) / 2.0), mn = (float)((double)(nmn + b->mn) / 2.0);
+    b->mn = mn;
+    b->mx = mx;
+    ordmm[0] = 0x7fffffff;
+    ordmm[1] = (int)0x80000000;
+}
+
+// next(i): first sorted position j > i farther than min_dist from i, else len
+__global__ void next_kernel(const float* __restrict__ pc, const uint32_t* __restrict__ sidx, uint32_t len,
+                            float sqd, uint32_t* __restrict__ jump, uint8_t* __restrict__ on)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    const float* a = pc + 3 * (size_t)sidx[i];
+    const float ax = a[0], ay = a[1], az = a[2];
+    uint32_t j = i + 1;
+    for (; j < len; ++j) {
+        const float* p = pc + 3 * (size_t)sidx[j];
+        if (sql2_3(p[0], p[1], p[2], ax, ay, az) > sqd) break;
+    }
+    jump[i] = j;
+    on[i] = (i == 0);
+}
+
+__global__ void double_kernel(const uint32_t* __restrict__ jin, uint32_t* __restrict__ jout,
+                              const uint8_t* __restrict__ onin, uint8_t* __restrict__ onout, uint32_t len)
+{
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    const uint32_t j = jin[i];
+    if (onin[i]) {
+        onout[i] = 1;
+        if (j < len) onout[j] = 1;
+    }
+    jout[i] = j < len ? jin[j] : len;
+}
+
+inline unsigned blocks(size_t n) { return (unsigned)((n + 255) / 256); }
+
+}  // namespace
+
+#define FCHK(x)                                   \
+    do {                                          \
+        hipError_t e_ = (x);                      \
+        if (e_ != hipSuccess) { release(); return e_; } \
+    } while (0)
+
+// d_pc: n x 3 f32 on the device; d_out: n u32 on the device (kept indices, final order);
+// *count: number kept.  Synchronous on `s`.
+extern "C" hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, float min_dist, float max_range,
+                                      const float origin[3], const float ws_min[3], const float ws_max[3], int cull,
+                                      uint32_t* d_out, size_t* count, hipStream_t s)
+{
+    *count = 0;
+    if (n == 0) return hipSuccess;
+    if (n > 0x7fffffffu) return hipErrorInvalidValue;
+    const uint32_t N = (uint32_t)n;
+    std::vector<void*> bufs;
+    auto release = [&]() { for (void* p : bufs) (void)hipFree(p); };
+    auto alloc = [&](void** p, size_t bytes) {
+        hipError_t e = hipMalloc(p, bytes ? bytes : 1);
+        if (e == hipSuccess) bufs.push_back(*p);
+        return e;
+    };
+    uint32_t *idx, *key, *skey, *sidx, *j0, *j1, *nsel;
+    uint8_t *on0, *on1;
+    Bounds* b;
+    int* ordmm;
+    FCHK(alloc((void**)&idx, 4 * n));
+    FCHK(alloc((void**)&key, 4 * n));
+    FCHK(alloc((void**)&skey, 4 * n));
+    FCHK(alloc((void**)&sidx, 4 * n));
+    FCHK(alloc((void**)&j0, 4 * n));
+    FCHK(alloc((void**)&j1, 4 * n));
+    FCHK(alloc((void**)&on0, n));
+    FCHK(alloc((void**)&on1, n));
+    FCHK(alloc((void**)&nsel, 4));
+    FCHK(alloc((void**)&b, sizeof(Bounds)));
+    FCHK(alloc((void**)&ordmm, 8));
+    size_t tsel = 0, tsort = 0;
+    FCHK(hipcub::DeviceSelect::Flagged(nullptr, tsel, idx, on0, sidx, nsel, N, s));
+    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, key, skey, idx, sidx, N, 0, 32, s));
+    void* tmp;
+    const size_t tbytes = tsel > tsort ? tsel : tsort;
+    FCHK(alloc(&tmp, tbytes));
+
+    // step 1 (filter.hh:194-214): kept indices first, the rest of the n-long list names point 0
+    const float sqd = min_dist * min_dist, sqr = max_range * max_range;
+    cull_kernel<<<blocks(n), 256, 0, s>>>(d_pc, N, sqr, origin[0], origin[1], origin[2], ws_min[0], ws_min[1],
+                                         ws_min[2], ws_max[0], ws_max[1], ws_max[2], cull, on0);
+    iota_kernel<<<blocks(n), 256, 0, s>>>(key, N);
+    size_t tb = tbytes;
+    FCHK(hipcub::DeviceSelect::Flagged(tmp, tb, key, on0, idx, nsel, N, s));
+    uint32_t hi = 0;
+    FCHK(hipMemcpyAsync(&hi, nsel, 4, hipMemcpyDeviceToHost, s));
+    FCHK(hipStreamSynchronize(s));
+    if (hi < N) FCHK(hipMemsetAsync(idx + hi, 0, 4 * (size_t)(N - hi), s));
+
+    auto fmin3 = [](float a, float b2, float c) { float m = a; if (b2 < m) m = b2; if (c < m) m = c; return m; };
+    Bounds hb;
+    hb.mn = fmin3(origin[0] - max_range, origin[1] - max_range, origin[2] - max_range);
+    hb.mx = fmin3(origin[0] + max_range, origin[1] + max_range, origin[2] + max_range);  // sic, filter.hh:192
+    hb.nmn = hb.nmx = 0.f;
+    const int hmm[2] = {0x7fffffff, (int)0x80000000};
+    FCHK(hipMemcpyAsync(b, &hb, sizeof hb, hipMemcpyHostToDevice, s));
+    FCHK(hipMemcpyAsync(ordmm, hmm, 8, hipMemcpyHostToDevice, s));
+
+    static const int perms[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
+    uint32_t len = N;
+    for (int pi = 0; pi < 6; ++pi) {
+        key_kernel<<<blocks(len), 256, 0, s>>>(d_pc, idx, len, perms[pi][0], perms[pi][1], perms[pi][2], b, ordmm,
+                                               key);
+        bounds_kernel<<<1, 1, 0, s>>>(b, ordmm);
+        tb = tbytes;
+        FCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, skey, idx, sidx, len, 0, 32, s));
+        next_kernel<<<blocks(len), 256, 0, s>>>(d_pc, sidx, len, sqd, j0, on0);
+        uint32_t *ja = j0, *jb = j1;
+        uint8_t *oa = on0, *ob = on1;
+        for (uint32_t reach = 1; reach < len; reach <<= 1) {
+            FCHK(hipMemsetAsync(ob, 0, len, s));
+            double_kernel<<<blocks(len), 256, 0, s>>>(ja, jb, oa, ob, len);
+            uint32_t* tj = ja; ja = jb; jb = tj;
+            uint8_t* to = oa; oa = ob; ob = to;
+        }
+        tb = tbytes;
+        FCHK(hipcub::DeviceSelect::Flagged(tmp, tb, sidx, oa, idx, nsel, len, s));
+        FCHK(hipMemcpyAsync(&len, nsel, 4, hipMemcpyDeviceToHost, s));
+        FCHK(hipStreamSynchronize(s));
+    }
+    FCHK(hipMemcpyAsync(d_out, idx, 4 * (size_t)len, hipMemcpyDeviceToDevice, s));
+    FCHK(hipStreamSynchronize(s));
+    *count = len;
+    release();
+    return hipSuccess;
+}

@@ -382,6 +382,29 @@ class Environment:
 
 
 # ---- sampling ---------------------------------------------------------------------------------
+def filter_pointcloud_indices(pc, min_dist: float, max_range: float, origin, workspace_min, workspace_max,
+                              cull: bool = True, ctx: Optional[Context] = None) -> np.ndarray:
+    """Indices of the points vamp.filter_pointcloud keeps (collision/filter.hh:175-268), in its
+    final space-filling-curve order, computed on the GPU (vgpu_filter.hip)."""
+    ctx = ctx or context()
+    pc = np.ascontiguousarray(pc, np.float32).reshape(-1, 3)
+    out = np.zeros(max(pc.shape[0], 1), np.uint32)
+    cnt = C.c_size_t(0)
+    o, lo, up = (np.ascontiguousarray(v, np.float32).reshape(3) for v in (origin, workspace_min, workspace_max))
+    check(load().vgpu_filter_pointcloud_host(ctx.h, pc.ctypes.data_as(_lib.F32P), pc.shape[0], float(min_dist),
+                                             float(max_range), o.ctypes.data_as(_lib.F32P),
+                                             lo.ctypes.data_as(_lib.F32P), up.ctypes.data_as(_lib.F32P), int(cull),
+                                             out.ctypes.data_as(_lib.U32P), C.byref(cnt)), ctx.h)
+    return out[:cnt.value].copy()
+
+
+def filter_pointcloud(pc, min_dist: float, max_range: float, origin, workspace_min, workspace_max,
+                      cull: bool = True, ctx: Optional[Context] = None) -> np.ndarray:
+    """vamp.filter_pointcloud (bindings/common.hh, collision/filter.hh:175-268): the kept points."""
+    pc = np.ascontiguousarray(pc, np.float32).reshape(-1, 3)
+    return pc[filter_pointcloud_indices(pc, min_dist, max_range, origin, workspace_min, workspace_max, cull, ctx)]
+
+
 def halton(dim: int, first: int, n: int, ctx: Optional[Context] = None) -> np.ndarray:
     """rng::Halton<dim>::next draws first .. first+n-1 (1-based) of a fresh sampler, on the GPU."""
     ctx = ctx or context()

@@ -60,6 +60,10 @@ SIGNATURES = {
     "vgpu_env_pointcloud_arrays": (C.c_int, [VP, C.c_int, F32P, F32P, U32P, F32P]),
     "vgpu_pointcloud_collides": (C.c_int, [VP, VP, C.c_int, VP, VP, C.c_size_t, C.c_int, VP]),
     "vgpu_pointcloud_collides_host": (C.c_int, [VP, VP, C.c_int, F32P, F32P, C.c_size_t, C.c_int, U8P]),
+    "vgpu_filter_pointcloud": (C.c_int, [VP, VP, C.c_size_t, C.c_float, C.c_float, F32P, F32P, F32P, C.c_int, VP,
+                                         C.POINTER(C.c_size_t)]),
+    "vgpu_filter_pointcloud_host": (C.c_int, [VP, F32P, C.c_size_t, C.c_float, C.c_float, F32P, F32P, F32P,
+                                              C.c_int, U32P, C.POINTER(C.c_size_t)]),
     "vgpu_env_upload": (C.c_int, [VP]),
     "vgpu_env_attach": (C.c_int, [VP, F32P, F32P, C.c_size_t]),
     "vgpu_env_detach": (C.c_int, [VP]),
