@@ -54,13 +54,6 @@ __device__ inline uint32_t morton(uint32_t x, uint32_t y, uint32_t z)
     return spread3(x, 11, 0) | spread3(y, 11, 1) | spread3(z, 10, 2);
 }
 
-__device__ inline int f2ord(float f)
-{
-    const int i = __float_as_int(f);
-    return i >= 0 ? i : i ^ 0x7fffffff;
-}
-__device__ inline float ord2f(int i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
-
 __global__ void cull_kernel(const float* __restrict__ pc, uint32_t n, float sqrange, float ox, float oy, float oz,
                             float lx, float ly, float lz, float ux, float uy, float uz, int cull,
                             uint8_t* __restrict__ flag)
@@ -78,10 +71,13 @@ __global__ void iota_kernel(uint32_t* __restrict__ v, uint32_t n)
     if (i < n) v[i] = i;
 }
 
-// keys of the current list under coordinate permutation (c0, c1, c2); min/max into b->nmn/nmx
-__global__ void key_kernel(const float* __restrict__ pc, const uint32_t* __restrict__ idx, uint32_t len, int c0,
-                           int c1, int c2, Bounds* b, int* ordmm, uint32_t* __restrict__ key)
+// keys of the current list under coordinate permutation (c0, c1, c2); each block's coordinate
+// min/max to part[2 * blockIdx.x + {0, 1}] (no same-address atomics)
+__global__ __launch_bounds__(256) void key_kernel(const float* __restrict__ pc, const uint32_t* __restrict__ idx,
+                                                  uint32_t len, int c0, int c1, int c2, const Bounds* b,
+                                                  float* __restrict__ part, uint32_t* __restrict__ key)
 {
+    __shared__ float slo[4], sup[4];
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const float mn = b->mn, mx = b->mx;
     float lo = 3.4e38f, up = -3.4e38f;
@@ -91,26 +87,51 @@ __global__ void key_kernel(const float* __restrict__ pc, const uint32_t* __restr
         lo = fminf(p[0], fminf(p[1], p[2]));
         up = fmaxf(p[0], fmaxf(p[1], p[2]));
     }
-    // wave reduction, one atomic per wave
     for (int off = 32; off > 0; off >>= 1) {
         lo = fminf(lo, __shfl_xor(lo, off));
         up = fmaxf(up, __shfl_xor(up, off));
     }
     if ((threadIdx.x & 63) == 0) {
-        atomicMin(&ordmm[0], f2ord(lo));
-        atomicMax(&ordmm[1], f2ord(up));
+        slo[threadIdx.x >> 6] = lo;
+        sup[threadIdx.x >> 6] = up;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = fminf(fminf(slo[0], slo[1]), fminf(slo[2], slo[3]));
+        part[2 * blockIdx.x + 1] = fmaxf(fmaxf(sup[0], sup[1]), fmaxf(sup[2], sup[3]));
     }
 }
 
-// the next pass's bounds (filter.hh:262-263): start from nmn = mx, nmx = mn
-__global__ void bounds_kernel(Bounds* b, int* ordmm)
+// the next pass's bounds (filter.hh:262-263) from the block partials: nmn starts at mx, nmx at mn
+__global__ __launch_bounds__(1024) void bounds_kernel(Bounds* b, const float* __restrict__ part, uint32_t nparts)
 {
-    const float nmn = fminf(b->mx, ord2f(ordmm[0])), nmx = fmaxf(b->mn, ord2f(ordmm[1]));
-    const float mx = (float)((double)(nmx + b->mx) / 2.0), mn = (float)((double)(nmn + b->mn) / 2.0);
-    b->mn = mn;
-    b->mx = mx;
-    ordmm[0] = 0x7fffffff;
-    ordmm[1] = (int)0x80000000;
+    __shared__ float slo[16], sup[16];
+    float lo = 3.4e38f, up = -3.4e38f;
+    for (uint32_t k = threadIdx.x; k < nparts; k += blockDim.x) {
+        lo = fminf(lo, part[2 * k]);
+        up = fmaxf(up, part[2 * k + 1]);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        lo = fminf(lo, __shfl_xor(lo, off));
+        up = fmaxf(up, __shfl_xor(up, off));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        slo[threadIdx.x >> 6] = lo;
+        sup[threadIdx.x >> 6] = up;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 16; ++w) {
+            lo = fminf(lo, slo[w]);
+            up = fmaxf(up, sup[w]);
+        }
+        lo = fminf(slo[0], lo);
+        up = fmaxf(sup[0], up);
+        const float nmn = fminf(b->mx, lo), nmx = fmaxf(b->mn, up);
+        const float mx = (float)((double)(nmx + b->mx) / 2.0), mn = (float)((double)(nmn + b->mn) / 2.0);
+        b->mn = mn;
+        b->mx = mx;
+    }
 }
 
 // next(i): first sorted position j > i farther than min_dist from i, else len
@@ -130,16 +151,15 @@ __global__ void next_kernel(const float* __restrict__ pc, const uint32_t* __rest
     on[i] = (i == 0);
 }
 
-__global__ void double_kernel(const uint32_t* __restrict__ jin, uint32_t* __restrict__ jout,
-                              const uint8_t* __restrict__ onin, uint8_t* __restrict__ onout, uint32_t len)
+// one doubling round: chain flags only ever go 0 -> 1 (in place; a flag set earlier in the same
+// round only marks chain nodes sooner), jump pointers double into the other buffer
+__global__ void double_kernel(const uint32_t* __restrict__ jin, uint32_t* __restrict__ jout, uint8_t* on,
+                              uint32_t len)
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= len) return;
     const uint32_t j = jin[i];
-    if (onin[i]) {
-        onout[i] = 1;
-        if (j < len) onout[j] = 1;
-    }
+    if (on[i] && j < len) on[j] = 1;
     jout[i] = j < len ? jin[j] : len;
 }
 
@@ -171,9 +191,9 @@ extern "C" hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, fl
         return e;
     };
     uint32_t *idx, *key, *skey, *sidx, *j0, *j1, *nsel;
-    uint8_t *on0, *on1;
+    uint8_t* on0;
     Bounds* b;
-    int* ordmm;
+    float* part;
     FCHK(alloc((void**)&idx, 4 * n));
     FCHK(alloc((void**)&key, 4 * n));
     FCHK(alloc((void**)&skey, 4 * n));
@@ -181,10 +201,9 @@ extern "C" hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, fl
     FCHK(alloc((void**)&j0, 4 * n));
     FCHK(alloc((void**)&j1, 4 * n));
     FCHK(alloc((void**)&on0, n));
-    FCHK(alloc((void**)&on1, n));
     FCHK(alloc((void**)&nsel, 4));
     FCHK(alloc((void**)&b, sizeof(Bounds)));
-    FCHK(alloc((void**)&ordmm, 8));
+    FCHK(alloc((void**)&part, 8 * (size_t)blocks(n)));
     size_t tsel = 0, tsort = 0;
     FCHK(hipcub::DeviceSelect::Flagged(nullptr, tsel, idx, on0, sidx, nsel, N, s));
     FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, key, skey, idx, sidx, N, 0, 32, s));
@@ -209,29 +228,24 @@ extern "C" hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, fl
     hb.mn = fmin3(origin[0] - max_range, origin[1] - max_range, origin[2] - max_range);
     hb.mx = fmin3(origin[0] + max_range, origin[1] + max_range, origin[2] + max_range);  // sic, filter.hh:192
     hb.nmn = hb.nmx = 0.f;
-    const int hmm[2] = {0x7fffffff, (int)0x80000000};
     FCHK(hipMemcpyAsync(b, &hb, sizeof hb, hipMemcpyHostToDevice, s));
-    FCHK(hipMemcpyAsync(ordmm, hmm, 8, hipMemcpyHostToDevice, s));
 
     static const int perms[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
     uint32_t len = N;
     for (int pi = 0; pi < 6; ++pi) {
-        key_kernel<<<blocks(len), 256, 0, s>>>(d_pc, idx, len, perms[pi][0], perms[pi][1], perms[pi][2], b, ordmm,
+        key_kernel<<<blocks(len), 256, 0, s>>>(d_pc, idx, len, perms[pi][0], perms[pi][1], perms[pi][2], b, part,
                                                key);
-        bounds_kernel<<<1, 1, 0, s>>>(b, ordmm);
+        bounds_kernel<<<1, 1024, 0, s>>>(b, part, blocks(len));
         tb = tbytes;
         FCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, skey, idx, sidx, len, 0, 32, s));
         next_kernel<<<blocks(len), 256, 0, s>>>(d_pc, sidx, len, sqd, j0, on0);
         uint32_t *ja = j0, *jb = j1;
-        uint8_t *oa = on0, *ob = on1;
         for (uint32_t reach = 1; reach < len; reach <<= 1) {
-            FCHK(hipMemsetAsync(ob, 0, len, s));
-            double_kernel<<<blocks(len), 256, 0, s>>>(ja, jb, oa, ob, len);
+            double_kernel<<<blocks(len), 256, 0, s>>>(ja, jb, on0, len);
             uint32_t* tj = ja; ja = jb; jb = tj;
-            uint8_t* to = oa; oa = ob; ob = to;
         }
         tb = tbytes;
-        FCHK(hipcub::DeviceSelect::Flagged(tmp, tb, sidx, oa, idx, nsel, len, s));
+        FCHK(hipcub::DeviceSelect::Flagged(tmp, tb, sidx, on0, idx, nsel, len, s));
         FCHK(hipMemcpyAsync(&len, nsel, 4, hipMemcpyDeviceToHost, s));
         FCHK(hipStreamSynchronize(s));
     }
