@@ -17,7 +17,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <cstdint>
-#include <vector>
+#include <mutex>
 
 namespace {
 
@@ -165,6 +165,14 @@ __global__ void double_kernel(const uint32_t* __restrict__ jin, uint32_t* __rest
 
 inline unsigned blocks(size_t n) { return (unsigned)((n + 255) / 256); }
 
+constexpr int kMaxDevices = 64;
+struct Pool {
+    char* base = nullptr;
+    size_t cap = 0;
+};
+Pool g_pools[kMaxDevices];
+std::mutex g_pool_mu;
+
 }  // namespace
 
 #define FCHK(x)                                   \
@@ -183,33 +191,49 @@ extern "C" hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, fl
     if (n == 0) return hipSuccess;
     if (n > 0x7fffffffu) return hipErrorInvalidValue;
     const uint32_t N = (uint32_t)n;
-    std::vector<void*> bufs;
-    auto release = [&]() { for (void* p : bufs) (void)hipFree(p); };
-    auto alloc = [&](void** p, size_t bytes) {
-        hipError_t e = hipMalloc(p, bytes ? bytes : 1);
-        if (e == hipSuccess) bufs.push_back(*p);
-        return e;
-    };
-    uint32_t *idx, *key, *skey, *sidx, *j0, *j1, *nsel;
-    uint8_t* on0;
-    Bounds* b;
-    float* part;
-    FCHK(alloc((void**)&idx, 4 * n));
-    FCHK(alloc((void**)&key, 4 * n));
-    FCHK(alloc((void**)&skey, 4 * n));
-    FCHK(alloc((void**)&sidx, 4 * n));
-    FCHK(alloc((void**)&j0, 4 * n));
-    FCHK(alloc((void**)&j1, 4 * n));
-    FCHK(alloc((void**)&on0, n));
-    FCHK(alloc((void**)&nsel, 4));
-    FCHK(alloc((void**)&b, sizeof(Bounds)));
-    FCHK(alloc((void**)&part, 8 * (size_t)blocks(n)));
+    // scratch: one grow-only pool per device, reused across calls (calls are synchronous and
+    // serialised by the pool lock)
+    std::lock_guard<std::mutex> lock(g_pool_mu);
+    int dev = 0;
+    {
+        hipError_t e = hipGetDevice(&dev);
+        if (e != hipSuccess) return e;
+        if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+    }
+    auto release = []() {};
     size_t tsel = 0, tsort = 0;
-    FCHK(hipcub::DeviceSelect::Flagged(nullptr, tsel, idx, on0, sidx, nsel, N, s));
-    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, key, skey, idx, sidx, N, 0, 32, s));
-    void* tmp;
+    FCHK(hipcub::DeviceSelect::Flagged(nullptr, tsel, (uint32_t*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr,
+                                       (uint32_t*)nullptr, N, s));
+    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                            (uint32_t*)nullptr, (uint32_t*)nullptr, N, 0, 32, s));
     const size_t tbytes = tsel > tsort ? tsel : tsort;
-    FCHK(alloc(&tmp, tbytes));
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    const size_t sizes[11] = {4 * n, 4 * n, 4 * n, 4 * n, 4 * n, 4 * n, n, 4, sizeof(Bounds), 8 * (size_t)blocks(n),
+                              tbytes};
+    size_t total = 0;
+    for (size_t v : sizes) total += al(v ? v : 1);
+    Pool& pool = g_pools[dev];
+    if (pool.cap < total) {
+        if (pool.base) FCHK(hipFree(pool.base));
+        pool.base = nullptr;
+        pool.cap = 0;
+        FCHK(hipMalloc((void**)&pool.base, total));
+        pool.cap = total;
+    }
+    void* ptr[11];
+    {
+        char* q = pool.base;
+        for (int k = 0; k < 11; ++k) {
+            ptr[k] = q;
+            q += al(sizes[k] ? sizes[k] : 1);
+        }
+    }
+    uint32_t *idx = (uint32_t*)ptr[0], *key = (uint32_t*)ptr[1], *skey = (uint32_t*)ptr[2], *sidx = (uint32_t*)ptr[3];
+    uint32_t *j0 = (uint32_t*)ptr[4], *j1 = (uint32_t*)ptr[5], *nsel = (uint32_t*)ptr[7];
+    uint8_t* on0 = (uint8_t*)ptr[6];
+    Bounds* b = (Bounds*)ptr[8];
+    float* part = (float*)ptr[9];
+    void* tmp = ptr[10];
 
     // step 1 (filter.hh:194-214): kept indices first, the rest of the n-long list names point 0
     const float sqd = min_dist * min_dist, sqr = max_range * max_range;
