@@ -111,7 +111,16 @@ def cpu_baseline(starts, goals, seconds):
     return {"value": units / dt, "unit": "interpolants/s", "cores": threads, "kind": "port",
             "sample": f"{n} edges of the same workload ({int(units)} interpolants), oracle/vamp_oracle.c "
                       f"validate_motion (rake=8, early exit), {threads} threads, {dt:.1f} s",
-            "cpu_model": cpu_model(), "ok_fraction": float(ok.mean())}
+            "cpu_model": cpu_model(), "ok_fraction": float(ok.mean())}, ok, nb
+
+
+def parity_record(got_ok, got_n, ref_ok, ref_n, checker):
+    """GPU results vs the checker on the same edges: bitwise on ok[] and n_e."""
+    m = len(ref_ok)
+    g_ok = np.asarray(got_ok[:m]).astype(bool)
+    g_n = np.asarray(got_n[:m])
+    return {"edges_compared": int(m), "mismatches": int((g_ok != np.asarray(ref_ok).astype(bool)).sum()),
+            "n_mismatches": int((g_n != np.asarray(ref_n)).sum()), "checker": checker}
 
 
 def cpu_model():
@@ -240,6 +249,7 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     f_sample = float(fl.mean())
     achieved = f_sample * n / (kern_ms * 1e-3) / 1e12
     cpu = None
+    parity = None
     if not a.no_cpu and world == 1:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
         m0 = 16384
@@ -250,8 +260,13 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         m = int(min(a.draws, m0 * a.cpu_seconds / dt0))
         qc = op.robot_scale("fetch", op.halton(8, np.arange(1, m + 1)))
         t = time.perf_counter()
-        op.robot_fkcc_threads("fetch", oenv, qc, threads=threads)
+        okc = op.robot_fkcc_threads("fetch", oenv, qc, threads=threads)
         dt = time.perf_counter() - t
+        g_ok = valid[:m].cpu().numpy().astype(bool)
+        g_q = q[:m].cpu().numpy()
+        parity = {"draws_compared": int(m), "mismatches": int((g_ok != okc.astype(bool)).sum()),
+                  "sample_mismatches": int((g_q.view(np.uint32) != qc.view(np.uint32)).any(1).sum()),
+                  "checker": "oracle/vamp_oracle.c Halton<8> + scale + Fetch fkcc on the same draws"}
         cpu = {"value": m / dt, "unit": "samples/s", "cores": threads, "kind": "port",
                "sample": f"draws 1..{m} of the same stage (Halton<8> scaling on the host untimed), "
                          f"oracle/vamp_oracle.c Fetch fkcc, {threads} threads, {dt:.1f} s",
@@ -278,6 +293,7 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                      "traffic": None, "kernel_ms": kern_ms, "algorithmic_flops_per_sample": f_sample,
                      "algorithmic_bytes_per_sample": 8 * 4 + 1},
         "cpu_baseline": cpu,
+        "parity": parity,
     }
     print(json.dumps(line))
 
@@ -467,6 +483,7 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     kern_s = wall / a.steps
     achieved = f_edge * E / kern_s / 1e12
     cpu = None
+    parity = None
     if not a.no_cpu and world == 1:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
         sc_, gc_ = starts[: 1 << 18].cpu().numpy(), goals[: 1 << 18].cpu().numpy()
@@ -478,6 +495,8 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         t = time.perf_counter()
         okc, nbc = op.pair_validate_motions(oenv, sc_[:m], gc_[:m], threads=threads)
         dt = time.perf_counter() - t
+        parity = parity_record(okd.cpu().numpy(), nb.cpu().numpy(), okc, nbc,
+                               "oracle/vamp_oracle.c vo_pair_validate_motions on the same edges")
         cpu = {"value": float(8 * nbc.astype(np.int64).sum()) / dt, "unit": "interpolants/s", "cores": threads,
                "kind": "port", "sample": f"{m} edges of the same workload, oracle/vamp_oracle.c vo_pair_validate_motions, "
                                          f"{threads} threads, {dt:.1f} s", "cpu_model": cpu_model()}
@@ -494,6 +513,7 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
          "traffic": None, "algorithmic_flops_per_edge": f_edge, "step_ms": kern_s * 1e3},
         cpu)
+    line["parity"] = parity
     print(json.dumps(line))
 
 
@@ -530,6 +550,7 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     kern_s = wall / a.steps
     achieved = f_cfg * N / kern_s / 1e12
     cpu = None
+    parity = None
     if not a.no_cpu and world == 1:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
         qc = q[: 1 << 18].cpu().numpy()
@@ -539,8 +560,11 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         dt0 = max(time.perf_counter() - t, 1e-3)
         m = int(min(len(qc), n0 * a.cpu_seconds / dt0))
         t = time.perf_counter()
-        op.fkcc_threads(oenv, qc[:m], (0, 0, 0), threads)
+        okc = op.fkcc_threads(oenv, qc[:m], (0, 0, 0), threads)
         dt = time.perf_counter() - t
+        g_ok = ok[:m].cpu().numpy().astype(bool)
+        parity = {"configs_compared": int(m), "mismatches": int((g_ok != okc.astype(bool)).sum()),
+                  "checker": "oracle/vamp_oracle.c fkcc + CAPT on the same configurations"}
         cpu = {"value": m / dt, "unit": "configs/s", "cores": threads, "kind": "port",
                "sample": f"{m} configurations of the same workload, oracle/vamp_oracle.c fkcc + CAPT, {threads} threads, "
                          f"{dt:.1f} s", "cpu_model": cpu_model()}
@@ -555,6 +579,7 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "algorithmic_flops_per_config": f_cfg, "step_ms": kern_s * 1e3,
          "note": "gather/latency-bound descent + affordance scan; CAPT arrays (~4.7 MB) L2/MALL resident"},
         cpu)
+    line["parity"] = parity
     print(json.dumps(line))
 
 
@@ -666,10 +691,15 @@ def main():
         achieved_step = (f_head + f_tail) * E / (kern_ms * 1e-3) / 1e12
         tr = traffic_record(a.traffic_json)
         cpu = None
+        parity = None
         if not a.no_cpu and world == 1:
             s_cpu = starts[: 1 << 20].cpu().numpy()
             g_cpu = goals[: 1 << 20].cpu().numpy()
-            cpu = cpu_baseline(s_cpu, g_cpu, a.cpu_seconds)
+            cpu, ref_ok, ref_n = cpu_baseline(s_cpu, g_cpu, a.cpu_seconds)
+            parity = parity_record(ok.cpu().numpy(), nb.cpu().numpy(), ref_ok, ref_n,
+                                   "oracle/vamp_oracle.c validate_motion on the same edges (host threads)")
+            if parity["mismatches"] or parity["n_mismatches"]:
+                print(f"PARITY FAILURE: {parity}", file=sys.stderr)
         ms_step = wall_max / a.steps * 1e3
         line = {
             "metric": "validated edge-interpolants/sec (Panda 7-DOF FK+CC)",
@@ -714,6 +744,7 @@ def main():
             },
             "roofline_hbm_fk": fk_leg,
             "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(line))
     if world > 1:

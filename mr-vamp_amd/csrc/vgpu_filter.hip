@@ -19,6 +19,12 @@
 #include <cstdint>
 #include <mutex>
 
+// the block reductions below (shuffle offsets 32..1, one leader per 64 lanes) assume wave64,
+// which gfx950 always runs; any other device target is refused at compile time
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "vgpu_filter.hip: the min/max reductions are written for wave64 gfx950"
+#endif
+
 namespace {
 
 struct Bounds {
@@ -60,7 +66,8 @@ __global__ void cull_kernel(const float* __restrict__ pc, uint32_t n, float sqra
 {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float x = pc[3 * i], y = pc[3 * i + 1], z = pc[3 * i + 2];
+    const float* p = pc + 3 * (size_t)i;
+    const float x = p[0], y = p[1], z = p[2];
     flag[i] = !cull || (sql2_3(x, y, z, ox, oy, oz) < sqrange && lx <= x && x <= ux && ly <= y && y <= uy &&
                         lz <= z && z <= uz);
 }
@@ -171,7 +178,7 @@ struct Pool {
     size_t cap = 0;
 };
 Pool g_pools[kMaxDevices];
-std::mutex g_pool_mu;
+std::mutex g_pool_mu[kMaxDevices];  // one lock per device: calls on different devices run concurrently
 
 }  // namespace
 
@@ -192,14 +199,14 @@ extern "C" hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, fl
     if (n > 0x7fffffffu) return hipErrorInvalidValue;
     const uint32_t N = (uint32_t)n;
     // scratch: one grow-only pool per device, reused across calls (calls are synchronous and
-    // serialised by the pool lock)
-    std::lock_guard<std::mutex> lock(g_pool_mu);
+    // serialised per device by that device's pool lock)
     int dev = 0;
     {
         hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return e;
         if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
     }
+    std::lock_guard<std::mutex> lock(g_pool_mu[dev]);
     auto release = []() {};
     size_t tsel = 0, tsort = 0;
     FCHK(hipcub::DeviceSelect::Flagged(nullptr, tsel, (uint32_t*)nullptr, (uint8_t*)nullptr, (uint32_t*)nullptr,
@@ -239,13 +246,24 @@ extern "C" hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, fl
     const float sqd = min_dist * min_dist, sqr = max_range * max_range;
     cull_kernel<<<blocks(n), 256, 0, s>>>(d_pc, N, sqr, origin[0], origin[1], origin[2], ws_min[0], ws_min[1],
                                          ws_min[2], ws_max[0], ws_max[1], ws_max[2], cull, on0);
+    FCHK(hipGetLastError());
     iota_kernel<<<blocks(n), 256, 0, s>>>(key, N);
+    FCHK(hipGetLastError());
     size_t tb = tbytes;
     FCHK(hipcub::DeviceSelect::Flagged(tmp, tb, key, on0, idx, nsel, N, s));
     uint32_t hi = 0;
     FCHK(hipMemcpyAsync(&hi, nsel, 4, hipMemcpyDeviceToHost, s));
     FCHK(hipStreamSynchronize(s));
-    if (hi < N) FCHK(hipMemsetAsync(idx + hi, 0, 4 * (size_t)(N - hi), s));
+    // The reference's list keeps length n, its unfilled tail naming point 0 (filter.hh:194-214).
+    // Those N - hi copies share one key, so the stable sort keeps them consecutive, and the scan
+    // keeps at most the first of them (the rest are at distance 0 from it, or from the same last
+    // kept point); they add nothing to the pass's min/max either.  One copy is therefore exact,
+    // and it avoids an O((N - hi)^2) next-scan over a run of identical points.
+    uint32_t len = N;
+    if (hi < N) {
+        FCHK(hipMemsetAsync(idx + hi, 0, 4, s));
+        len = hi + 1;
+    }
 
     auto fmin3 = [](float a, float b2, float c) { float m = a; if (b2 < m) m = b2; if (c < m) m = c; return m; };
     Bounds hb;
@@ -255,17 +273,20 @@ extern "C" hipError_t vgpu_filter_pointcloud_run(const float* d_pc, size_t n, fl
     FCHK(hipMemcpyAsync(b, &hb, sizeof hb, hipMemcpyHostToDevice, s));
 
     static const int perms[6][3] = {{0, 1, 2}, {0, 2, 1}, {1, 0, 2}, {1, 2, 0}, {2, 0, 1}, {2, 1, 0}};
-    uint32_t len = N;
     for (int pi = 0; pi < 6; ++pi) {
         key_kernel<<<blocks(len), 256, 0, s>>>(d_pc, idx, len, perms[pi][0], perms[pi][1], perms[pi][2], b, part,
                                                key);
+        FCHK(hipGetLastError());
         bounds_kernel<<<1, 1024, 0, s>>>(b, part, blocks(len));
+        FCHK(hipGetLastError());
         tb = tbytes;
         FCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, skey, idx, sidx, len, 0, 32, s));
         next_kernel<<<blocks(len), 256, 0, s>>>(d_pc, sidx, len, sqd, j0, on0);
+        FCHK(hipGetLastError());
         uint32_t *ja = j0, *jb = j1;
         for (uint32_t reach = 1; reach < len; reach <<= 1) {
             double_kernel<<<blocks(len), 256, 0, s>>>(ja, jb, on0, len);
+            FCHK(hipGetLastError());
             uint32_t* tj = ja; ja = jb; jb = tj;
         }
         tb = tbytes;

@@ -82,7 +82,7 @@ def test_cpp_mirror_compiles_and_links(lib, tmp_path):
 def test_cpp_mirror_validate_matches_oracle(lib, tmp_path, oracle):
     """The C++ mirror's planning::validate_motions<Panda_0_0> on the sphere cage equals the
     oracle's validate_motion on the same edges (margin-free: random edges; any disagreement
-    here would also show in test_gpu_parity)."""
+    here would also show in test_gpu_parity): bit-exact."""
     import numpy as np
     exe = _build_example(str(tmp_path))
     rng = np.random.default_rng(7)
@@ -103,7 +103,7 @@ def test_cpp_mirror_validate_matches_oracle(lib, tmp_path, oracle):
     py_ok, _ = vamp_amd.panda_0_0.validate_batch(s, g, env)
     assert np.array_equal(got, np.asarray(py_ok, bool))
     want, _ = oracle.validate_motions(oracle.sphere_cage_env(), s, g)
-    assert (got != want).sum() <= 2  # near-margin edges only; exact masks are tested in test_gpu_parity
+    assert np.array_equal(got, want)  # same host, same rsqrt table: bit-exact
 
 
 def test_attachment_host_pose_identity():

@@ -5,9 +5,9 @@ reference-DAG fixture tests/golden/attach_panda_cage.npz (margin-filtered)."""
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import golden, host_fixture
 from test_gpu_parity import gpu_env_from_oracle, random_scene
-from test_oracle import same_rsqrt_host, stable
+from test_oracle import EDGE_MIN_COVERAGE, fixture_check, same_rsqrt_host, stable
 
 pytestmark = pytest.mark.gpu
 F = np.float32
@@ -33,7 +33,7 @@ def both(vamp, oracle, fx=None):
 
 
 def test_fkcc_attach_cage(vamp, oracle):
-    fx = golden("attach_panda_cage.npz")
+    fx = host_fixture("attach_panda_cage.npz", oracle)
     same = same_rsqrt_host(oracle, fx)
     oenv = oracle.sphere_cage_env()
     env = gpu_env_from_oracle(vamp, oenv)
@@ -44,13 +44,13 @@ def test_fkcc_attach_cage(vamp, oracle):
         got = vamp.PandaBase(*base).fkcc_attach_batch(q, env)
         assert np.array_equal(got, oracle.robot_fkcc_attach_threads("panda", oenv, o, q, base)), tag
         m = stable(fx["test_margin_" + tag], fx["cull_margin_" + tag], same)
-        assert np.array_equal(got[m], fx["valid_" + tag][m])
+        fixture_check(f"panda fkcc_attach cage {tag} (GPU)", got, fx["valid_" + tag], m, same)
         # validate(q) ignores attachments (bindings: fkcc, not fkcc_attach)
         assert np.array_equal(vamp.PandaBase(*base).fkcc_batch(q, env), oracle.fkcc_threads(oenv, q, base))
 
 
 def test_validate_attach_cage(vamp, oracle):
-    fx = golden("attach_panda_cage.npz")
+    fx = host_fixture("attach_panda_cage.npz", oracle)
     same = same_rsqrt_host(oracle, fx)
     oenv = oracle.sphere_cage_env()
     env = gpu_env_from_oracle(vamp, oenv)
@@ -61,7 +61,7 @@ def test_validate_attach_cage(vamp, oracle):
     assert np.array_equal(n, on) and np.array_equal(n, fx["n"])
     assert np.array_equal(ok, ook), "GPU != oracle on the same host"
     m = stable(fx["edge_test_margin"], fx["edge_cull_margin"], same)
-    assert np.array_equal(ok[m], fx["ok"][m])
+    fixture_check("panda attached validate_motion cage (GPU)", ok, fx["ok"], m, same, EDGE_MIN_COVERAGE)
     assert (~ok).sum() > 0 and ok.sum() > 0
     env.detach()
     ok2, _ = vamp.panda_0_0.validate_batch(fx["starts"], fx["goals"], env)
@@ -104,7 +104,7 @@ def _mbm_env(vamp, oracle, fx):
 def test_robot_attach(vamp, oracle, robot):
     """Fetch / UR5 fkcc_attach and the attached rake on their MBM scene: GPU == oracle on the
     same host, and == the reference-DAG fixture on the margin-filtered set."""
-    fx = golden(f"attach_{robot}.npz")
+    fx = host_fixture(f"attach_{robot}.npz", oracle)
     same = same_rsqrt_host(oracle, fx)
     oenv, env = _mbm_env(vamp, oracle, fx)
     a, o = both(vamp, oracle, fx)
@@ -113,12 +113,12 @@ def test_robot_attach(vamp, oracle, robot):
     got = r.fkcc_attach_batch(fx["q"], env)
     assert np.array_equal(got, oracle.robot_fkcc_attach_threads(robot, oenv, o, fx["q"]))
     m = stable(fx["test_margin"], fx["cull_margin"], same)
-    assert np.array_equal(got[m], fx["valid"][m])
+    fixture_check(f"{robot} fkcc_attach table_pick (GPU)", got, fx["valid"], m, same)
     ok, n = r.validate_batch(fx["starts"], fx["goals"], env)
     ook, on = oracle.robot_validate_motions_att(robot, oenv, o, fx["starts"], fx["goals"])
     assert np.array_equal(n, on) and np.array_equal(ok, ook)
     me = stable(fx["edge_test_margin"], fx["edge_cull_margin"], same)
-    assert np.array_equal(ok[me], fx["ok"][me])
+    fixture_check(f"{robot} attached validate_motion table_pick (GPU)", ok, fx["ok"], me, same, EDGE_MIN_COVERAGE)
 
 
 def test_baxter_attach_is_plain(vamp, oracle):

@@ -6,9 +6,9 @@ restatement (bit-exact, same host) and the reference-DAG fixtures of fetch/fk.hh
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import golden, host_fixture
 from test_gpu_parity import gpu_env_from_oracle
-from test_oracle import FK_TOL, same_rsqrt_host, stable
+from test_oracle import EDGE_MIN_COVERAGE, FK_TOL, fixture_check, same_rsqrt_host, stable
 from test_oracle_fetch import fetch_env
 
 pytestmark = pytest.mark.gpu
@@ -23,27 +23,27 @@ def vamp():
 
 
 def test_fetch_sphere_fk(vamp, oracle):
-    fx = golden("fk_fetch.npz")
+    fx = host_fixture("fk_fetch.npz", oracle)
     got = vamp.fetch.sphere_fk_batch(fx["q"])
     assert np.abs(got - fx["xyz"]).max() <= FK_TOL
     assert np.array_equal(got, oracle.robot_sphere_fk("fetch", fx["q"]))
 
 
 def test_fetch_fkcc_table_pick(vamp, oracle):
-    fx = golden("fetch_table_pick.npz")
+    fx = host_fixture("fetch_table_pick.npz", oracle)
     oenv = fetch_env(oracle, fx)
     env = gpu_env_from_oracle(vamp, oenv)
     got = vamp.fetch.fkcc_batch(fx["q"], env)
     assert np.array_equal(got, oracle.robot_fkcc_threads("fetch", oenv, fx["q"]))
     m = stable(fx["test_margin"], fx["cull_margin"], same_rsqrt_host(oracle, fx))
-    assert np.array_equal(got[m], fx["valid"][m])
+    fixture_check("fetch fkcc table_pick (GPU)", got, fx["valid"], m, same_rsqrt_host(oracle, fx))
     empty = vamp.Environment()
     got_e = vamp.fetch.fkcc_batch(fx["q_empty"], empty)
     assert np.array_equal(got_e, oracle.robot_fkcc_threads("fetch", oracle.Env(), fx["q_empty"]))
 
 
 def test_fetch_validate_table_pick(vamp, oracle):
-    fx = golden("fetch_table_pick.npz")
+    fx = host_fixture("fetch_table_pick.npz", oracle)
     oenv = fetch_env(oracle, fx)
     env = gpu_env_from_oracle(vamp, oenv)
     ok, n = vamp.fetch.validate_batch(fx["starts"], fx["goals"], env)
@@ -51,13 +51,13 @@ def test_fetch_validate_table_pick(vamp, oracle):
     assert np.array_equal(n, rn) and np.array_equal(n, fx["n"])
     assert np.array_equal(ok, rok)
     m = stable(fx["edge_test_margin"], fx["edge_cull_margin"], same_rsqrt_host(oracle, fx))
-    assert np.array_equal(ok[m], fx["ok"][m])
+    fixture_check("fetch validate_motion table_pick (GPU)", ok, fx["ok"], m, same_rsqrt_host(oracle, fx), EDGE_MIN_COVERAGE)
 
 
 def test_fetch_validate_long_edges(vamp, oracle):
     """raw full-range edges (n_e up to ~40 blocks) and zero-length edges, empty + table scene"""
     rng = np.random.default_rng(11)
-    fx = golden("fetch_table_pick.npz")
+    fx = host_fixture("fetch_table_pick.npz", oracle)
     oenv = fetch_env(oracle, fx)
     env = gpu_env_from_oracle(vamp, oenv)
     s = oracle.robot_scale("fetch", rng.random((3000, 8), dtype=F))
@@ -72,7 +72,7 @@ def test_fetch_validate_long_edges(vamp, oracle):
 
 def test_fetch_sample_fkcc(vamp, oracle):
     """PRM vertex stage: Halton<8> draws across the first reset, fused with scale + fkcc"""
-    fx = golden("fetch_table_pick.npz")
+    fx = host_fixture("fetch_table_pick.npz", oracle)
     oenv = fetch_env(oracle, fx)
     n, first = 8192, 996_000
     q, ok = vamp.fetch.sample_fkcc(first, n, gpu_env_from_oracle(vamp, oenv))
@@ -87,7 +87,7 @@ def test_roadmap_vertices_single_gpu(vamp, oracle):
     (one rank here; the all-gather itself is covered by tests/test_roadmap_dist.py)."""
     import torch
     from vamp_amd import roadmap
-    fx = golden("fetch_table_pick.npz")
+    fx = host_fixture("fetch_table_pick.npz", oracle)
     oenv = fetch_env(oracle, fx)
     env = gpu_env_from_oracle(vamp, oenv)
     n, first = 30000, 990_001

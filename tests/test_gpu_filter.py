@@ -44,3 +44,23 @@ def test_filter_matches_oracle(vamp, name, pc, md, rng_, cull):
 
 def test_filter_empty(vamp):
     assert vamp.filter_pointcloud_indices(np.zeros((0, 3), F), 0.1, 1.0, [0] * 3, [-1] * 3, [1] * 3).size == 0
+
+
+def test_filter_mostly_culled_1m(vamp):
+    """a 1M-point cloud wider than the workspace culls ~95 % of its points; the
+    reference's n-long list then ends in ~950k copies of point 0 (filter.hh:194-214).  The GPU
+    keeps one copy (exact, see vgpu_filter.hip) -- same indices as the oracle, and fast."""
+    import time
+    rng = np.random.default_rng(3)
+    n = 1 << 20
+    pc = np.empty((n, 3), F)
+    pc[:, :2] = rng.uniform(-3, 3, (n, 2))
+    pc[:, 2] = rng.uniform(-0.5, 2.0, n)
+    args = (0.005, 1.5, [0.0, 0.0, 0.5], [-1.2, -1.2, -1.2], [1.2, 1.2, 1.2], True)
+    vamp.filter_pointcloud_indices(pc[:4096], *args)  # warm the scratch pool
+    t = time.perf_counter()
+    got = vamp.filter_pointcloud_indices(pc, *args)
+    dt = time.perf_counter() - t
+    want = O.filter_pointcloud(pc, *args)
+    np.testing.assert_array_equal(got, want)
+    assert dt < 1.0, dt  # was O((N - kept)^2) before the tail collapse

@@ -9,8 +9,8 @@ see tests/test_oracle.py).
 import numpy as np
 import pytest
 
-from conftest import golden
-from test_oracle import FK_TOL, same_rsqrt_host, stable
+from conftest import golden, host_fixture
+from test_oracle import EDGE_MIN_COVERAGE, FK_TOL, fixture_check, same_rsqrt_host, stable
 
 pytestmark = pytest.mark.gpu
 F = np.float32
@@ -70,7 +70,7 @@ def test_rsqrt_table_matches_oracle_probe(vamp, oracle):
 
 @pytest.mark.parametrize("tag,base", [("b000", (0, 0, 0)), ("b220", (200, 200, 0)), ("b105", (100, -50, 5))])
 def test_sphere_fk(vamp, oracle, tag, base):
-    fx = golden("fk_panda.npz")
+    fx = host_fixture("fk_panda.npz", oracle)
     robot = vamp.PandaBase(*base)
     got = robot.sphere_fk_batch(fx["q"])
     ora = oracle.sphere_fk(fx["q"], base)
@@ -81,7 +81,7 @@ def test_sphere_fk(vamp, oracle, tag, base):
 
 
 def test_fkcc_cage(vamp, oracle):
-    fx = golden("fkcc_panda_cage.npz")
+    fx = host_fixture("fkcc_panda_cage.npz", oracle)
     oenv = oracle.sphere_cage_env()
     env = gpu_env_from_oracle(vamp, oenv)
     same = same_rsqrt_host(oracle, fx)
@@ -91,11 +91,11 @@ def test_fkcc_cage(vamp, oracle):
         got = robot.fkcc_batch(q, env)
         assert np.array_equal(got, oracle.fkcc_threads(oenv, q, base)), "GPU != oracle on the same host"
         m = stable(fx["test_margin" + sfx], fx["cull_margin" + sfx], same)
-        assert np.array_equal(got[m], fx["valid" + sfx][m])
+        fixture_check(f"panda fkcc cage{sfx or '_b000'} (GPU)", got, fx["valid" + sfx], m, same)
 
 
 def test_validate_motions_cage(vamp, oracle):
-    fx = golden("edges_panda_cage.npz")
+    fx = host_fixture("edges_panda_cage.npz", oracle)
     oenv = oracle.sphere_cage_env()
     env = gpu_env_from_oracle(vamp, oenv)
     robot = vamp.panda_0_0
@@ -103,9 +103,9 @@ def test_validate_motions_cage(vamp, oracle):
     ook, on = oracle.validate_motions(oenv, fx["starts"], fx["goals"], (0, 0, 0))
     assert np.array_equal(n, on) and np.array_equal(n, fx["n"])
     assert np.array_equal(ok, ook), "GPU != oracle on the same host"
-    same = same_rsqrt_host(oracle, golden("fkcc_panda_cage.npz"))
+    same = same_rsqrt_host(oracle, fx)
     m = stable(fx["test_margin"], fx["cull_margin"], same)
-    assert np.array_equal(ok[m], fx["ok"][m])
+    fixture_check("panda validate_motion cage edges (GPU)", ok, fx["ok"], m, same, EDGE_MIN_COVERAGE)
 
 
 @pytest.mark.parametrize("seed", [1, 2, 3])

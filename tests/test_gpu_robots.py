@@ -5,9 +5,9 @@ against the reference-DAG fixtures (tests/test_oracle_robots.py)."""
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import golden, host_fixture
 from test_gpu_parity import gpu_env_from_oracle
-from test_oracle import FK_TOL, same_rsqrt_host, stable
+from test_oracle import EDGE_MIN_COVERAGE, FK_TOL, fixture_check, same_rsqrt_host, stable
 from test_oracle_robots import CASES, scene_env
 
 pytestmark = pytest.mark.gpu
@@ -23,7 +23,7 @@ def vamp():
 
 @pytest.mark.parametrize("robot", sorted(CASES))
 def test_sphere_fk(vamp, oracle, robot):
-    fx = golden(f"fk_{robot}.npz")
+    fx = host_fixture(f"fk_{robot}.npz", oracle)
     got = getattr(vamp, robot).sphere_fk_batch(fx["q"])
     assert np.abs(got - fx["xyz"]).max() <= FK_TOL
     assert np.array_equal(got, oracle.robot_sphere_fk(robot, fx["q"]))
@@ -31,20 +31,20 @@ def test_sphere_fk(vamp, oracle, robot):
 
 @pytest.mark.parametrize("robot", sorted(CASES))
 def test_fkcc(vamp, oracle, robot):
-    fx = golden(CASES[robot])
+    fx = host_fixture(CASES[robot], oracle)
     oenv = scene_env(oracle, fx)
     rob = getattr(vamp, robot)
     got = rob.fkcc_batch(fx["q"], gpu_env_from_oracle(vamp, oenv))
     assert np.array_equal(got, oracle.robot_fkcc_threads(robot, oenv, fx["q"]))
     m = stable(fx["test_margin"], fx["cull_margin"], same_rsqrt_host(oracle, fx))
-    assert np.array_equal(got[m], fx["valid"][m])
+    fixture_check(f"{robot} fkcc {CASES[robot]} (GPU)", got, fx["valid"], m, same_rsqrt_host(oracle, fx))
     got_e = rob.fkcc_batch(fx["q_empty"], vamp.Environment())
     assert np.array_equal(got_e, oracle.robot_fkcc_threads(robot, oracle.Env(), fx["q_empty"]))
 
 
 @pytest.mark.parametrize("robot", sorted(CASES))
 def test_validate(vamp, oracle, robot):
-    fx = golden(CASES[robot])
+    fx = host_fixture(CASES[robot], oracle)
     oenv = scene_env(oracle, fx)
     env = gpu_env_from_oracle(vamp, oenv)
     rob = getattr(vamp, robot)
@@ -52,6 +52,8 @@ def test_validate(vamp, oracle, robot):
     rok, rn = oracle.robot_validate_motions(robot, oenv, fx["starts"], fx["goals"])
     assert np.array_equal(n, rn) and np.array_equal(n, fx["n"])
     assert np.array_equal(ok, rok)
+    me = stable(fx["edge_test_margin"], fx["edge_cull_margin"], same_rsqrt_host(oracle, fx))
+    fixture_check(f"{robot} validate_motion {CASES[robot]} (GPU)", ok, fx["ok"], me, same_rsqrt_host(oracle, fx), EDGE_MIN_COVERAGE)
     dim = oracle.ROBOTS[robot][1]
     rng = np.random.default_rng(13)
     s = oracle.robot_scale(robot, rng.random((1500, dim), dtype=F))
@@ -64,7 +66,7 @@ def test_validate(vamp, oracle, robot):
 
 @pytest.mark.parametrize("robot", sorted(CASES))
 def test_sample_fkcc(vamp, oracle, robot):
-    fx = golden(CASES[robot])
+    fx = host_fixture(CASES[robot], oracle)
     oenv = scene_env(oracle, fx)
     dim = oracle.ROBOTS[robot][1]
     n, first = 4096, 998_000

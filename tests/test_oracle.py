@@ -9,7 +9,7 @@ remainder reported.
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import golden, host_fixture
 
 F = np.float32
 FK_TOL = 1e-5          # north_star: FK sphere centres within 1e-5 abs
@@ -29,9 +29,29 @@ def same_rsqrt_host(oracle, fx):
     return kb == int(fx["rsqrt_kbits"]) and np.array_equal(lut, fx["rsqrt_lut"])
 
 
+MIN_COVERAGE = 0.9        # per-configuration masks: the margin filter may drop at most 10 %
+EDGE_MIN_COVERAGE = 0.7   # edges: an edge's margin is the minimum over all its interpolants' tests
+
+
+def fixture_check(name, got, ref, keep, same_host, min_coverage=MIN_COVERAGE):
+    """Compare `got` with a reference-DAG fixture on the margin-filtered set `keep`: exact there,
+    and the filter must keep at least `min_coverage` of the fixture.  Records coverage and the
+    flip counts inside / outside the filter (printed in the session summary, conftest.COVERAGE)."""
+    import conftest
+    got, ref, keep = np.asarray(got), np.asarray(ref), np.asarray(keep, bool)
+    diff = got != ref
+    rec = {"name": name, "total": int(keep.size), "kept": int(keep.sum()),
+           "coverage": float(keep.mean()) if keep.size else 1.0, "same_rsqrt": bool(same_host),
+           "flips_kept": int(diff[keep].sum()), "flips_dropped": int(diff[~keep].sum())}
+    conftest.COVERAGE.append(rec)
+    assert rec["flips_kept"] == 0, rec
+    assert rec["coverage"] >= min_coverage, rec
+    return rec
+
+
 @pytest.mark.parametrize("tag,base", [("b000", (0, 0, 0)), ("b220", (200, 200, 0)), ("b105", (100, -50, 5))])
 def test_sphere_fk_vs_reference_dag(oracle, tag, base):
-    fx = golden("fk_panda.npz")
+    fx = host_fixture("fk_panda.npz", oracle)
     got = oracle.sphere_fk(fx["q"], base)
     err = np.abs(got - fx[tag]).max()
     assert err <= FK_TOL, err
@@ -39,7 +59,7 @@ def test_sphere_fk_vs_reference_dag(oracle, tag, base):
 
 
 def test_fkcc_mask_vs_reference_dag(oracle):
-    fx = golden("fkcc_panda_cage.npz")
+    fx = host_fixture("fkcc_panda_cage.npz", oracle)
     env = oracle.sphere_cage_env()
     assert np.array_equal(env.arrays()["spheres"], fx["env_spheres"])
     same = same_rsqrt_host(oracle, fx)
@@ -48,27 +68,26 @@ def test_fkcc_mask_vs_reference_dag(oracle):
         got = oracle.fkcc_threads(env, q, base)
         ref = fx["valid" + sfx]
         m = stable(fx["test_margin" + sfx], fx["cull_margin" + sfx], same)
-        assert m.mean() > 0.97
-        assert np.array_equal(got[m], ref[m])
+        fixture_check(f"panda fkcc cage{sfx or '_b000'} (oracle)", got, ref, m, same)
         flips = int((got != ref).sum())
         assert flips <= max(2, int(2e-4 * len(q))), flips
 
 
 def test_validate_motion_vs_reference_dag(oracle):
-    fx = golden("edges_panda_cage.npz")
+    fx = host_fixture("edges_panda_cage.npz", oracle)
     env = oracle.sphere_cage_env()
     ok, n = oracle.validate_motions(env, fx["starts"], fx["goals"], (0, 0, 0))
     assert np.array_equal(n, fx["n"])
-    same = same_rsqrt_host(oracle, golden("fkcc_panda_cage.npz"))
+    same = same_rsqrt_host(oracle, fx)
     m = stable(fx["test_margin"], fx["cull_margin"], same)
-    assert np.array_equal(ok[m], fx["ok"][m])
+    fixture_check("panda validate_motion cage edges (oracle)", ok, fx["ok"], m, same, EDGE_MIN_COVERAGE)
     assert int((ok != fx["ok"]).sum()) <= 2
 
 
 def test_rake_block_equals_broadcast_single_config(oracle):
     """validate(q) == validate_motion(q, q) == fkcc of the broadcast block
     (bindings/common.hh:172-182): n == 1 and the block is q in every lane."""
-    fx = golden("fkcc_panda_cage.npz")
+    fx = host_fixture("fkcc_panda_cage.npz", oracle)
     env = oracle.sphere_cage_env()
     q = fx["q"][:512]
     ok, n = oracle.validate_motions(env, q, q, (0, 0, 0))
@@ -77,7 +96,7 @@ def test_rake_block_equals_broadcast_single_config(oracle):
 
 
 def test_empty_environment_is_self_collision_only(oracle):
-    fx = golden("fkcc_panda_cage.npz")
+    fx = host_fixture("fkcc_panda_cage.npz", oracle)
     q = fx["q"][:4096]
     empty = oracle.Env()
     v_empty = oracle.fkcc(empty, q)

@@ -9,7 +9,7 @@ turned 45 degrees).  Scene: the sphere cage.  Same tolerances as tests/test_orac
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import golden, host_fixture
 from test_oracle import stable, same_rsqrt_host
 
 
@@ -21,13 +21,13 @@ def _att(oracle, fx):
 
 
 def test_attachment_fixture_is_the_held_object(oracle):
-    fx = golden("attach_panda_cage.npz")
+    fx = host_fixture("attach_panda_cage.npz", oracle)
     ref = oracle.held_object().as_dict()
     assert np.array_equal(fx["att_tf"], ref["tf"]) and np.array_equal(fx["att_spheres"], ref["spheres"])
 
 
 def test_fkcc_attach_mask_vs_reference_dag(oracle):
-    fx = golden("attach_panda_cage.npz")
+    fx = host_fixture("attach_panda_cage.npz", oracle)
     same = same_rsqrt_host(oracle, fx)
     env = oracle.sphere_cage_env()
     att = _att(oracle, fx)
@@ -43,7 +43,7 @@ def test_fkcc_attach_mask_vs_reference_dag(oracle):
 
 
 def test_validate_motion_attach_vs_reference_dag(oracle):
-    fx = golden("attach_panda_cage.npz")
+    fx = host_fixture("attach_panda_cage.npz", oracle)
     same = same_rsqrt_host(oracle, fx)
     env = oracle.sphere_cage_env()
     ok, n = oracle.robot_validate_motions_att("panda", env, _att(oracle, fx), fx["starts"], fx["goals"])
@@ -81,7 +81,7 @@ def test_robot_fkcc_attach_vs_reference_dag(oracle, robot):
     from conftest import GOLD
     if not os.path.exists(os.path.join(GOLD, f"attach_{robot}.npz")):
         pytest.skip("fixture not generated")
-    fx = golden(f"attach_{robot}.npz")
+    fx = host_fixture(f"attach_{robot}.npz", oracle)
     same = same_rsqrt_host(oracle, fx)
     env = _mbm_env(oracle, fx)
     att = _att(oracle, fx)

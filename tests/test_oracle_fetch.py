@@ -9,8 +9,8 @@ set, near-boundary flips counted.
 """
 import numpy as np
 
-from conftest import golden
-from test_oracle import FK_TOL, stable, same_rsqrt_host
+from conftest import golden, host_fixture
+from test_oracle import EDGE_MIN_COVERAGE, FK_TOL, fixture_check, same_rsqrt_host, stable
 
 
 def fetch_env(oracle, fx):
@@ -21,7 +21,7 @@ def fetch_env(oracle, fx):
 
 
 def test_fetch_sphere_fk_vs_reference_dag(oracle):
-    fx = golden("fk_fetch.npz")
+    fx = host_fixture("fk_fetch.npz", oracle)
     got = oracle.robot_sphere_fk("fetch", fx["q"])
     err = np.abs(got - fx["xyz"]).max()
     assert err <= FK_TOL, err
@@ -29,7 +29,7 @@ def test_fetch_sphere_fk_vs_reference_dag(oracle):
 
 def test_fetch_env_rows_rebuild(oracle):
     """The committed scene rows are what mbm_env builds (sorted by min_distance)."""
-    fx = golden("fetch_table_pick.npz")
+    fx = host_fixture("fetch_table_pick.npz", oracle)
     a = fetch_env(oracle, fx).arrays()
     for k in ("cuboids", "capsules"):
         assert np.array_equal(a[k], fx["env_" + k])
@@ -37,26 +37,26 @@ def test_fetch_env_rows_rebuild(oracle):
 
 
 def test_fetch_fkcc_mask_vs_reference_dag(oracle):
-    fx = golden("fetch_table_pick.npz")
+    fx = host_fixture("fetch_table_pick.npz", oracle)
     same = same_rsqrt_host(oracle, fx)
     env = fetch_env(oracle, fx)
     got = oracle.robot_fkcc_threads("fetch", env, fx["q"])
     m = stable(fx["test_margin"], fx["cull_margin"], same)
     assert m.mean() > 0.9  # 2634 self tests per configuration: more of them near a boundary than Panda
-    assert np.array_equal(got[m], fx["valid"][m])
+    fixture_check("fetch fkcc table_pick (oracle)", got, fx["valid"], m, same)
     assert int((got != fx["valid"]).sum()) <= max(2, int(2e-4 * len(got)))
     got_e = oracle.robot_fkcc_threads("fetch", oracle.Env(), fx["q_empty"])
     assert np.array_equal(got_e[fx["test_margin_empty"] > 1e-4], fx["valid_empty"][fx["test_margin_empty"] > 1e-4])
 
 
 def test_fetch_validate_motion_vs_reference_dag(oracle):
-    fx = golden("fetch_table_pick.npz")
+    fx = host_fixture("fetch_table_pick.npz", oracle)
     same = same_rsqrt_host(oracle, fx)
     env = fetch_env(oracle, fx)
     ok, n = oracle.robot_validate_motions("fetch", env, fx["starts"], fx["goals"])
     assert np.array_equal(n, fx["n"])
     m = stable(fx["edge_test_margin"], fx["edge_cull_margin"], same)
-    assert np.array_equal(ok[m], fx["ok"][m])
+    fixture_check("fetch validate_motion table_pick (oracle)", ok, fx["ok"], m, same, EDGE_MIN_COVERAGE)
     assert int((ok != fx["ok"]).sum()) <= 2
 
 

@@ -11,7 +11,7 @@ spheres under-cover their links by up to 0.6 mm), so the margin filter here is 1
 """
 import numpy as np
 
-from conftest import golden
+from conftest import golden, host_fixture
 from test_oracle import same_rsqrt_host
 
 INTER_MARGIN = 1e-3
@@ -34,14 +34,14 @@ def pair_env(oracle, fx):
 
 
 def test_pair_scene_rows(oracle):
-    fx = golden("pair_scene.npz")
+    fx = host_fixture("pair_scene.npz", oracle)
     a = oracle.pair_scene().arrays()
     for k in ("spheres", "zcuboids"):
         assert np.array_equal(a[k], fx["env_" + k])
 
 
 def test_pair_fkcc_vs_dag_composition(oracle):
-    fx = golden("pair_scene.npz")
+    fx = host_fixture("pair_scene.npz", oracle)
     env = pair_env(oracle, fx)
     got = oracle.pair_fkcc_threads(env, fx["q"])
     m = (fx["test_margin"] > 1e-4) & (fx["inter_margin"] > INTER_MARGIN)
@@ -59,7 +59,7 @@ def test_pair_fkcc_vs_dag_composition(oracle):
 
 
 def test_pair_validate_vs_dag_composition(oracle):
-    fx = golden("pair_scene.npz")
+    fx = host_fixture("pair_scene.npz", oracle)
     env = pair_env(oracle, fx)
     ok, n = oracle.pair_validate_motions(env, fx["starts"], fx["goals"])
     assert np.array_equal(n, fx["n"])

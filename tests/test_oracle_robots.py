@@ -7,7 +7,7 @@ tests/test_oracle.py: FK within 1e-5, masks/edges bit-exact on the margin-filter
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import golden, host_fixture
 from test_oracle import FK_TOL, stable, same_rsqrt_host
 
 CASES = {"ur5": "ur5_table_pick.npz", "baxter": "baxter_bookshelf.npz"}
@@ -22,14 +22,14 @@ def scene_env(oracle, fx):
 
 @pytest.mark.parametrize("robot", sorted(CASES))
 def test_sphere_fk_vs_reference_dag(oracle, robot):
-    fx = golden(f"fk_{robot}.npz")
+    fx = host_fixture(f"fk_{robot}.npz", oracle)
     got = oracle.robot_sphere_fk(robot, fx["q"])
     assert np.abs(got - fx["xyz"]).max() <= FK_TOL
 
 
 @pytest.mark.parametrize("robot", sorted(CASES))
 def test_fkcc_vs_reference_dag(oracle, robot):
-    fx = golden(CASES[robot])
+    fx = host_fixture(CASES[robot], oracle)
     same = same_rsqrt_host(oracle, fx)
     got = oracle.robot_fkcc_threads(robot, scene_env(oracle, fx), fx["q"])
     m = stable(fx["test_margin"], fx["cull_margin"], same)
@@ -43,7 +43,7 @@ def test_fkcc_vs_reference_dag(oracle, robot):
 
 @pytest.mark.parametrize("robot", sorted(CASES))
 def test_validate_motion_vs_reference_dag(oracle, robot):
-    fx = golden(CASES[robot])
+    fx = host_fixture(CASES[robot], oracle)
     same = same_rsqrt_host(oracle, fx)
     ok, n = oracle.robot_validate_motions(robot, scene_env(oracle, fx), fx["starts"], fx["goals"])
     assert np.array_equal(n, fx["n"])

@@ -26,6 +26,22 @@ import numpy as np
 F = np.float32
 REMAT = False  # rebuild rotation matrices per check (A/B on MI355X: 5.80 -> 6.81 ms, off)
 
+# Emitted types.  The HIP kernels compute one configuration per lane in `float` with the
+# per-lane check bits in `uint32_t`; the CPU restatement (--cpu, mr-vamp_amd/csrc/cpu/) emits
+# the SAME expression text over 8-lane AVX2 vectors: `V` (one rake block, __m256) and `VB`
+# (sign-bit lane masks), so both are the same op sequence (vcpu_simd.hh supplies the operators).
+TY = {"f": "float", "b": "uint32_t", "b0": "0u", "qual": "__device__ __forceinline__", "cpu": False}
+TY_CPU = {"f": "V", "b": "VB", "b0": "VB()", "qual": "VCPU_INLINE", "cpu": True}
+
+
+def bdecl(name, comment=""):
+    """declaration of a zeroed check-bit accumulator"""
+    return f"{TY['b']} {name} = {TY['b0']};" + (f"  // {comment}" if comment else "")
+
+
+def xyzr_decl():
+    return "V X, Y, Z; float R;" if TY["cpu"] else "float X, Y, Z, R;"
+
 
 def flit(v) -> str:
     v = float(F(v))
@@ -69,7 +85,7 @@ class Emitter:
     def tmp(self, expr) -> SV:
         name = f"t{self.n}"
         self.n += 1
-        self.lines.append("    " * self.indent + f"const float {name} = {expr};")
+        self.lines.append("    " * self.indent + f"const {TY['f']} {name} = {expr};")
         self.flops += 1
         return SV("var", name=name)
 
@@ -243,9 +259,9 @@ class RobotGen:
         hdr = [
             f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
             f"// {E.flops} float ops (Horner sin/cos counted as 16 each).",
-            f"__device__ __forceinline__ void {self.name}_sphere_fk_store(",
-            "    " + ", ".join(f"float q{i}" for i in range(dim)) + ",",
-            "    float bx, float by, float bz, float* __restrict__ out, size_t ld)",
+            f"{TY['qual']} void {self.name}_sphere_fk_store(",
+            "    " + ", ".join(f"{TY['f']} q{i}" for i in range(dim)) + ",",
+            f"    float bx, float by, float bz, {TY['f']}* __restrict__ out, size_t ld)",
             "{",
         ]
         return "\n".join(hdr + E.lines + ["}", ""])
@@ -336,7 +352,7 @@ class RobotGen:
         """Children of a fired check; `on_hit` is the statement run when any lane's child fires."""
         spheres = self.m["spheres"]
         if kind == "env":
-            E.raw("uint32_t h = 0u;  // sign bit: this lane hit (a hit lane keeps no obstacle loop alive)")
+            E.raw(bdecl("h", "sign bit: this lane hit (a hit lane keeps no obstacle loop alive)"))
             for kid in ck["children"]:
                 sp = spheres[kid["sphere"]]
                 cw = self.world(fr.center(sp["frame"], sp["offset"]), kid["base"])
@@ -366,7 +382,7 @@ class RobotGen:
         spheres = self.m["spheres"]
         E.raw("{")
         E.indent += 1
-        E.raw("uint32_t h = 0u;  // OR of the children's test-value bits: sign bit = any child fired")
+        E.raw(bdecl("h", "OR of the children's test-value bits: sign bit = any child fired"))
         # Child pairs in chunks of CH distinct b-spheres: the chunk's b centres stay in
         # registers while each a-sphere centre is recomputed per chunk (bounded live set;
         # the OR is order-independent).
@@ -427,7 +443,7 @@ class RobotGen:
                 ga, gb = self.Frames(self, E, 0), self.Frames(self, E, dim)
                 sa_ = [i for i, sp in enumerate(spheres) if sp["link"] == links[la]]
                 sb_ = [i for i, sp in enumerate(spheres) if sp["link"] == links[lb]]
-                E.raw("uint32_t h = 0u;")
+                E.raw(bdecl("h"))
                 cb = {j: wc(gb.center(spheres[j]["frame"], spheres[j]["offset"]), "b") for j in sb_}
                 for i in sa_:
                     ca = wc(ga.center(spheres[i]["frame"], spheres[i]["offset"]), "a")
@@ -439,11 +455,11 @@ class RobotGen:
                 E.indent -= 1
                 E.raw("}")
         E.raw("return false;")
-        args = ", ".join(f"float q{i}" for i in range(2 * dim))
+        args = ", ".join(f"{TY['f']} q{i}" for i in range(2 * dim))
         hdr = [f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
                "// Two-arm composite: inter-robot sphere check, bounding-first.",
                "template <class Grp>",
-               f"__device__ __forceinline__ bool {self.name}_pair_inter(",
+               f"{TY['qual']} bool {self.name}_pair_inter(",
                f"    {args},",
                "    float ax, float ay, float az, float bx, float by, float bz)",
                "{"]
@@ -452,8 +468,8 @@ class RobotGen:
     def signature(self, ret, fname, extra=""):
         dim = self.m["dimension"]
         return [f"template <class Grp, bool EXT>",
-                f"__device__ __forceinline__ {ret} {self.name}_{fname}(",
-                f"    {extra}" + ", ".join(f"float q{i}" for i in range(dim)) + ",",
+                f"{TY['qual']} {ret} {self.name}_{fname}(",
+                f"    {extra}" + ", ".join(f"{TY['f']} q{i}" for i in range(dim)) + ",",
                 "    const EnvView& env, float bx, float by, float bz)",
                 "{"]
 
@@ -512,9 +528,9 @@ class RobotGen:
         m = self.m
         if o["kind"] == "attenv":
             E.raw("{  // attachment vs environment")
-            E.raw("    uint32_t h = 0u;")
+            E.raw("    " + bdecl("h"))
             E.raw("    for (int k = 0; k < env.n_att; ++k) {")
-            E.raw("        float X, Y, Z, R;")
+            E.raw("        " + xyzr_decl())
             E.raw("        att_sphere(env, ap, k, X, Y, Z, R);")
             E.raw("        h = env_bits<Grp, EXT>(env, X, Y, Z, R, h);")
             E.raw("    }")
@@ -525,9 +541,9 @@ class RobotGen:
         c, r = self.self_ent(fr, ck["ent"])
         E.raw(f"{{  // attachment vs {ck['link']} ({len(ck['children'])} children)")
         E.indent += 1
-        E.raw("uint32_t h = 0u;")
+        E.raw(bdecl("h"))
         E.raw("for (int k = 0; k < env.n_att; ++k) {")
-        E.raw("    float X, Y, Z, R;")
+        E.raw("    " + xyzr_decl())
         E.raw("    att_sphere(env, ap, k, X, Y, Z, R);")
         E.raw(f"    h |= self_bits({c[0].expr()}, {c[1].expr()}, {c[2].expr()}, {flit(r)}, X, Y, Z, R);")
         E.raw("}")
@@ -536,13 +552,13 @@ class RobotGen:
         else:
             E.raw("if (Grp::any_bits(h)) {")
             E.indent += 1
-            E.raw("uint32_t hc = 0u;")
+            E.raw(bdecl("hc"))
             spheres = m["spheres"]
             for sidx in ck["children"]:
                 sp = spheres[sidx]
                 cs = fr.center(sp["frame"], sp["offset"])
                 E.raw("for (int k = 0; k < env.n_att; ++k) {")
-                E.raw("    float X, Y, Z, R;")
+                E.raw("    " + xyzr_decl())
                 E.raw("    att_sphere(env, ap, k, X, Y, Z, R);")
                 E.raw(f"    hc |= self_bits({cs[0].expr()}, {cs[1].expr()}, {cs[2].expr()}, {flit(sp['radius'])}, "
                       "X, Y, Z, R);")
@@ -610,10 +626,12 @@ class RobotGen:
 
 
 def main():
-    global REMAT
+    global REMAT, TY
     if "--no-remat" in sys.argv:
         REMAT = False
         sys.argv.remove("--no-remat")
+    if "--cpu" in sys.argv:
+        TY = TY_CPU
     argv = [a for a in sys.argv if not a.startswith("--")]
     sys.argv[1:3] = argv[1:3]
     model = json.load(open(sys.argv[1]))
@@ -624,7 +642,11 @@ def main():
         vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model[key])
         consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
     out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
-    if "att_checks" in model:  # the attachment variant: its fkcc only (first rake block)
+    if TY["cpu"]:  # CPU restatement: sphere_fk + monolithic fkcc only (one rake block per call)
+        out = g.gen_sphere_fk() + "\n" + g.gen_fkcc()
+        if "att_checks" in model:
+            out = g.gen_fkcc()
+    elif "att_checks" in model:  # the attachment variant: its fkcc only (first rake block)
         out = g.gen_fkcc()
     elif len(model["check_order"]) <= 64:  # check masks: 32-bit up to 32 checks, 64-bit up to 64
         out += "\n" + g.gen_staged()

@@ -36,6 +36,26 @@ import fkhh_interp as fi  # noqa: E402
 import oracle_py as op  # noqa: E402
 
 GOLD = os.path.join(ROOT, "tests", "golden")
+# --lut FILE (an rsqrt table saved by tools/dump_host_rsqrt.py on another host, e.g. the GPU box's
+# EPYC): the same inputs, every collision output evaluated under THAT host's _mm256_rsqrt_ps cull,
+# written to tests/golden/alt_rsqrt/.  A test on that host then compares against it without the
+# cross-host cull-margin filter (tests/conftest.py:host_fixture).
+ALT_LUT = None
+ALT_DIR = os.path.join(GOLD, "alt_rsqrt")
+
+
+def host_lut():
+    """the rsqrt table the interpreted reference culls with: this host's, or --lut's"""
+    if ALT_LUT is not None:
+        return ALT_LUT
+    return op.rsqrt_probe()
+
+
+def out_path(name):
+    if ALT_LUT is not None:
+        os.makedirs(ALT_DIR, exist_ok=True)
+        return os.path.join(ALT_DIR, name)
+    return os.path.join(GOLD, name)
 PROBE = os.path.join(ROOT, "oracle", "_ref", "ref_probe")
 F = np.float32
 
@@ -75,8 +95,8 @@ def make_ref_pins(rng):
                          probe("halton", [0], 8, 24, 2_000_990).reshape(-1, 8)])
     k7 = np.concatenate([np.arange(1, 2049), np.arange(999_981, 1_000_021)])
     k8 = np.concatenate([k7, np.arange(2_000_991, 2_001_015)])
-    lut, kb = op.rsqrt_probe()
-    np.savez_compressed(os.path.join(GOLD, "ref_pins.npz"), sincos_q=q, sin=sc[:n], cos=sc[n:],
+    lut, kb = host_lut()
+    np.savez_compressed(out_path("ref_pins.npz"), sincos_q=q, sin=sc[:n], cos=sc[n:],
                         extent_in=ext_in, extent=ex[:8192], extent_root=ex[8192:], rsqrt_lut=lut, rsqrt_kbits=kb,
                         rake_starts=s, rake_goals=g, rake_out=rk, rake_blocks=NB, halton7=h7, halton7_k=k7,
                         halton8=h8, halton8_k=k8)
@@ -187,11 +207,11 @@ def make_robot(rng, robot, scene, out_name, n_cfg=16384, n_empty=4096, n_edges=1
     fk = fi.parse_function(src, r"inline void sphere_fk\(")
     cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
     dim = op.ROBOTS[robot][1]
-    lut, kb = op.rsqrt_probe()
+    lut, kb = host_lut()
     rs = fi.RsqrtHost(lut, kb)
     q = op.robot_scale(robot, rng.random((1024, dim), dtype=F))
     xyz, r = fi.run_sphere_fk(fk, q, (0, 0, 0))
-    np.savez_compressed(os.path.join(GOLD, f"fk_{robot}.npz"), q=q, radii=r.astype(F),
+    np.savez_compressed(out_path(f"fk_{robot}.npz"), q=q, radii=r.astype(F),
                         xyz=np.ascontiguousarray(np.transpose(xyz, (2, 1, 0))))
     print(f"fk_{robot}.npz")
     env = op.mbm_env(mbm_scene(robot, scene))
@@ -216,7 +236,7 @@ def make_robot(rng, robot, scene, out_name, n_cfg=16384, n_empty=4096, n_edges=1
     goals = np.concatenate([g, gb])
     starts[:4] = goals[:4]
     ok, n, tm, cm = interp_validate(cc, starts, goals, (0, 0, 0), envnp, rs, op.RESOLUTION[robot])
-    np.savez_compressed(os.path.join(GOLD, out_name), rsqrt_lut=lut, rsqrt_kbits=kb,
+    np.savez_compressed(out_path(out_name), rsqrt_lut=lut, rsqrt_kbits=kb,
                         **{"env_" + k: v for k, v in arr.items()},
                         q=q, valid=valid, test_margin=st.test_margin.astype(F), cull_margin=st.cull_margin.astype(F),
                         q_empty=qe, valid_empty=valid_e, test_margin_empty=st_e.test_margin.astype(F),
@@ -236,7 +256,7 @@ def make_attach(rng):
     src = open("/root/reference/src/impl/vamp/robots/panda/fk.hh").read()
     cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
     ca = fi.parse_function(src, r"inline bool interleaved_sphere_fk_attachment\(")
-    lut, kb = op.rsqrt_probe()
+    lut, kb = host_lut()
     rs = fi.RsqrtHost(lut, kb)
     env, envnp = sphere_cage()
     att = op.held_object()
@@ -256,7 +276,7 @@ def make_attach(rng):
     d = np.linalg.norm((g - s).astype(np.float64), axis=1)
     g = (s + (g - s) * np.minimum(1.0, 1.0 / np.maximum(d, 1e-9)).astype(F)[:, None]).astype(F)
     ok, n, tm, cm = interp_validate(cc, s, g, (0, 0, 0), envnp, rs, 32, cc_first=ca, att=ad)
-    np.savez_compressed(os.path.join(GOLD, "attach_panda_cage.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
+    np.savez_compressed(out_path("attach_panda_cage.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
                         att_tf=ad["tf"], att_spheres=ad["spheres"], starts=s, goals=g, ok=ok, n=n.astype(np.int32),
                         edge_test_margin=tm.astype(F), edge_cull_margin=cm.astype(F), **out)
     print("attach_panda_cage.npz", out["valid_b000"].mean(), out["plain_b000"].mean(), out["valid_b220"].mean(),
@@ -271,7 +291,7 @@ def make_attach_robot(rng, robot, scene, n_cfg=8192, n_edges=1024):
     cc = fi.parse_function(src, r"inline bool interleaved_sphere_fk\(")
     ca = fi.parse_function(src, r"inline bool interleaved_sphere_fk_attachment\(")
     dim = op.ROBOTS[robot][1]
-    lut, kb = op.rsqrt_probe()
+    lut, kb = host_lut()
     rs = fi.RsqrtHost(lut, kb)
     env = op.mbm_env(mbm_scene(robot, scene))
     envnp = envnp_of(env)
@@ -288,7 +308,7 @@ def make_attach_robot(rng, robot, scene, n_cfg=8192, n_edges=1024):
     g = (s + (g - s) * np.minimum(1.0, 1.0 / np.maximum(d, 1e-9)).astype(F)[:, None]).astype(F)
     ok, n, tm, cm = interp_validate(cc, s, g, (0, 0, 0), envnp, rs, op.RESOLUTION[robot], cc_first=ca, att=ad)
     arr = env.arrays()
-    np.savez_compressed(os.path.join(GOLD, f"attach_{robot}.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
+    np.savez_compressed(out_path(f"attach_{robot}.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
                         att_tf=ad["tf"], att_spheres=ad["spheres"], q=q, valid=valid, plain=plain,
                         test_margin=st.test_margin.astype(F), cull_margin=st.cull_margin.astype(F), starts=s, goals=g,
                         ok=ok, n=n.astype(np.int32), edge_test_margin=tm.astype(F), edge_cull_margin=cm.astype(F),
@@ -304,7 +324,7 @@ def make_l2_pins(rng):
         v = (rng.normal(size=(4096, dim)) * rng.choice([1e-3, 1.0, 30.0], size=(4096, 1))).astype(F)
         out[f"v{dim}"] = v
         out[f"d{dim}"] = probe("l2norm", v, dim)
-    np.savez_compressed(os.path.join(GOLD, "ref_pins_l2.npz"), **out)
+    np.savez_compressed(out_path("ref_pins_l2.npz"), **out)
 
 
 def pair_inter_flat(xa, xb):
@@ -332,7 +352,7 @@ def make_pair(rng):
     composition (AND of the three) independently of the C restatement's bounding-first order."""
     global RADII_PANDA
     fk, cc = fi.load_panda()
-    lut, kb = op.rsqrt_probe()
+    lut, kb = host_lut()
     rs = fi.RsqrtHost(lut, kb)
     env = op.pair_scene()
     envnp = envnp_of(env)
@@ -358,7 +378,7 @@ def make_pair(rng):
         sc = np.minimum(1.0, 1.0 / np.maximum(d, 1e-9)).astype(F)
         g[:, a] = (s[:, a] + (g[:, a] - s[:, a]) * sc[:, None]).astype(F)
     ok, n, etm = pair_interp_validate(fk, cc, s, g, envnp, rs)
-    np.savez_compressed(os.path.join(GOLD, "pair_scene.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
+    np.savez_compressed(out_path("pair_scene.npz"), rsqrt_lut=lut, rsqrt_kbits=kb,
                         **{"env_" + k: v for k, v in env.arrays().items()}, q=q, valid=valid,
                         valid_a=va, valid_b=vb, inter_hit=hit, inter_margin=imarg.astype(F), test_margin=tm.astype(F), cull_margin=cm.astype(F),
                         starts=s, goals=g, ok=ok, n=n.astype(np.int32), edge_test_margin=etm[0].astype(F),
@@ -406,7 +426,11 @@ def pair_interp_validate(fk, cc, starts, goals, envnp, rs):
 
 
 def main():
+    global ALT_LUT
     os.makedirs(GOLD, exist_ok=True)
+    if "--lut" in sys.argv:
+        z = np.load(sys.argv[sys.argv.index("--lut") + 1], allow_pickle=False)
+        ALT_LUT = (z["rsqrt_lut"].astype(np.uint32), int(z["rsqrt_kbits"]))
     if "--pair" in sys.argv:
         make_l2_pins(np.random.default_rng(20261017))
         make_pair(np.random.default_rng(20261018))
@@ -433,13 +457,16 @@ def main():
     if not os.path.exists(PROBE):
         subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "ref"])
     rng = np.random.default_rng(20251015)
-    make_ref_pins(rng)
-    print("ref_pins.npz")
-    make_ext_pins(np.random.default_rng(20261015))
-    print("ref_pins_ext.npz")
+    make_ref_pins(rng)  # (under --lut only for its rng draws: the pins are this host's probe)
+    if ALT_LUT is not None:
+        os.remove(out_path("ref_pins.npz"))
+    else:
+        print("ref_pins.npz")
+        make_ext_pins(np.random.default_rng(20261015))
+        print("ref_pins_ext.npz")
 
     fk, cc = fi.load_panda()
-    lut, kb = op.rsqrt_probe()
+    lut, kb = host_lut()
     rs = fi.RsqrtHost(lut, kb)
 
     # ---- FK sphere centres at both bases
@@ -448,8 +475,9 @@ def main():
     for tag, base in (("b000", (0, 0, 0)), ("b220", (200, 200, 0)), ("b105", (100, -50, 5))):
         xyz, r = fi.run_sphere_fk(fk, q, base)
         out[tag] = np.ascontiguousarray(np.transpose(xyz, (2, 1, 0)))
-    np.savez_compressed(os.path.join(GOLD, "fk_panda.npz"), q=q, radii=r.astype(F), **out)
-    print("fk_panda.npz")
+    if ALT_LUT is None:  # FK does not cull: nothing host-dependent
+        np.savez_compressed(out_path("fk_panda.npz"), q=q, radii=r.astype(F), **out)
+        print("fk_panda.npz")
 
     # ---- per-configuration masks (G = 1) on the sphere cage
     env, envnp = sphere_cage()
@@ -457,7 +485,7 @@ def main():
     valid, st = fi.run_fkcc(cc, q, (0, 0, 0), envnp, rs, G=1)
     q2 = op.scale(rng.random((8192, 7), dtype=F))
     valid2, st2 = fi.run_fkcc(cc, q2, (200, 200, 0), envnp, rs, G=1)
-    np.savez_compressed(os.path.join(GOLD, "fkcc_panda_cage.npz"), env_spheres=env.arrays()["spheres"], q=q,
+    np.savez_compressed(out_path("fkcc_panda_cage.npz"), env_spheres=env.arrays()["spheres"], q=q,
                         valid=valid, test_margin=st.test_margin.astype(F), cull_margin=st.cull_margin.astype(F),
                         q_b220=q2, valid_b220=valid2, test_margin_b220=st2.test_margin.astype(F),
                         cull_margin_b220=st2.cull_margin.astype(F), rsqrt_lut=lut, rsqrt_kbits=kb)
@@ -478,8 +506,9 @@ def main():
     goals = np.concatenate([g, gb])
     starts[:8] = goals[:8]  # zero-length edges
     ok, n, tm, cm = interp_validate(cc, starts, goals, (0, 0, 0), envnp, rs)
-    np.savez_compressed(os.path.join(GOLD, "edges_panda_cage.npz"), starts=starts, goals=goals, ok=ok,
-                        n=n.astype(np.int32), test_margin=tm.astype(F), cull_margin=cm.astype(F))
+    np.savez_compressed(out_path("edges_panda_cage.npz"), starts=starts, goals=goals, ok=ok,
+                        n=n.astype(np.int32), test_margin=tm.astype(F), cull_margin=cm.astype(F),
+                        **({"rsqrt_lut": lut, "rsqrt_kbits": kb} if ALT_LUT is not None else {}))
     print("edges_panda_cage.npz", ok[:E].mean(), ok[E:].mean(), n.max())
 
 
