@@ -14,9 +14,13 @@ limits), generated and filtered on the GPU before timing; inputs are resident in
 
 One step = one vgpu_validate_motions launch over the rank's whole edge batch (reference
 semantics: validate_motion per edge, 8-lane rake, early exit on the first colliding
-block).  Units = sum over edges of 8 * n_e (validate.hh:41).  Multi-GPU: each rank owns
-an independent shard of edges (weak scaling, no collective on the data path); the timed
-region is bracketed by barrier + synchronize and the max over ranks is reported.
+block).  Units (rake/early-exit mode) = 8 x the rake blocks the reference
+evaluates: every block of a valid edge, and an invalid edge's blocks through its first
+invalid one (counted by the CPU rake on the same edges, whose results must equal the GPU's
+edge for edge); the full count 8 * n_e of every edge is reported beside it.  Multi-GPU:
+each rank owns an independent shard of edges (weak scaling, no collective on the data
+path); the timed region is bracketed by barrier + synchronize and the max over ranks is
+reported.  CPU baseline: the build's AVX2 rake (mr-vamp_amd/csrc/cpu) on the host cores.
 """
 from __future__ import annotations
 
@@ -49,6 +53,8 @@ def parse():
     ap.add_argument("--edges", type=int, default=1 << 20, help="edges per GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU baseline sample time")
+    ap.add_argument("--oracle-edges", type=int, default=1 << 18,
+                    help="edges checked against the scalar oracle (the CPU rake checks every edge)")
     ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     ap.add_argument("--workload", default="validate", choices=["validate", "capt", "fetch_prm", "prm_edges", "pair"],
@@ -88,8 +94,40 @@ def make_edges(torch, vamp, env, robot, n_edges, seed, dev):
     return s, gl
 
 
-def cpu_baseline(starts, goals, seconds):
-    """The C restatement (oracle/, kind "port") on this host's cores, bounded sample."""
+def host_threads():
+    """CPU threads of the baseline legs: one per core of this rank's CPU share (16 on the GPU box,
+    fewer when the affinity set is smaller)."""
+    return max(1, min(16, len(os.sched_getaffinity(0))))
+
+
+def cpu_rake_baseline(vamp, env, robot, starts, goals, seconds):
+    """CPU reference timing: the build's own AVX2 rake (mr-vamp_amd/csrc/cpu/, one
+    ConfigurationBlock<8> per register, bit-identical to the oracle and the GPU), one std::thread
+    per core over static contiguous chunks, validate_motion with the reference's early exit.  The
+    sample is the bench's whole edge batch, repeated until ~`seconds` of work.  Returns the line's
+    cpu_baseline entry and the results of one pass (ok, n_e, blocks evaluated) for parity/units."""
+    threads = host_threads()
+    t = time.perf_counter()
+    ok, nb, ne = robot.cpu_validate_batch(starts, goals, env, threads=threads)
+    dt1 = max(time.perf_counter() - t, 1e-6)
+    reps = max(1, int(seconds / dt1))
+    t = time.perf_counter()
+    for _ in range(reps):
+        robot.cpu_validate_batch(starts, goals, env, threads=threads)
+    dt = (time.perf_counter() - t) / reps
+    ev = float(8 * ne.astype(np.int64).sum())
+    full = float(8 * nb.astype(np.int64).sum())
+    return {"value": ev / dt, "unit": "interpolants/s", "cores": threads, "kind": "port",
+            "counting": "rake_early_exit (8 x rake blocks evaluated, the reference's early exit)",
+            "value_full_mask_count": full / dt,
+            "per_core": ev / dt / threads,
+            "sample": f"the bench's {len(starts)} edges x {reps} passes ({dt:.3f} s per pass): mr-vamp_amd/csrc/cpu "
+                      f"AVX2 rake (vgpu_cpu_validate_motions), {threads} threads, static contiguous chunks",
+            "cpu_model": cpu_model(), "ok_fraction": float(ok.mean())}, ok, nb, ne
+
+
+def oracle_sample(starts, goals, n):
+    """The independent checker (oracle/vamp_oracle.c, scalar restatement) on the first n edges."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as op
 
@@ -97,30 +135,7 @@ def cpu_baseline(starts, goals, seconds):
     env = op.Env()
     for c in CAGE:
         env.add_sphere(c, np.float32(0.2))
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    # calibrate on a small slice, then run ~`seconds` worth
-    n0 = min(len(starts), 2048 * threads)
-    t = time.perf_counter()
-    op.validate_motions(env, starts[:n0], goals[:n0], (0, 0, 0), threads)
-    dt = max(time.perf_counter() - t, 1e-3)
-    n = int(min(len(starts), max(n0, n0 * seconds / dt)))
-    t = time.perf_counter()
-    ok, nb = op.validate_motions(env, starts[:n], goals[:n], (0, 0, 0), threads)
-    dt = time.perf_counter() - t
-    units = float(8 * nb.astype(np.int64).sum())
-    return {"value": units / dt, "unit": "interpolants/s", "cores": threads, "kind": "port",
-            "sample": f"{n} edges of the same workload ({int(units)} interpolants), oracle/vamp_oracle.c "
-                      f"validate_motion (rake=8, early exit), {threads} threads, {dt:.1f} s",
-            "cpu_model": cpu_model(), "ok_fraction": float(ok.mean())}, ok, nb
-
-
-def parity_record(got_ok, got_n, ref_ok, ref_n, checker):
-    """GPU results vs the checker on the same edges: bitwise on ok[] and n_e."""
-    m = len(ref_ok)
-    g_ok = np.asarray(got_ok[:m]).astype(bool)
-    g_n = np.asarray(got_n[:m])
-    return {"edges_compared": int(m), "mismatches": int((g_ok != np.asarray(ref_ok).astype(bool)).sum()),
-            "n_mismatches": int((g_n != np.asarray(ref_n)).sum()), "checker": checker}
+    return op.validate_motions(env, starts[:n], goals[:n], (0, 0, 0), host_threads())
 
 
 def cpu_model():
@@ -131,6 +146,15 @@ def cpu_model():
     except OSError:
         pass
     return "unknown"
+
+
+def parity_record(got_ok, got_n, ref_ok, ref_n, checker):
+    """GPU results vs the checker on the same edges: bitwise on ok[] and n_e."""
+    m = len(ref_ok)
+    g_ok = np.asarray(got_ok[:m]).astype(bool)
+    g_n = np.asarray(got_n[:m])
+    return {"edges_compared": int(m), "mismatches": int((g_ok != np.asarray(ref_ok).astype(bool)).sum()),
+            "n_mismatches": int((g_n != np.asarray(ref_n)).sum()), "checker": checker}
 
 
 def algorithmic_flops(starts, goals, n=512):
@@ -252,24 +276,26 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     parity = None
     if not a.no_cpu and world == 1:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
-        m0 = 16384
+        m0 = 65536
         t = time.perf_counter()
-        op.robot_fkcc_threads("fetch", oenv, op.robot_scale("fetch", op.halton(8, np.arange(1, m0 + 1))),
-                              threads=threads)
+        robot.cpu_fkcc_batch(op.robot_scale("fetch", op.halton(8, np.arange(1, m0 + 1))), env, threads=threads)
         dt0 = max(time.perf_counter() - t, 1e-3)
-        m = int(min(a.draws, m0 * a.cpu_seconds / dt0))
+        m = int(min(n, m0 * a.cpu_seconds / dt0))
         qc = op.robot_scale("fetch", op.halton(8, np.arange(1, m + 1)))
         t = time.perf_counter()
-        okc = op.robot_fkcc_threads("fetch", oenv, qc, threads=threads)
+        okc = robot.cpu_fkcc_batch(qc, env, threads=threads)
         dt = time.perf_counter() - t
         g_ok = valid[:m].cpu().numpy().astype(bool)
         g_q = q[:m].cpu().numpy()
-        parity = {"draws_compared": int(m), "mismatches": int((g_ok != okc.astype(bool)).sum()),
+        oo = op.robot_fkcc_threads("fetch", oenv, qc[:65536], threads=threads).astype(bool)
+        parity = {"draws_compared": int(m), "mismatches": int((g_ok != okc).sum()),
                   "sample_mismatches": int((g_q.view(np.uint32) != qc.view(np.uint32)).any(1).sum()),
-                  "checker": "oracle/vamp_oracle.c Halton<8> + scale + Fetch fkcc on the same draws"}
+                  "checker": "mr-vamp_amd/csrc/cpu AVX2 rake Fetch fkcc on the oracle's Halton<8> + scale draws",
+                  "oracle_mismatches": int((g_ok[:65536] != oo).sum()),
+                  "oracle_checker": "oracle/vamp_oracle.c Fetch fkcc, first 65536 draws"}
         cpu = {"value": m / dt, "unit": "samples/s", "cores": threads, "kind": "port",
                "sample": f"draws 1..{m} of the same stage (Halton<8> scaling on the host untimed), "
-                         f"oracle/vamp_oracle.c Fetch fkcc, {threads} threads, {dt:.1f} s",
+                         f"mr-vamp_amd/csrc/cpu AVX2 rake Fetch fkcc, {threads} threads, {dt:.1f} s",
                "cpu_model": cpu_model()}
     line = {
         "metric": "PRM vertex-stage samples/sec (Fetch 8-DOF Halton<8> + FK+CC, RCCL all-gather of valid vertices)",
@@ -473,8 +499,11 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, env, okd.data_ptr(), nb.data_ptr(), ctx)
 
     wall = timed_steps(a, torch, dist, dev, world, step)
-    units = float(8 * nb.long().sum().item())
+    # rake/early-exit units from the CPU rake on the same edges (bit-identical results), as configs[1]
+    _, c_nb, c_ne = robot.cpu_validate_batch(starts.cpu().numpy(), goals.cpu().numpy(), env, threads=host_threads())
+    units = float(8 * c_ne.astype(np.int64).sum())
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, units, dev, world)
+    _, units_full_all = reduce_over_ranks(dist, torch, wall, float(8 * c_nb.astype(np.int64).sum()), dev, world)
     if rank != 0:
         return
     s_np, g_np = starts[:256].cpu().numpy(), goals[:256].cpu().numpy()
@@ -486,20 +515,25 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     parity = None
     if not a.no_cpu and world == 1:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
-        sc_, gc_ = starts[: 1 << 18].cpu().numpy(), goals[: 1 << 18].cpu().numpy()
-        n0 = 1024 * threads
+        sc_, gc_ = starts.cpu().numpy(), goals.cpu().numpy()
+        n0 = 2048 * threads
         t = time.perf_counter()
-        op.pair_validate_motions(oenv, sc_[:n0], gc_[:n0], threads=threads)
+        robot.cpu_validate_batch(sc_[:n0], gc_[:n0], env, threads=threads)
         dt0 = max(time.perf_counter() - t, 1e-3)
         m = int(min(len(sc_), n0 * a.cpu_seconds / dt0))
         t = time.perf_counter()
-        okc, nbc = op.pair_validate_motions(oenv, sc_[:m], gc_[:m], threads=threads)
+        okc, nbc, nec = robot.cpu_validate_batch(sc_[:m], gc_[:m], env, threads=threads)
         dt = time.perf_counter() - t
-        parity = parity_record(okd.cpu().numpy(), nb.cpu().numpy(), okc, nbc,
-                               "oracle/vamp_oracle.c vo_pair_validate_motions on the same edges")
-        cpu = {"value": float(8 * nbc.astype(np.int64).sum()) / dt, "unit": "interpolants/s", "cores": threads,
-               "kind": "port", "sample": f"{m} edges of the same workload, oracle/vamp_oracle.c vo_pair_validate_motions, "
-                                         f"{threads} threads, {dt:.1f} s", "cpu_model": cpu_model()}
+        g_ok, g_nb = okd.cpu().numpy(), nb.cpu().numpy()
+        oo, on = op.pair_validate_motions(oenv, sc_[:8192], gc_[:8192], threads=threads)
+        parity = {"cpu_rake": parity_record(g_ok, g_nb, okc, nbc, f"mr-vamp_amd/csrc/cpu AVX2 rake, first {m} edges"),
+                  "oracle": parity_record(g_ok, g_nb, oo, on, "oracle/vamp_oracle.c vo_pair_validate_motions, "
+                                                              "first 8192 edges")}
+        cpu = {"value": float(8 * nec.astype(np.int64).sum()) / dt, "unit": "interpolants/s", "cores": threads,
+               "kind": "port", "counting": "rake_early_exit",
+               "value_full_mask_count": float(8 * nbc.astype(np.int64).sum()) / dt,
+               "sample": f"{m} edges of the same workload, mr-vamp_amd/csrc/cpu AVX2 rake (composite), "
+                         f"{threads} threads, {dt:.1f} s", "cpu_model": cpu_model()}
     line = contract_line(
         a, world, wall_max, units_all,
         "validated edge-interpolants/sec (2x Panda 14-DOF composite FK+CC with inter-robot collision)",
@@ -513,6 +547,8 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
          "traffic": None, "algorithmic_flops_per_edge": f_edge, "step_ms": kern_s * 1e3},
         cpu)
+    line["counting"] = "rake_early_exit (8 x rake blocks the reference evaluates)"
+    line["value_full_mask_count"] = units_full_all * a.steps / wall_max
     line["parity"] = parity
     print(json.dumps(line))
 
@@ -553,21 +589,25 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     parity = None
     if not a.no_cpu and world == 1:
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
-        qc = q[: 1 << 18].cpu().numpy()
-        n0 = 2048 * threads
+        qc = q.cpu().numpy()
+        n0 = 4096 * threads
         t = time.perf_counter()
-        op.fkcc_threads(oenv, qc[:n0], (0, 0, 0), threads)
+        robot.cpu_fkcc_batch(qc[:n0], env, threads=threads)
         dt0 = max(time.perf_counter() - t, 1e-3)
         m = int(min(len(qc), n0 * a.cpu_seconds / dt0))
         t = time.perf_counter()
-        okc = op.fkcc_threads(oenv, qc[:m], (0, 0, 0), threads)
+        okc = robot.cpu_fkcc_batch(qc[:m], env, threads=threads)
         dt = time.perf_counter() - t
-        g_ok = ok[:m].cpu().numpy().astype(bool)
-        parity = {"configs_compared": int(m), "mismatches": int((g_ok != okc.astype(bool)).sum()),
-                  "checker": "oracle/vamp_oracle.c fkcc + CAPT on the same configurations"}
+        g_ok = ok.cpu().numpy().astype(bool)
+        oo = op.fkcc_threads(oenv, qc[:65536], (0, 0, 0), threads).astype(bool)
+        parity = {"cpu_rake": {"configs_compared": int(m), "mismatches": int((g_ok[:m] != okc).sum()),
+                               "checker": "mr-vamp_amd/csrc/cpu AVX2 rake fkcc + CAPT"},
+                  "oracle": {"configs_compared": 65536, "mismatches": int((g_ok[:65536] != oo).sum()),
+                             "checker": "oracle/vamp_oracle.c fkcc + CAPT"}}
         cpu = {"value": m / dt, "unit": "configs/s", "cores": threads, "kind": "port",
-               "sample": f"{m} configurations of the same workload, oracle/vamp_oracle.c fkcc + CAPT, {threads} threads, "
-                         f"{dt:.1f} s", "cpu_model": cpu_model()}
+               "sample": f"{m} configurations of the same workload, mr-vamp_amd/csrc/cpu AVX2 rake fkcc (broadcast "
+                         f"block per configuration, CAPT collides_simd), {threads} threads, {dt:.1f} s",
+               "cpu_model": cpu_model()}
     line = contract_line(
         a, world, wall_max, units_all, "CAPT point-cloud collision queries/sec (Panda 7-DOF fkcc vs 10k-point cloud)",
         "configs/s", "weak", "synthetic (10k points on the cage spheres, seed 1; uniform Panda configurations)",
@@ -626,8 +666,18 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
-    units_local = float(8 * nb.long().sum().item())
     ok_frac = float(ok.float().mean().item())
+    # Units: the reference's early exit counts the interpolants of the rake blocks
+    # it evaluates -- up to and including an edge's first invalid block.  Those counts come from the
+    # CPU rake on the same edges (bit-identical results, and it reports the first failing block);
+    # the GPU's own results are compared with it edge by edge below.
+    s_all, g_all = starts.cpu().numpy(), goals.cpu().numpy()
+    if not a.no_cpu and world == 1:
+        cpu_leg, c_ok, c_nb, c_ne = cpu_rake_baseline(vamp, env, robot, s_all, g_all, a.cpu_seconds)
+    else:
+        c_ok, c_nb, c_ne = robot.cpu_validate_batch(s_all, g_all, env, threads=host_threads())
+    units_local = float(8 * c_ne.astype(np.int64).sum())       # rake_early_exit
+    units_full_local = float(8 * c_nb.astype(np.int64).sum())  # every interpolant of every edge
 
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
@@ -647,6 +697,7 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / a.steps  # HIP events on the launch stream
 
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, units_local, dev, world)
+    _, units_full_all = reduce_over_ranks(dist, torch, wall, units_full_local, dev, world)
 
     # secondary leg (untimed for the headline): the HBM-bound sphere_fk stream, 4M configs
     fk_leg = None
@@ -693,12 +744,14 @@ def main():
         cpu = None
         parity = None
         if not a.no_cpu and world == 1:
-            s_cpu = starts[: 1 << 20].cpu().numpy()
-            g_cpu = goals[: 1 << 20].cpu().numpy()
-            cpu, ref_ok, ref_n = cpu_baseline(s_cpu, g_cpu, a.cpu_seconds)
-            parity = parity_record(ok.cpu().numpy(), nb.cpu().numpy(), ref_ok, ref_n,
-                                   "oracle/vamp_oracle.c validate_motion on the same edges (host threads)")
-            if parity["mismatches"] or parity["n_mismatches"]:
+            cpu = cpu_leg
+            g_ok, g_nb = ok.cpu().numpy(), nb.cpu().numpy()
+            parity = {"cpu_rake": parity_record(g_ok, g_nb, c_ok, c_nb, "mr-vamp_amd/csrc/cpu AVX2 rake, every edge"),
+                      "oracle": parity_record(g_ok, g_nb, *oracle_sample(s_all, g_all, a.oracle_edges),
+                                              "oracle/vamp_oracle.c validate_motion (scalar restatement), first "
+                                              f"{a.oracle_edges} edges")}
+            bad = [k for k, v in parity.items() if v["mismatches"] or v["n_mismatches"]]
+            if bad:
                 print(f"PARITY FAILURE: {parity}", file=sys.stderr)
         ms_step = wall_max / a.steps * 1e3
         line = {
@@ -723,6 +776,9 @@ def main():
                 "edge_valid_fraction": ok_frac,
                 "parallelism": f"dp{world} (independent edge shards, no collective)",
             },
+            "counting": "rake_early_exit: 8 x rake blocks the reference evaluates (through an edge's first invalid "
+                        "block); value_full_mask_count counts 8 * n_e of every edge, evaluated or not",
+            "value_full_mask_count": units_full_all * a.steps / wall_max,
             "roofline": {
                 "kernel": "validate_motions step: staged bound/queue/children kernels of head and tail "
                           "(vgpu_staged.hip), one call",

@@ -217,6 +217,32 @@ int vgpu_build_roadmap_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *en
                             double space_measure, double gamma_scale, size_t *offsets, uint32_t *adj,
                             size_t adj_cap, size_t *n_adj, uint32_t *component);
 
+/* ---- CPU rake (host AVX2; no context, no GPU) --------------------------------------------------- */
+/* The reference's single-call entry points stay on the CPU (a GPU launch costs far more than one
+ * ~2 us edge): the same generated op sequence as the kernels over one 8-lane AVX2 register per
+ * rake block, culling with this host's own _mm256_rsqrt_ps -- bit-identical to the GPU path and to
+ * the oracle.  `env` may be a host-only environment (vgpu_env_create(NULL, ...)).  `threads` <= 0
+ * uses every hardware thread; batches are split into static contiguous chunks. */
+/* Robot::fkcc<8>(env, block) (robots/panda_base.hh:53-58): block = ConfigurationBlock<8>, dim rows
+ * of 8 lanes (SoA, lane l = configuration l); *valid = 1 when every lane is collision-free. */
+int vgpu_cpu_fkcc_block(const vgpu_robot *robot, vgpu_env *env, const float *block, int *valid);
+/* Robot::fkcc_attach<8>(env, block) (robots/panda_base.hh:61-65); requires an attachment. */
+int vgpu_cpu_fkcc_attach_block(const vgpu_robot *robot, vgpu_env *env, const float *block, int *valid);
+/* Robot::sphere_fk<8>(block, out) (robots/panda_base.hh:67-71): out[3][n_spheres][8] (x, y, z rows). */
+int vgpu_cpu_sphere_fk_block(const vgpu_robot *robot, const float *block, float *out);
+/* planning::validate_motion<Robot, 8, Robot::resolution>(start, goal, env) (validate.hh:67-75). */
+int vgpu_cpu_validate_motion(const vgpu_robot *robot, vgpu_env *env, const float *start, const float *goal,
+                             int *valid);
+/* Batches (host pointers): fkcc / fkcc_attach of each configuration broadcast to the rake, and
+ * validate_motion of each edge; n_blocks (optional) = n_e, n_evaluated (optional) = rake blocks
+ * the reference evaluates before the edge's result is known (early exit at the first invalid
+ * block: interpolants evaluated = 8 * n_evaluated). */
+int vgpu_cpu_fkcc(const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n, uint8_t *valid, int threads);
+int vgpu_cpu_fkcc_attach(const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n, uint8_t *valid,
+                         int threads);
+int vgpu_cpu_validate_motions(const vgpu_robot *robot, vgpu_env *env, const float *starts, const float *goals,
+                              size_t n_edges, uint8_t *ok, int32_t *n_blocks, int32_t *n_evaluated, int threads);
+
 /* ---- robot metadata ------------------------------------------------------------------------ */
 /* dimension, resolution, n_spheres of a robot kind (robots/panda_base.hh:19-23) */
 /* Point-cloud filter (replaces vamp::collision::filter_pointcloud, collision/filter.hh:175-268,

@@ -1,0 +1,277 @@
+// vcpu.cpp -- the CPU rake: validate_motion / fkcc / sphere_fk on the host, one reference
+// ConfigurationBlock<8> per AVX2 register (vcpu_simd.hh).
+//
+// Role: the reference's single-edge entry points -- Robot::fkcc<8>(env, block),
+// validate_motion<Robot, 8, res>(start, goal, env) -- stay on the CPU, because a GPU launch costs
+// far more than one ~2 us edge; planners call these (the C++ mirror include/vamp_gpu.hpp routes
+// its Robot concept here).  The batch forms, threaded over the host cores with static contiguous
+// chunks, are the CPU reference timing of bench.py (§8(d): "the build's own AVX2 restatement").
+// Both are bit-identical to the oracle and to the GPU kernels: the same generated op sequence
+// (tools/gen_kernels.py), the host's own _mm256_rsqrt_ps cull, the reference rake arithmetic.
+#include <algorithm>
+#include <cmath>
+#include <thread>
+#include <vector>
+
+#include "../vgpu_host_env.hh"
+#include "vcpu_robot.hh"
+
+namespace vcpu {
+namespace {
+
+struct Bound {
+    const RobotCpu* R = nullptr;
+    float base[6] = {0, 0, 0, 0, 0, 0};
+};
+
+// vgpu_api.cpp:check_robot, without a context: PandaBase<X100, Y100, Z100> bases (panda/fk.hh:
+// 109-111, static_cast<float>(x100) / 100.0f); Fetch / UR5 / Baxter have none
+int bind(const vgpu_robot* r, Bound& b)
+{
+    if (!r) return VGPU_ERR_INVALID_ARG;
+    switch (r->kind) {
+        case VGPU_ROBOT_PANDA: b.R = robot_panda(); break;
+        case VGPU_ROBOT_PANDA_PAIR: b.R = robot_panda_pair(); break;
+        case VGPU_ROBOT_FETCH: b.R = robot_fetch(); break;
+        case VGPU_ROBOT_UR5: b.R = robot_ur5(); break;
+        case VGPU_ROBOT_BAXTER: b.R = robot_baxter(); break;
+        default: return VGPU_ERR_UNSUPPORTED;
+    }
+    const bool panda = r->kind == VGPU_ROBOT_PANDA || r->kind == VGPU_ROBOT_PANDA_PAIR;
+    if (!panda && (r->base_x100 || r->base_y100 || r->base_z100)) return VGPU_ERR_INVALID_ARG;
+    b.base[0] = (float)r->base_x100 / 100.0f;
+    b.base[1] = (float)r->base_y100 / 100.0f;
+    b.base[2] = (float)r->base_z100 / 100.0f;
+    b.base[3] = (float)r->base2_x100 / 100.0f;
+    b.base[4] = (float)r->base2_y100 / 100.0f;
+    b.base[5] = (float)r->base2_z100 / 100.0f;
+    return VGPU_OK;
+}
+
+struct Env {
+    EnvView v;
+    bool ext = false, attached = false;
+};
+
+int view(vgpu_env* e, Env& out)
+{
+    if (!e) return VGPU_ERR_INVALID_ARG;
+    vgpu::HostEnvView h;
+    if (int rc = vgpu_env_host_view(e, &h)) return rc;
+    for (int t = 0; t < OBS_TYPES; ++t) {
+        out.v.obs[t] = h.obs[t];
+        out.v.n[t] = h.n[t];
+    }
+    out.v.hf = h.hf;
+    out.v.pc = h.pc;
+    out.v.base = h.base;
+    out.v.n_hf = h.n_hf;
+    out.v.n_pc = h.n_pc;
+    out.v.att = h.att;
+    out.v.n_att = h.n_att;
+    out.ext = h.n_hf > 0 || h.n_pc > 0;
+    out.attached = h.attached;
+    return VGPU_OK;
+}
+
+// FloatVector<dim>::l2_norm in the reference's lane order (vector/avx.hh:441-452 hsum; two
+// registers fma(lo, lo, hi * hi) first for dim > 8), then std::sqrt -- as oracle vo_l2_norm
+float l2_norm(const float* v, int dim)
+{
+    float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (dim <= 8) {
+        for (int i = 0; i < dim; ++i) s[i] = v[i] * v[i];
+    } else {
+        for (int i = 0; i < 8; ++i) {
+            const float hi = i + 8 < dim ? v[i + 8] : 0.0f;
+            s[i] = std::fma(v[i], v[i], hi * hi);
+        }
+    }
+    const float a = (s[0] + s[4]) + (s[2] + s[6]);
+    const float b = (s[1] + s[5]) + (s[3] + s[7]);
+    return std::sqrt(a + b);
+}
+
+// validate_motion<Robot, 8, Robot::resolution> (planning/validate.hh:23-75).  Returns validity;
+// *n = n_e (validate.hh:41), *evaluated = rake blocks evaluated before the result was known
+// (the reference's early exit: the first invalid block ends the edge).
+bool validate_one(const Bound& b, const Env& env, const float* start, const float* goal, int32_t* n,
+                  int32_t* evaluated)
+{
+    const RobotCpu& R = *b.R;
+    const int D = R.dim;
+    float v[kMaxDim];
+    for (int j = 0; j < D; ++j) v[j] = goal[j] - start[j];  // validate.hh:72
+    const float distance = l2_norm(v, D);                     // validate.hh:73
+    const V pct = _mm256_setr_ps(1.0f / 8, 2.0f / 8, 3.0f / 8, 4.0f / 8, 5.0f / 8, 6.0f / 8, 7.0f / 8, 1.0f);
+    V block[kMaxDim];
+    for (int j = 0; j < D; ++j) block[j] = fma(V(v[j]), pct, V(start[j]));  // validate.hh:37 (contracted)
+    float nf = std::ceil(distance / 8.0f * (float)R.resolution);            // validate.hh:41
+    if (!(nf > 1.0f)) nf = 1.0f;
+    const int32_t ne = nf < 2147483520.0f ? (int32_t)nf : 2147483520;
+    if (n) *n = ne;
+    // validate.hh:43: the first block through fkcc_attach when the environment has an attachment
+    bool valid = (env.attached && R.fkcc_attach) ? R.fkcc_attach(block, env.v, b.base, env.ext)
+                                                 : R.fkcc(block, env.v, b.base, env.ext);
+    int32_t done = 1;
+    if (valid && ne > 1) {
+        V back[kMaxDim];
+        for (int j = 0; j < D; ++j) back[j] = V(v[j] / (float)(8 * (int64_t)ne));  // validate.hh:50
+        for (int32_t i = 1; i < ne; ++i) {
+            for (int j = 0; j < D; ++j) block[j] = block[j] - back[j];  // validate.hh:52-56
+            ++done;
+            if (!R.fkcc(block, env.v, b.base, env.ext)) {
+                valid = false;
+                break;
+            }
+        }
+    }
+    if (evaluated) *evaluated = done;
+    return valid;
+}
+
+// static contiguous chunks, one std::thread each (SURVEY §8(d) CPU reference timing)
+template <class Fn>
+void parallel_for(size_t n, int threads, Fn fn)
+{
+    const size_t T = (size_t)std::max(1, std::min<int>(threads, (int)std::max<size_t>(1, n)));
+    if (T == 1) {
+        fn(0, n);
+        return;
+    }
+    std::vector<std::thread> pool;
+    pool.reserve(T);
+    for (size_t t = 0; t < T; ++t) {
+        const size_t lo = n * t / T, hi = n * (t + 1) / T;
+        pool.emplace_back([=] { fn(lo, hi); });
+    }
+    for (auto& th : pool) th.join();
+}
+
+int resolve_threads(int threads)
+{
+    if (threads > 0) return threads;
+    const unsigned hw = std::thread::hardware_concurrency();
+    return hw ? (int)hw : 1;
+}
+
+}  // namespace
+}  // namespace vcpu
+
+using namespace vcpu;
+
+extern "C" int vgpu_cpu_fkcc_block(const vgpu_robot* robot, vgpu_env* env, const float* block, int* valid)
+{
+    Bound b;
+    Env e;
+    if (!block || !valid) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    if (int rc = view(env, e)) return rc;
+    V q[kMaxDim];
+    for (int j = 0; j < b.R->dim; ++j) q[j] = V(_mm256_loadu_ps(block + 8 * j));
+    *valid = b.R->fkcc(q, e.v, b.base, e.ext) ? 1 : 0;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_cpu_fkcc_attach_block(const vgpu_robot* robot, vgpu_env* env, const float* block, int* valid)
+{
+    Bound b;
+    Env e;
+    if (!block || !valid) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    if (!b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
+    if (int rc = view(env, e)) return rc;
+    if (!e.attached) return VGPU_ERR_INVALID_ARG;
+    V q[kMaxDim];
+    for (int j = 0; j < b.R->dim; ++j) q[j] = V(_mm256_loadu_ps(block + 8 * j));
+    *valid = b.R->fkcc_attach(q, e.v, b.base, e.ext) ? 1 : 0;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_cpu_sphere_fk_block(const vgpu_robot* robot, const float* block, float* out)
+{
+    Bound b;
+    if (!block || !out) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    V q[kMaxDim];
+    for (int j = 0; j < b.R->dim; ++j) q[j] = V(_mm256_loadu_ps(block + 8 * j));
+    std::vector<V> o((size_t)3 * b.R->n_spheres);
+    b.R->sphere_fk(q, b.base, o.data());
+    for (size_t i = 0; i < o.size(); ++i) _mm256_storeu_ps(out + 8 * i, o[i].v);
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_cpu_validate_motion(const vgpu_robot* robot, vgpu_env* env, const float* start,
+                                        const float* goal, int* valid)
+{
+    Bound b;
+    Env e;
+    if (!start || !goal || !valid) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    if (int rc = view(env, e)) return rc;
+    if (e.attached && !b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
+    *valid = validate_one(b, e, start, goal, nullptr, nullptr) ? 1 : 0;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_cpu_fkcc(const vgpu_robot* robot, vgpu_env* env, const float* q, size_t n, uint8_t* valid,
+                             int threads)
+{
+    Bound b;
+    Env e;
+    if ((n && (!q || !valid))) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    if (int rc = view(env, e)) return rc;
+    const int D = b.R->dim;
+    parallel_for(n, resolve_threads(threads), [&](size_t lo, size_t hi) {
+        V blk[kMaxDim];
+        for (size_t i = lo; i < hi; ++i) {
+            for (int j = 0; j < D; ++j) blk[j] = V(q[(size_t)D * i + j]);  // the broadcast block of validate(q)
+            valid[i] = b.R->fkcc(blk, e.v, b.base, e.ext) ? 1 : 0;
+        }
+    });
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_cpu_fkcc_attach(const vgpu_robot* robot, vgpu_env* env, const float* q, size_t n,
+                                    uint8_t* valid, int threads)
+{
+    Bound b;
+    Env e;
+    if ((n && (!q || !valid))) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    if (!b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
+    if (int rc = view(env, e)) return rc;
+    if (!e.attached) return VGPU_ERR_INVALID_ARG;
+    const int D = b.R->dim;
+    parallel_for(n, resolve_threads(threads), [&](size_t lo, size_t hi) {
+        V blk[kMaxDim];
+        for (size_t i = lo; i < hi; ++i) {
+            for (int j = 0; j < D; ++j) blk[j] = V(q[(size_t)D * i + j]);
+            valid[i] = b.R->fkcc_attach(blk, e.v, b.base, e.ext) ? 1 : 0;
+        }
+    });
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_cpu_validate_motions(const vgpu_robot* robot, vgpu_env* env, const float* starts,
+                                         const float* goals, size_t n, uint8_t* ok, int32_t* n_blocks,
+                                         int32_t* n_evaluated, int threads)
+{
+    Bound b;
+    Env e;
+    if (n && (!starts || !goals || !ok)) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    if (int rc = view(env, e)) return rc;
+    if (e.attached && !b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
+    const int D = b.R->dim;
+    parallel_for(n, resolve_threads(threads), [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            int32_t ne = 0, ev = 0;
+            ok[i] = validate_one(b, e, starts + (size_t)D * i, goals + (size_t)D * i, &ne, &ev) ? 1 : 0;
+            if (n_blocks) n_blocks[i] = ne;
+            if (n_evaluated) n_evaluated[i] = ev;
+        }
+    });
+    return VGPU_OK;
+}

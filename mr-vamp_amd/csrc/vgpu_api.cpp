@@ -14,12 +14,14 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
 #include "../../include/vamp_gpu.h"
 #include "vgpu_capt.hh"
 #include "vgpu_device.hh"
+#include "vgpu_host_env.hh"
 #include "vgpu_ops.hh"
 
 extern "C" {
@@ -248,7 +250,10 @@ struct vgpu_env {
     std::array<float, 7> att_tf{};
     std::vector<std::array<float, 4>> att_spheres;
     size_t hf_off = 0, pc_off = 0, att_off = 0;
-    bool dirty = true;
+    bool dirty = true;       // device copy stale
+    bool host_dirty = true;  // host copy (the CPU rake's view, csrc/cpu/) stale
+    std::vector<float> host_blob;
+    std::mutex host_mu;
     float* dev = nullptr;
     size_t dev_floats = 0;
     size_t off[OBS_TYPES] = {0, 0, 0, 0, 0};
@@ -493,7 +498,7 @@ extern "C" int vgpu_env_add_sphere(vgpu_env* e, const float c[3], float r)
 {
     if (!e || !c || !finite3(c) || !std::isfinite(r)) return VGPU_ERR_INVALID_ARG;
     e->spheres.push_back({c[0], c[1], c[2], r, sphere_min_distance(c[0], c[1], c[2], r)});
-    e->dirty = true;
+    e->dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -508,7 +513,7 @@ extern "C" int vgpu_env_add_cuboid_axes(vgpu_env* e, const float c[3], const flo
         e->zcuboids.push_back(row);
     else
         e->cuboids.push_back(row);
-    e->dirty = true;
+    e->dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -535,7 +540,7 @@ extern "C" int vgpu_env_add_capsule_endpoints(vgpu_env* e, const float p1[3], co
         e->zcapsules.push_back(row);
     else
         e->capsules.push_back(row);
-    e->dirty = true;
+    e->dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -578,7 +583,7 @@ extern "C" int vgpu_env_add_heightfield(vgpu_env* e, const float center[3], cons
     h.yd = yd;
     h.data.assign(data, data + xd * yd);
     e->heightfields.push_back(std::move(h));
-    e->dirty = true;
+    e->dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -593,7 +598,7 @@ extern "C" int vgpu_env_add_pointcloud(vgpu_env* e, const float* points, size_t 
     e->pointclouds.emplace_back();
     vgpu::capt_build(points, n, r_min, r_max, r_point, e->pointclouds.back());
     if (build_ns) *build_ns = e->pointclouds.back().build_ns;
-    e->dirty = true;
+    e->dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -646,7 +651,7 @@ extern "C" int vgpu_env_attach(vgpu_env* e, const float tf[7], const float* sphe
     for (size_t k = 0; k < n; ++k)
         for (int i = 0; i < 4; ++i) e->att_spheres[k][i] = spheres[4 * k + i];
     e->attached = true;
-    e->dirty = true;
+    e->dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -655,22 +660,22 @@ extern "C" int vgpu_env_detach(vgpu_env* e)
     if (!e) return VGPU_ERR_INVALID_ARG;
     e->attached = false;
     e->att_spheres.clear();
-    e->dirty = true;
+    e->dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
-extern "C" int vgpu_env_upload(vgpu_env* e)
+// The environment as one float blob: per obstacle type, records sorted by min_distance
+// (environment.hh:40-66) followed by kObsPad sentinels (md = +inf), then heightfield / point-cloud
+// headers and arrays, then the attachment.  The same layout serves the device (vgpu_env_upload)
+// and the CPU rake (vgpu_env_host_view); offsets are recorded in the environment.
+static int build_blob(vgpu_env* e, std::vector<float>& blob)
 {
-    if (!e) return VGPU_ERR_INVALID_ARG;
-    vgpu_ctx* c = e->ctx;
-    if (!c) return VGPU_ERR_INVALID_ARG;  // host-only environment
-    if (!e->dirty && e->dev) return VGPU_OK;
     sort_md(e->spheres);
     sort_md(e->capsules);
     sort_md(e->zcapsules);
     sort_md(e->cuboids);
     sort_md(e->zcuboids);
-    std::vector<float> blob;
+    blob.clear();
     auto put = [&](auto& v, int type, int np) {
         const int S = kObsStride[type];
         e->off[type] = blob.size();
@@ -741,7 +746,19 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     blob.resize(blob.size() + kAttHdr, 0.0f);
     std::copy(e->att_tf.begin(), e->att_tf.end(), blob.begin() + e->att_off);
     for (const auto& sp : e->att_spheres) blob.insert(blob.end(), sp.begin(), sp.end());
-    if (blob.size() >= ((size_t)1 << 32)) return fail(c, VGPU_ERR_INVALID_ARG, "environment larger than 16 GiB");
+    if (blob.size() >= ((size_t)1 << 32)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "environment larger than 16 GiB");
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_upload(vgpu_env* e)
+{
+    if (!e) return VGPU_ERR_INVALID_ARG;
+    vgpu_ctx* c = e->ctx;
+    if (!c) return VGPU_ERR_INVALID_ARG;  // host-only environment
+    if (!e->dirty && e->dev) return VGPU_OK;
+    std::lock_guard<std::mutex> lock(e->host_mu);  // build_blob re-sorts the host rows
+    std::vector<float> blob;
+    if (int rc = build_blob(e, blob)) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     if (blob.size() > e->dev_floats) {
         if (e->dev) {
@@ -755,6 +772,32 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     HIPCHK(c, hipMemcpyAsync(e->dev, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));  // blob is a host temporary
     e->dirty = false;
+    return VGPU_OK;
+}
+
+// Host view for the CPU rake (csrc/cpu/vcpu.cpp): the same blob in host memory, rebuilt when the
+// environment changed.  Offsets are identical to the device copy's.
+int vgpu_env_host_view(vgpu_env* e, vgpu::HostEnvView* v)
+{
+    if (!e || !v) return VGPU_ERR_INVALID_ARG;
+    std::lock_guard<std::mutex> lock(e->host_mu);
+    if (e->host_dirty) {
+        if (int rc = build_blob(e, e->host_blob)) return rc;
+        e->host_dirty = false;
+    }
+    const float* b = e->host_blob.data();
+    for (int t = 0; t < OBS_TYPES; ++t) {
+        v->obs[t] = b + e->off[t];
+        v->n[t] = e->cnt[t];
+    }
+    v->hf = b + e->hf_off;
+    v->pc = b + e->pc_off;
+    v->base = b;
+    v->n_hf = (int)e->heightfields.size();
+    v->n_pc = (int)e->pointclouds.size();
+    v->att = b + e->att_off;
+    v->n_att = e->attached ? (int)e->att_spheres.size() : 0;
+    v->attached = e->attached;
     return VGPU_OK;
 }
 

@@ -334,6 +334,23 @@ class Environment:
         lib = load()
         h = C.c_void_p()
         check(lib.vgpu_env_create(ctx.h, C.byref(h)), ctx.h)
+        self._realise(lib, h, ctx.h)
+        check(lib.vgpu_env_upload(h), ctx.h)
+        self._handles[ctx.device] = h
+        return h
+
+    def host_handle(self) -> C.c_void_p:
+        """A host-only twin (no context) for the CPU rake (vgpu_cpu_*)."""
+        if "cpu" in self._handles:
+            return self._handles["cpu"]
+        lib = load()
+        h = C.c_void_p()
+        check(lib.vgpu_env_create(None, C.byref(h)))
+        self._realise(lib, h, None)
+        self._handles["cpu"] = h
+        return h
+
+    def _realise(self, lib, h, ctx_h):
         for kind, s in self._ops:
             if kind == "sphere":
                 rc = lib.vgpu_env_add_sphere(h, _f3(s.center), float(np.float32(s.r)))
@@ -360,10 +377,7 @@ class Environment:
                 else:
                     rc = lib.vgpu_env_add_capsule_euler(h, _f3(s.center), _f3(s.euler), float(np.float32(s.r)),
                                                         float(np.float32(s.length)))
-            check(rc, ctx.h)
-        check(lib.vgpu_env_upload(h), ctx.h)
-        self._handles[ctx.device] = h
-        return h
+            check(rc, ctx_h)
 
     def counts(self, ctx: Optional[Context] = None) -> List[int]:
         ctx = ctx or context()
@@ -512,27 +526,72 @@ class Robot:
         q = np.asarray(q, np.float32)
         return ((q - self.S_A) * self.D_M).astype(np.float32)
 
-    # --- reference-named single calls ---
-    def fk(self, configuration, ctx: Optional[Context] = None) -> List[Sphere]:
+    # --- reference-named single calls: the CPU rake (host AVX2, csrc/cpu/), as the reference's
+    # single-edge entry points stay on the CPU (a GPU launch costs far more than one edge) ---
+    def fk(self, configuration) -> List[Sphere]:
         """vamp.<robot>.fk(q) (bindings/common.hh:132-152): the collision spheres."""
-        xyz = self.sphere_fk_batch(np.asarray(configuration, np.float32)[None, :], ctx)[0]
+        q = np.asarray(configuration, np.float32).reshape(self.dimension())
+        xyz = self.cpu_sphere_fk_block(np.repeat(q[:, None], 8, axis=1))[:, :, 0].T
         radii = self.radii
         return [Sphere(xyz[s], float(radii[s])) for s in range(xyz.shape[0])]
 
-    def validate(self, configuration, environment: Environment, ctx: Optional[Context] = None) -> bool:
+    def validate(self, configuration, environment: Environment) -> bool:
         """vamp.<robot>.validate(q, env) (bindings/common.hh:172-190): bounds check in the
         descaled unit box, then validate_motion(q, q) == fkcc of the broadcast block."""
         q = np.asarray(configuration, np.float32)
         d = self.descale_configuration(q)
         if not ((d <= 1.0).all() and (d >= 0.0).all()):
             return False
-        return bool(self.fkcc_batch(q[None, :], environment, ctx)[0])
+        return bool(self.cpu_fkcc_batch(q[None, :], environment, threads=1)[0])
 
-    def validate_motion(self, start, goal, environment: Environment, ctx: Optional[Context] = None) -> bool:
+    def validate_motion(self, start, goal, environment: Environment) -> bool:
         """planning::validate_motion<Robot, 8, resolution> (planning/validate.hh:67-75)."""
-        ok, _ = self.validate_batch(np.asarray(start, np.float32)[None], np.asarray(goal, np.float32)[None],
-                                    environment, ctx)
-        return bool(ok[0])
+        s = np.ascontiguousarray(start, np.float32).reshape(self.dimension())
+        g = np.ascontiguousarray(goal, np.float32).reshape(self.dimension())
+        v = C.c_int()
+        check(load().vgpu_cpu_validate_motion(C.byref(self.c_robot), environment.host_handle(),
+                                              s.ctypes.data_as(_lib.F32P), g.ctypes.data_as(_lib.F32P), C.byref(v)))
+        return bool(v.value)
+
+    # --- CPU rake batches and blocks (host numpy in/out; threads <= 0: every hardware thread) ---
+    def cpu_fkcc_block(self, block, environment: Environment, attach: bool = False) -> bool:
+        """Robot::fkcc<8>(env, block) / fkcc_attach<8>: block = ConfigurationBlock<8> [dim][8]."""
+        b = np.ascontiguousarray(block, np.float32).reshape(self.dimension(), 8)
+        v = C.c_int()
+        fn = load().vgpu_cpu_fkcc_attach_block if attach else load().vgpu_cpu_fkcc_block
+        check(fn(C.byref(self.c_robot), environment.host_handle(), b.ctypes.data_as(_lib.F32P), C.byref(v)))
+        return bool(v.value)
+
+    def cpu_sphere_fk_block(self, block) -> np.ndarray:
+        """Robot::sphere_fk<8>(block): [3][n_spheres][8] world-frame centres."""
+        b = np.ascontiguousarray(block, np.float32).reshape(self.dimension(), 8)
+        out = np.empty((3, self.n_spheres(), 8), np.float32)
+        check(load().vgpu_cpu_sphere_fk_block(C.byref(self.c_robot), b.ctypes.data_as(_lib.F32P),
+                                              out.ctypes.data_as(_lib.F32P)))
+        return out
+
+    def cpu_fkcc_batch(self, q, environment: Environment, threads: int = 0, attach: bool = False) -> np.ndarray:
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, self.dimension())
+        out = np.empty(q.shape[0], np.uint8)
+        fn = load().vgpu_cpu_fkcc_attach if attach else load().vgpu_cpu_fkcc
+        check(fn(C.byref(self.c_robot), environment.host_handle(), q.ctypes.data_as(_lib.F32P), q.shape[0],
+                 out.ctypes.data_as(_lib.U8P), int(threads)))
+        return out.astype(bool)
+
+    def cpu_validate_batch(self, starts, goals, environment: Environment, threads: int = 0):
+        """validate_motion of every edge on the CPU rake: (ok, n_e, blocks evaluated)."""
+        s = np.ascontiguousarray(starts, np.float32).reshape(-1, self.dimension())
+        g = np.ascontiguousarray(goals, np.float32).reshape(-1, self.dimension())
+        if s.shape != g.shape:
+            raise ValueError("starts and goals differ in shape")
+        ok = np.empty(s.shape[0], np.uint8)
+        nb = np.empty(s.shape[0], np.int32)
+        ne = np.empty(s.shape[0], np.int32)
+        check(load().vgpu_cpu_validate_motions(C.byref(self.c_robot), environment.host_handle(),
+                                               s.ctypes.data_as(_lib.F32P), g.ctypes.data_as(_lib.F32P), s.shape[0],
+                                               ok.ctypes.data_as(_lib.U8P), nb.ctypes.data_as(_lib.I32P),
+                                               ne.ctypes.data_as(_lib.I32P), int(threads)))
+        return ok.astype(bool), nb, ne
 
     # --- batches (host numpy in/out) ---
     def sphere_fk_batch(self, q, ctx: Optional[Context] = None) -> np.ndarray:

@@ -89,6 +89,14 @@ SIGNATURES = {
     "vgpu_roadmap_edge_gather": (C.c_int, [VP, C.c_int, VP, C.c_size_t, C.c_size_t, VP, C.c_uint32, VP, VP, VP,
                                            VP]),
     "vgpu_roadmap_assemble": (C.c_int, [C.c_size_t, U32P, C.c_size_t, C.POINTER(C.c_size_t), U32P, U32P]),
+    "vgpu_cpu_fkcc_block": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.POINTER(C.c_int)]),
+    "vgpu_cpu_fkcc_attach_block": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.POINTER(C.c_int)]),
+    "vgpu_cpu_sphere_fk_block": (C.c_int, [C.POINTER(VgpuRobot), F32P, F32P]),
+    "vgpu_cpu_validate_motion": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.POINTER(C.c_int)]),
+    "vgpu_cpu_fkcc": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P, C.c_int]),
+    "vgpu_cpu_fkcc_attach": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P, C.c_int]),
+    "vgpu_cpu_validate_motions": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P, I32P,
+                                            C.c_int]),
     "vgpu_build_roadmap_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, C.c_double, C.c_double,
                                           C.POINTER(C.c_size_t), U32P, C.c_size_t, C.POINTER(C.c_size_t), U32P]),
 }

@@ -432,8 +432,39 @@ class RobotGen:
         bcb = [wc(fb.bound_center(b), "b") for b in range(nb)]
         spheres = m["spheres"]
         links = [b["link"] for b in m["bounding"]]
+        if TY["cpu"]:
+            # CPU: every sphere centre of both arms once, up front (the same op sequence per centre
+            # as the per-block recomputation below, so the same bits), then the tests -- one
+            # straight-line function a host compiler handles (the GPU form recomputes frames per
+            # fired pair to keep its register live set small)
+            cas = {i: wc(fa.center(sp["frame"], sp["offset"]), "a") for i, sp in enumerate(spheres)}
+            cbs = {j: wc(fb.center(sp["frame"], sp["offset"]), "b") for j, sp in enumerate(spheres)}
         for la in range(nb):
             for lb in range(nb):
+                if not TY["cpu"]:
+                    break
+                ra, rb = m["bounding"][la]["radius"], m["bounding"][lb]["radius"]
+                A_, B_ = bca[la], bcb[lb]
+                E.raw(f"// {links[la]} (A) vs {links[lb]} (B)")
+                E.raw(f"if (Grp::any(self_lane({A_[0].expr()}, {A_[1].expr()}, {A_[2].expr()}, {flit(ra)}, "
+                      f"{B_[0].expr()}, {B_[1].expr()}, {B_[2].expr()}, {flit(rb)}))) {{")
+                E.indent += 1
+                E.raw(bdecl("h"))
+                for i in [i for i, sp in enumerate(spheres) if sp["link"] == links[la]]:
+                    for j in [j for j, sp in enumerate(spheres) if sp["link"] == links[lb]]:
+                        ca, cb = cas[i], cbs[j]
+                        E.raw(f"h |= self_bits({ca[0].expr()}, {ca[1].expr()}, {ca[2].expr()}, "
+                              f"{flit(spheres[i]['radius'])}, {cb[0].expr()}, {cb[1].expr()}, "
+                              f"{cb[2].expr()}, {flit(spheres[j]['radius'])});")
+                E.raw("if (Grp::any_bits(h)) return true;")
+                E.indent -= 1
+                E.raw("}")
+            if TY["cpu"]:
+                continue
+        for la in range(nb):
+            for lb in range(nb):
+                if TY["cpu"]:
+                    break
                 ra, rb = m["bounding"][la]["radius"], m["bounding"][lb]["radius"]
                 A_, B_ = bca[la], bcb[lb]
                 E.raw(f"// {links[la]} (A) vs {links[lb]} (B)")
