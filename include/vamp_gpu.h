@@ -243,6 +243,42 @@ int vgpu_cpu_fkcc_attach(const vgpu_robot *robot, vgpu_env *env, const float *q,
 int vgpu_cpu_validate_motions(const vgpu_robot *robot, vgpu_env *env, const float *starts, const float *goals,
                               size_t n_edges, uint8_t *ok, int32_t *n_blocks, int32_t *n_evaluated, int threads);
 
+/* planning::validate_vector<Robot, 8, Robot::resolution>(start, vector, distance, env)
+ * (validate.hh:23-65): the caller's distance sets the back-step count (RRT-Connect, rrtc.hh:139). */
+int vgpu_cpu_validate_vector(const vgpu_robot *robot, vgpu_env *env, const float *start, const float *vector,
+                             float distance, int *valid);
+
+/* ---- RRT-Connect on the CPU rake (BASELINE configs[0]) ------------------------------------------ */
+/* vamp::planning::RRTCSettings (planning/rrtc_settings.hh:5-20); defaults: range 2, dynamic_domain 1,
+ * radius 4, alpha 1e-4, min_radius 1, balance 1, tree_ratio 1, max_iterations = max_samples =
+ * 100000, start_tree_first 1 (the Python layer sets range per robot and 1e6 iterations/samples,
+ * src/vamp/__init__.py:80-102). */
+typedef struct vgpu_rrtc_settings {
+    float range;
+    int32_t dynamic_domain;
+    float radius, alpha, min_radius;
+    int32_t balance;
+    float tree_ratio;
+    uint64_t max_iterations, max_samples;
+    int32_t start_tree_first;
+} vgpu_rrtc_settings;
+/* vamp::planning::PlanningResult (planning/plan.hh): solved = non-empty path */
+typedef struct vgpu_plan_result {
+    int32_t solved;
+    uint64_t iterations;
+    int64_t nanoseconds;
+    uint64_t size[2]; /* start tree, goal tree */
+    float cost;
+    size_t path_len;
+} vgpu_plan_result;
+/* RRTC<Robot, 8, Robot::resolution>::solve(start, goals, env, settings, rng) (planning/rrtc.hh:33-248)
+ * with rng::Halton<dim>: *rng_index is the 1-based index of the sampler's next draw (a fresh sampler:
+ * 1; skip(k): +k) and is advanced by the draws taken.  path[path_cap][dim] receives the path; if
+ * path_cap < result->path_len the call returns VGPU_ERR_INVALID_ARG with path_len set. */
+int vgpu_cpu_rrtc(const vgpu_robot *robot, vgpu_env *env, const float *start, const float *goals, size_t n_goals,
+                  const vgpu_rrtc_settings *settings, uint64_t *rng_index, float *path, size_t path_cap,
+                  vgpu_plan_result *result);
+
 /* ---- robot metadata ------------------------------------------------------------------------ */
 /* dimension, resolution, n_spheres of a robot kind (robots/panda_base.hh:19-23) */
 /* Point-cloud filter (replaces vamp::collision::filter_pointcloud, collision/filter.hh:175-268,

@@ -17,12 +17,6 @@
 #include "vcpu_robot.hh"
 
 namespace vcpu {
-namespace {
-
-struct Bound {
-    const RobotCpu* R = nullptr;
-    float base[6] = {0, 0, 0, 0, 0, 0};
-};
 
 // vgpu_api.cpp:check_robot, without a context: PandaBase<X100, Y100, Z100> bases (panda/fk.hh:
 // 109-111, static_cast<float>(x100) / 100.0f); Fetch / UR5 / Baxter have none
@@ -47,11 +41,6 @@ int bind(const vgpu_robot* r, Bound& b)
     b.base[5] = (float)r->base2_z100 / 100.0f;
     return VGPU_OK;
 }
-
-struct Env {
-    EnvView v;
-    bool ext = false, attached = false;
-};
 
 int view(vgpu_env* e, Env& out)
 {
@@ -92,17 +81,14 @@ float l2_norm(const float* v, int dim)
     return std::sqrt(a + b);
 }
 
-// validate_motion<Robot, 8, Robot::resolution> (planning/validate.hh:23-75).  Returns validity;
-// *n = n_e (validate.hh:41), *evaluated = rake blocks evaluated before the result was known
-// (the reference's early exit: the first invalid block ends the edge).
-bool validate_one(const Bound& b, const Env& env, const float* start, const float* goal, int32_t* n,
-                  int32_t* evaluated)
+// validate_vector<Robot, 8, Robot::resolution>(start, v, distance) (planning/validate.hh:23-65).
+// Returns validity; *n = n_e (validate.hh:41), *evaluated = rake blocks evaluated before the
+// result was known (the reference's early exit: the first invalid block ends the edge).
+bool validate_vector_one(const Bound& b, const Env& env, const float* start, const float* v, float distance,
+                         int32_t* n, int32_t* evaluated)
 {
     const RobotCpu& R = *b.R;
     const int D = R.dim;
-    float v[kMaxDim];
-    for (int j = 0; j < D; ++j) v[j] = goal[j] - start[j];  // validate.hh:72
-    const float distance = l2_norm(v, D);                     // validate.hh:73
     const V pct = _mm256_setr_ps(1.0f / 8, 2.0f / 8, 3.0f / 8, 4.0f / 8, 5.0f / 8, 6.0f / 8, 7.0f / 8, 1.0f);
     V block[kMaxDim];
     for (int j = 0; j < D; ++j) block[j] = fma(V(v[j]), pct, V(start[j]));  // validate.hh:37 (contracted)
@@ -130,6 +116,15 @@ bool validate_one(const Bound& b, const Env& env, const float* start, const floa
     return valid;
 }
 
+// validate_motion<Robot, 8, Robot::resolution> (planning/validate.hh:67-75)
+bool validate_one(const Bound& b, const Env& env, const float* start, const float* goal, int32_t* n,
+                  int32_t* evaluated)
+{
+    float v[kMaxDim];
+    for (int j = 0; j < b.R->dim; ++j) v[j] = goal[j] - start[j];                   // validate.hh:72
+    return validate_vector_one(b, env, start, v, l2_norm(v, b.R->dim), n, evaluated);  // validate.hh:73
+}
+
 // static contiguous chunks, one std::thread each (SURVEY §8(d) CPU reference timing)
 template <class Fn>
 void parallel_for(size_t n, int threads, Fn fn)
@@ -155,7 +150,6 @@ int resolve_threads(int threads)
     return hw ? (int)hw : 1;
 }
 
-}  // namespace
 }  // namespace vcpu
 
 using namespace vcpu;
@@ -211,6 +205,19 @@ extern "C" int vgpu_cpu_validate_motion(const vgpu_robot* robot, vgpu_env* env, 
     if (int rc = view(env, e)) return rc;
     if (e.attached && !b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
     *valid = validate_one(b, e, start, goal, nullptr, nullptr) ? 1 : 0;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_cpu_validate_vector(const vgpu_robot* robot, vgpu_env* env, const float* start,
+                                        const float* vector, float distance, int* valid)
+{
+    Bound b;
+    Env e;
+    if (!start || !vector || !valid) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    if (int rc = view(env, e)) return rc;
+    if (e.attached && !b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
+    *valid = validate_vector_one(b, e, start, vector, distance, nullptr, nullptr) ? 1 : 0;
     return VGPU_OK;
 }
 

@@ -32,11 +32,19 @@ void sphere_fk(const V* q, const float* b, V* out)
             out[c * 118 + 59 + s] = outb[c * 59 + s];
         }
 }
+
+// both arms' scaling, concatenated
+constexpr float pair_s_m[14] = {panda_s_m[0], panda_s_m[1], panda_s_m[2], panda_s_m[3], panda_s_m[4], panda_s_m[5],
+                                panda_s_m[6], panda_s_m[0], panda_s_m[1], panda_s_m[2], panda_s_m[3], panda_s_m[4],
+                                panda_s_m[5], panda_s_m[6]};
+constexpr float pair_s_a[14] = {panda_s_a[0], panda_s_a[1], panda_s_a[2], panda_s_a[3], panda_s_a[4], panda_s_a[5],
+                                panda_s_a[6], panda_s_a[0], panda_s_a[1], panda_s_a[2], panda_s_a[3], panda_s_a[4],
+                                panda_s_a[5], panda_s_a[6]};
 }  // namespace
 
 const RobotCpu* robot_panda_pair()
 {
-    static const RobotCpu r{14, 32, 118, fkcc, nullptr, sphere_fk};
+    static const RobotCpu r{14, 32, 118, fkcc, nullptr, sphere_fk, pair_s_m, pair_s_a};
     return &r;
 }
 }  // namespace vcpu

@@ -3,6 +3,7 @@
 // -mavx2 -mfma -ffp-contract=off: the generated straight-line code is large).
 #pragma once
 
+#include "../../../include/vamp_gpu.h"
 #include "vcpu_simd.hh"
 
 namespace vcpu {
@@ -20,7 +21,27 @@ struct RobotCpu {
     bool (*fkcc_attach)(const V* q, const EnvView& env, const float* base, bool ext);
     // Robot::sphere_fk<8>: out[3][n_spheres] (x rows, then y, then z), world frame
     void (*sphere_fk)(const V* q, const float* base, V* out);
+    // Robot::scale_configuration q * s_m + s_a (contracted to one fma per joint, ref_probe "scale")
+    const float* s_m;
+    const float* s_a;
 };
+
+// a bound robot (vgpu_robot -> op table + base offsets) and a host environment view (vcpu.cpp)
+struct Bound {
+    const RobotCpu* R = nullptr;
+    float base[6] = {0, 0, 0, 0, 0, 0};
+};
+struct Env {
+    EnvView v;
+    bool ext = false, attached = false;
+};
+int bind(const vgpu_robot* r, Bound& b);
+int view(vgpu_env* e, Env& out);
+float l2_norm(const float* v, int dim);
+bool validate_vector_one(const Bound& b, const Env& env, const float* start, const float* v, float distance,
+                         int32_t* n, int32_t* evaluated);
+bool validate_one(const Bound& b, const Env& env, const float* start, const float* goal, int32_t* n,
+                  int32_t* evaluated);
 
 const RobotCpu* robot_panda();
 const RobotCpu* robot_fetch();

@@ -437,6 +437,56 @@ def compact_device(rows_ptr: int, valid_ptr: int, n: int, dim: int, rows_out_ptr
     return int(cnt.value)
 
 
+# ---- planning (RRT-Connect on the CPU rake: BASELINE configs[0]) -------------------------------
+class RRTCSettings:
+    """vamp::planning::RRTCSettings (planning/rrtc_settings.hh:5-20), same field names/defaults."""
+
+    def __init__(self, **kw):
+        self.range = 2.0
+        self.dynamic_domain = True
+        self.radius = 4.0
+        self.alpha = 0.0001
+        self.min_radius = 1.0
+        self.balance = True
+        self.tree_ratio = 1.0
+        self.max_iterations = 100000
+        self.max_samples = 100000
+        self.start_tree_first = True
+        for k, v in kw.items():
+            if not hasattr(self, k):
+                raise AttributeError(k)
+            setattr(self, k, v)
+
+    def c(self) -> _lib.VgpuRrtcSettings:
+        return _lib.VgpuRrtcSettings(float(self.range), int(self.dynamic_domain), float(self.radius),
+                                     float(self.alpha), float(self.min_radius), int(self.balance),
+                                     float(self.tree_ratio), int(self.max_iterations), int(self.max_samples),
+                                     int(self.start_tree_first))
+
+
+class Halton:
+    """rng::Halton<dim> (random/halton.hh) as the planners consume it: vamp.<robot>.halton() with
+    reset() / skip(n) / next(); the state is the 1-based index of the next draw."""
+
+    def __init__(self, dim: int):
+        self.dim = dim
+        self.index = 1
+
+    def reset(self):
+        self.index = 1
+
+    def skip(self, n: int):
+        self.index += int(n)
+
+
+class PlanningResult:
+    """vamp::planning::PlanningResult (planning/plan.hh): path, cost, iterations, size, nanoseconds."""
+
+    def __init__(self, path, cost, iterations, size, nanoseconds, solved):
+        self.path, self.cost, self.iterations = path, cost, iterations
+        self.size, self.nanoseconds, self.solved = size, nanoseconds, solved
+
+
 # ---- robots -----------------------------------------------------------------------------------
 # Robot::space_measure of each robot: the reference's generated constant returned as float
 # (panda/fk.hh:88-91 "-> float"), values as extracted into model/<robot>.json; the composite is
@@ -552,6 +602,47 @@ class Robot:
         check(load().vgpu_cpu_validate_motion(C.byref(self.c_robot), environment.host_handle(),
                                               s.ctypes.data_as(_lib.F32P), g.ctypes.data_as(_lib.F32P), C.byref(v)))
         return bool(v.value)
+
+    def halton(self) -> Halton:
+        """vamp.<robot>.halton(): a fresh Halton<dimension> sampler."""
+        return Halton(self.dimension())
+
+    def rrtc(self, start, goals, environment: Environment, settings: Optional[RRTCSettings] = None,
+             rng: Optional[Halton] = None) -> PlanningResult:
+        """vamp.<robot>.rrtc(start, goal(s), env, settings, rng) (bindings/common.hh:191-200 ->
+        planning/rrtc.hh:33-248) on the CPU rake; rng advances by the draws taken."""
+        dim = self.dimension()
+        s = np.ascontiguousarray(start, np.float32).reshape(dim)
+        g = np.ascontiguousarray(goals, np.float32).reshape(-1, dim)
+        settings = settings or RRTCSettings()
+        rng = rng or self.halton()
+        idx = C.c_uint64(rng.index)
+        res = _lib.VgpuPlanResult()
+        cap = 4096
+        while True:
+            path = np.empty((cap, dim), np.float32)
+            i0 = C.c_uint64(idx.value)
+            rc = load().vgpu_cpu_rrtc(C.byref(self.c_robot), environment.host_handle(), s.ctypes.data_as(_lib.F32P),
+                                      g.ctypes.data_as(_lib.F32P), g.shape[0], C.byref(settings.c()), C.byref(i0),
+                                      path.ctypes.data_as(_lib.F32P), cap, C.byref(res))
+            if rc == _lib.VGPU_OK or res.path_len <= cap:
+                check(rc)
+                idx = i0
+                break
+            cap = int(res.path_len)
+        rng.index = int(idx.value)
+        return PlanningResult(path[:res.path_len].copy(), float(res.cost), int(res.iterations),
+                              (int(res.size[0]), int(res.size[1])), int(res.nanoseconds), bool(res.solved))
+
+    def cpu_validate_vector(self, start, vector, distance: float, environment: Environment) -> bool:
+        """planning::validate_vector<Robot, 8, resolution>(start, vector, distance, env)."""
+        s = np.ascontiguousarray(start, np.float32).reshape(self.dimension())
+        v = np.ascontiguousarray(vector, np.float32).reshape(self.dimension())
+        ok = C.c_int()
+        check(load().vgpu_cpu_validate_vector(C.byref(self.c_robot), environment.host_handle(),
+                                              s.ctypes.data_as(_lib.F32P), v.ctypes.data_as(_lib.F32P),
+                                              float(np.float32(distance)), C.byref(ok)))
+        return bool(ok.value)
 
     # --- CPU rake batches and blocks (host numpy in/out; threads <= 0: every hardware thread) ---
     def cpu_fkcc_block(self, block, environment: Environment, attach: bool = False) -> bool:
@@ -724,4 +815,4 @@ __all__ += ["PandaPair", "panda_pair"]
 # robots/ur5.hh (6 dof) and robots/baxter.hh (14-dof dual arm): no base offset
 ur5 = Robot("ur5", 0, 0, 0, kind=_lib.VGPU_ROBOT_UR5)
 baxter = Robot("baxter", 0, 0, 0, kind=_lib.VGPU_ROBOT_BAXTER)
-__all__ += ["ur5", "baxter"]
+__all__ += ["ur5", "baxter", "RRTCSettings", "Halton", "PlanningResult"]

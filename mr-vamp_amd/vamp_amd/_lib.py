@@ -33,6 +33,17 @@ class VgpuRobot(C.Structure):
                 ("base2_x100", C.c_int32), ("base2_y100", C.c_int32), ("base2_z100", C.c_int32)]
 
 
+class VgpuRrtcSettings(C.Structure):
+    _fields_ = [("range", C.c_float), ("dynamic_domain", C.c_int32), ("radius", C.c_float), ("alpha", C.c_float),
+                ("min_radius", C.c_float), ("balance", C.c_int32), ("tree_ratio", C.c_float),
+                ("max_iterations", C.c_uint64), ("max_samples", C.c_uint64), ("start_tree_first", C.c_int32)]
+
+
+class VgpuPlanResult(C.Structure):
+    _fields_ = [("solved", C.c_int32), ("iterations", C.c_uint64), ("nanoseconds", C.c_int64),
+                ("size", C.c_uint64 * 2), ("cost", C.c_float), ("path_len", C.c_size_t)]
+
+
 # every exported symbol of include/vamp_gpu.h with its signature (restype, argtypes)
 SIGNATURES = {
     "vgpu_ctx_create": (C.c_int, [C.c_int, C.POINTER(VP)]),
@@ -97,6 +108,9 @@ SIGNATURES = {
     "vgpu_cpu_fkcc_attach": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P, C.c_int]),
     "vgpu_cpu_validate_motions": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P, I32P,
                                             C.c_int]),
+    "vgpu_cpu_validate_vector": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_float, C.POINTER(C.c_int)]),
+    "vgpu_cpu_rrtc": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, C.POINTER(VgpuRrtcSettings),
+                                C.POINTER(C.c_uint64), F32P, C.c_size_t, C.POINTER(VgpuPlanResult)]),
     "vgpu_build_roadmap_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, C.c_double, C.c_double,
                                           C.POINTER(C.c_size_t), U32P, C.c_size_t, C.POINTER(C.c_size_t), U32P]),
 }

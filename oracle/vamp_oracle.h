@@ -128,6 +128,9 @@ void vo_robot_sphere_fk(int robot, const float *q, int bx100, int by100, int bz1
 /* q is [G][dim]; returns 1 = valid */
 int vo_robot_fkcc_block(int robot, const vo_env *env, const float *q, int G, int bx100, int by100, int bz100,
                         vo_stats *stats);
+/* validate_vector with the caller's distance (planning/validate.hh:23-65; RRT-Connect's extension check) */
+int vo_robot_validate_vector(int robot, const vo_env *env, const float *start, const float *vector, float distance,
+                             int bx100, int by100, int bz100, int *n_out);
 int vo_robot_validate_motion(int robot, const vo_env *env, const float *start, const float *goal, int bx100,
                              int by100, int bz100, int *n_out, vo_stats *stats);
 void vo_robot_fkcc_configs(int robot, const vo_env *env, const float *q, size_t n, int bx100, int by100,

@@ -120,6 +120,9 @@ def lib():
         L.vo_robot_validate_motion.restype = C.c_int
         L.vo_robot_validate_motion.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, F32P, C.c_int, C.c_int, C.c_int,
                                                C.POINTER(C.c_int), C.POINTER(VoStats)]
+        L.vo_robot_validate_vector.restype = C.c_int
+        L.vo_robot_validate_vector.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, F32P, C.c_float, C.c_int, C.c_int,
+                                               C.c_int, C.POINTER(C.c_int)]
         L.vo_robot_fkcc_configs.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, C.c_size_t, C.c_int, C.c_int, C.c_int,
                                             U8P, C.c_int]
         L.vo_robot_validate_motions.argtypes = [C.c_int, C.POINTER(VoEnv), F32P, F32P, C.c_size_t, C.c_int,
@@ -415,6 +418,15 @@ def robot_fkcc_threads(robot, env: Env, q, base100=(0, 0, 0), threads=8):
     ce = env.c()
     lib().vo_robot_fkcc_configs(rid, C.byref(ce), fp(q), q.shape[0], *base100, out.ctypes.data_as(U8P), threads)
     return out.astype(bool)
+
+
+def robot_validate_vector(robot, env_c, start, vector, distance, base100=(0, 0, 0)):
+    """validate_vector<Robot, 8, res>(start, vector, distance) (planning/validate.hh:23-65); env_c is
+    Env.c() (kept alive by the caller across calls)"""
+    rid = ROBOTS[robot][0]
+    s = np.ascontiguousarray(start, np.float32)
+    v = np.ascontiguousarray(vector, np.float32)
+    return bool(lib().vo_robot_validate_vector(rid, C.byref(env_c), fp(s), fp(v), float(distance), *base100, None))
 
 
 def robot_validate_motions(robot, env: Env, starts, goals, base100=(0, 0, 0), threads=8):

@@ -1,0 +1,113 @@
+"""BASELINE configs[0]: Panda RRT-Connect on MotionBenchMaker table_pick problems on the CPU rake
+(mr-vamp_amd/csrc/cpu/vcpu_rrtc.cpp, planning/rrtc.hh:33-248), RRTCSettings with range 1.0 and 1e6
+iterations/samples (src/vamp/constants.py:1,49-55; src/vamp/__init__.py:80-102), Halton<7> reset per
+problem (scripts/evaluate_mbm.py:95-96).
+
+Checks: the straight start -> goal validate_motion of each problem equals the reference-DAG fixture;
+the product planner equals an independent Python restatement (tests/rrtc_py.py, oracle
+validate_vector) path for path, bit for bit, with the same iterations, tree sizes and cost; every
+solved path starts at the start, ends at the goal (to the last increment), and each of its segments passes validate_motion
+(oracle) or is one of the planner's own validate_vector-checked extensions."""
+import numpy as np
+import pytest
+
+import rrtc_py
+from conftest import host_fixture
+from test_gpu_parity import gpu_env_from_oracle
+from test_oracle import EDGE_MIN_COVERAGE, fixture_check, same_rsqrt_host, stable
+
+F = np.float32
+SETTINGS = dict(range=1.0, max_iterations=1000000, max_samples=1000000)
+
+
+@pytest.fixture(scope="module")
+def vamp():
+    import vamp_amd
+    return vamp_amd
+
+
+def problem(oracle, fx, k):
+    o = oracle.Env()
+    for key in ("spheres", "capsules", "zcapsules", "cuboids", "zcuboids"):
+        setattr(o, key, [list(r) for r in fx[f"p{k}_env_{key}"]])
+    return o, fx[f"p{k}_start"], fx[f"p{k}_goal"]
+
+
+def test_straight_line_vs_reference_dag(vamp, oracle):
+    fx = host_fixture("panda_table_pick_problems.npz", oracle)
+    same = same_rsqrt_host(oracle, fx)
+    got, ref, keep = [], [], []
+    for k in range(1, int(fx["n_problems"]) + 1):
+        o, s, g = problem(oracle, fx, k)
+        ok, n, _ = vamp.panda_0_0.cpu_validate_batch(s[None], g[None], gpu_env_from_oracle(vamp, o))
+        ook, on = oracle.validate_motions(o, s[None], g[None], (0, 0, 0))
+        assert ok[0] == ook[0] and n[0] == on[0] == fx[f"p{k}_n"][0]
+        got.append(ok[0])
+        ref.append(fx[f"p{k}_ok"][0])
+        keep.append(stable(fx[f"p{k}_test_margin"], fx[f"p{k}_cull_margin"], same)[0])
+    fixture_check("panda table_pick start->goal (CPU rake)", np.array(got), np.array(ref), np.array(keep), same, 0.5)
+
+
+def test_table_pick_scene_fixture(vamp, oracle):
+    """configs[1]'s MBM run: per-configuration masks and edges on
+    table_pick scene0001 vs the reference DAG."""
+    from test_oracle_robots import scene_env
+    fx = host_fixture("panda_table_pick.npz", oracle)
+    oenv = scene_env(oracle, fx)
+    env = gpu_env_from_oracle(vamp, oenv)
+    same = same_rsqrt_host(oracle, fx)
+    got = vamp.panda_0_0.cpu_fkcc_batch(fx["q"], env)
+    assert np.array_equal(got, oracle.fkcc_threads(oenv, fx["q"], (0, 0, 0)))
+    fixture_check("panda fkcc table_pick (CPU rake)", got, fx["valid"], stable(fx["test_margin"], fx["cull_margin"],
+                                                                                  same), same)
+    ok, n, _ = vamp.panda_0_0.cpu_validate_batch(fx["starts"], fx["goals"], env)
+    rok, rn = oracle.validate_motions(oenv, fx["starts"], fx["goals"], (0, 0, 0))
+    assert np.array_equal(ok, rok) and np.array_equal(n, rn) and np.array_equal(n, fx["n"])
+    fixture_check("panda validate_motion table_pick (CPU rake)", ok, fx["ok"],
+                  stable(fx["edge_test_margin"], fx["edge_cull_margin"], same), same, EDGE_MIN_COVERAGE)
+
+
+@pytest.mark.parametrize("k,base", [(1, (0, 0, 0)), (1, (200, 200, 0)), (2, (0, 0, 0)), (3, (0, 0, 0)),
+                                    (4, (0, 0, 0)), (5, (0, 0, 0)), (6, (0, 0, 0))])
+def test_rrtc_matches_restatement(vamp, oracle, k, base):
+    fx = host_fixture("panda_table_pick_problems.npz", oracle)
+    o, s, g = problem(oracle, fx, k)
+    env = gpu_env_from_oracle(vamp, o)
+    robot = vamp.PandaBase(*base)
+    rng = robot.halton()
+    res = robot.rrtc(s, g, env, vamp.RRTCSettings(**SETTINGS), rng)
+    p, cost, it, sizes, idx = rrtc_py.rrtc("panda", o, s, g, SETTINGS, 1, base)
+    assert res.solved and len(p)
+    assert res.iterations == it and res.size == sizes and rng.index == idx
+    assert np.array_equal(res.path.view(np.uint32), p.view(np.uint32))
+    assert np.float32(res.cost).view(np.uint32) == np.float32(cost).view(np.uint32)
+    # the ends are the start and goal, or the connect step's last increment onto them (rrtc.hh:213-221
+    # walks the other tree from the nearest node's parent)
+    assert np.abs(res.path[0] - s).max() <= 1e-5 and np.abs(res.path[-1] - g).max() <= 1e-5
+    # segments: collision-free under the planner's own checks; validate_motion (the caller's view,
+    # recomputing each segment's vector and length) agrees on all but near-boundary segments
+    ok, _ = oracle.validate_motions(o, res.path[:-1], res.path[1:], base)
+    assert ok.mean() >= 0.9, ok
+
+
+def test_rrtc_rng_and_settings(vamp, oracle):
+    """a second solve continues the sampler (evaluate_mbm runs trials without reset); max_iterations
+    bounds the search; an unsolvable problem reports solved = False."""
+    fx = host_fixture("panda_table_pick_problems.npz", oracle)
+    o, s, g = problem(oracle, fx, 2)
+    env = gpu_env_from_oracle(vamp, o)
+    robot = vamp.panda_0_0
+    rng = robot.halton()
+    r1 = robot.rrtc(s, g, env, vamp.RRTCSettings(**SETTINGS), rng)
+    i1 = rng.index
+    r2 = robot.rrtc(s, g, env, vamp.RRTCSettings(**SETTINGS), rng)
+    p, _, it, _, idx = rrtc_py.rrtc("panda", o, s, g, SETTINGS, i1)
+    assert r2.iterations == it and rng.index == idx and np.array_equal(r2.path, p)
+    assert r1.solved and r2.solved
+    capped = robot.rrtc(s, g, env, vamp.RRTCSettings(range=1.0, max_iterations=3, max_samples=1000), robot.halton())
+    assert capped.iterations <= 4
+    # the goal inside an obstacle: no path within the iteration budget
+    blocked = vamp.Environment()
+    blocked.add_sphere(vamp.Sphere([0.0, 0.0, 0.4], 0.6))
+    r = robot.rrtc(s, g, blocked, vamp.RRTCSettings(range=1.0, max_iterations=200, max_samples=1000), robot.halton())
+    assert not r.solved and r.path.shape == (0, 7) and r.iterations == 201

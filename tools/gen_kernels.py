@@ -673,8 +673,8 @@ def main():
         vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model[key])
         consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
     out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
-    if TY["cpu"]:  # CPU restatement: sphere_fk + monolithic fkcc only (one rake block per call)
-        out = g.gen_sphere_fk() + "\n" + g.gen_fkcc()
+    if TY["cpu"]:  # CPU restatement: scale constants, sphere_fk + monolithic fkcc (one rake block per call)
+        out = "\n".join(consts).replace("__device__ constexpr", "constexpr") + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
         if "att_checks" in model:
             out = g.gen_fkcc()
     elif "att_checks" in model:  # the attachment variant: its fkcc only (first rake block)

@@ -1,25 +1,15 @@
 #!/bin/bash
-# One GPU-box session: parity tests, smoke, short bench, rocprofv3 kernel stats.
-# Every GPU step has its own time limit and the chain stops at the first failure.
-set -o pipefail
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# One GPU-box pass (run through gpurun from the repo root): GPU parity tests, the CPU-rake tests on
+# the box's host (its own rsqrt table), and the bench legs.  Every step is time-limited; the chain
+# stops at the first failure.   usage: bash tools/gpu_check.sh TAG [workloads...]
+TAG=${1:-r02}
+shift
+WL=${*:-validate capt pair fetch_prm}
 mkdir -p gpurun_out
-export TMPDIR=/tmp
-STEP=${1:-all}
-rocm-smi --showproductname > gpurun_out/smi.txt 2>&1 || true
-lscpu > gpurun_out/lscpu.txt 2>&1 || true
-if [ "$STEP" = "all" ] || [ "$STEP" = "test" ]; then
-  timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest gpu failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
-  tail -3 gpurun_out/pytest_gpu.log
-  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
-  cat gpurun_out/smoke.log
-fi
-if [ "$STEP" = "all" ] || [ "$STEP" = "bench" ]; then
-  timeout -k 10 600 python bench.py --steps 10 --warmup 2 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
-  cat gpurun_out/bench.json
-fi
-if [ "$STEP" = "all" ] || [ "$STEP" = "prof" ]; then
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 1 --no-cpu > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; tail -30 gpurun_out/prof.log; exit 1; }
-  find gpurun_out/prof -name "*stats*" | head
-fi
-echo done
+timeout -k 10 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread \
+    > gpurun_out/${TAG}_gputest.log 2>&1 || exit 1
+timeout -k 10 300 python -u -m pytest tests/test_cpu_rake.py tests/test_c_abi.py -q --timeout 200 \
+    > gpurun_out/${TAG}_cputest_box.log 2>&1 || exit 2
+for w in $WL; do
+    timeout -k 10 300 python -u bench.py --workload $w > gpurun_out/${TAG}_bench_$w.log 2>&1 || exit 3
+done

@@ -199,7 +199,7 @@ def envnp_of(env):
                     zcuboids=a["zcuboids"])
 
 
-def make_robot(rng, robot, scene, out_name, n_cfg=16384, n_empty=4096, n_edges=1024):
+def make_robot(rng, robot, scene, out_name, n_cfg=16384, n_empty=4096, n_edges=1024, fk_fixture=True):
     """A generated robot (fetch, ur5, baxter): FK centres, per-configuration masks and edges on
     the empty scene and one MotionBenchMaker scene, from the reference's generated
     robots/<robot>/fk.hh evaluated by tools/fkhh_interp.py."""
@@ -211,9 +211,10 @@ def make_robot(rng, robot, scene, out_name, n_cfg=16384, n_empty=4096, n_edges=1
     rs = fi.RsqrtHost(lut, kb)
     q = op.robot_scale(robot, rng.random((1024, dim), dtype=F))
     xyz, r = fi.run_sphere_fk(fk, q, (0, 0, 0))
-    np.savez_compressed(out_path(f"fk_{robot}.npz"), q=q, radii=r.astype(F),
-                        xyz=np.ascontiguousarray(np.transpose(xyz, (2, 1, 0))))
-    print(f"fk_{robot}.npz")
+    if fk_fixture:
+        np.savez_compressed(out_path(f"fk_{robot}.npz"), q=q, radii=r.astype(F),
+                            xyz=np.ascontiguousarray(np.transpose(xyz, (2, 1, 0))))
+        print(f"fk_{robot}.npz")
     env = op.mbm_env(mbm_scene(robot, scene))
     arr = env.arrays()
     envnp = envnp_of(env)
@@ -243,6 +244,41 @@ def make_robot(rng, robot, scene, out_name, n_cfg=16384, n_empty=4096, n_edges=1
                         starts=starts, goals=goals, ok=ok, n=n.astype(np.int32), edge_test_margin=tm.astype(F),
                         edge_cull_margin=cm.astype(F))
     print(out_name, valid.mean(), valid_e.mean(), ok[:E].mean(), ok[E:].mean(), n.max())
+
+
+def mbm_request(robot, name, dim):
+    """start / goal joint positions of a MotionBenchMaker request (request*.yaml): the first `dim`
+    joints of start_state, the goal_constraints' joint positions in joint order"""
+    import tarfile
+
+    import yaml
+    with tarfile.open(f"/root/reference/resources/{robot}/problems.tar.bz2") as t:
+        rq = yaml.safe_load(t.extractfile(f"problems/{name}").read().decode())
+    start = np.array(rq["start_state"]["joint_state"]["position"][:dim], F)
+    goal = np.array([c["position"] for c in rq["goal_constraints"][0]["joint_constraints"]][:dim], F)
+    return start, goal
+
+
+def make_panda_mbm(rng, n_problems=16):
+    """Panda on MotionBenchMaker table_pick (the configs[0] planning problem and the configs[1] MBM
+    run): masks / edges on scene0001 from the reference DAG (make_robot), plus the
+    first `n_problems` problems' resolved scenes, start / goal and the reference-DAG result of the
+    straight start -> goal validate_motion (base (0,0,0): the scenes are origin-centred)."""
+    make_robot(rng, "panda", "table_pick_panda/scene0001.yaml", "panda_table_pick.npz", fk_fixture=False)
+    fk, cc = fi.load_panda()
+    lut, kb = host_lut()
+    rs = fi.RsqrtHost(lut, kb)
+    out = {"rsqrt_lut": lut, "rsqrt_kbits": kb}
+    for k in range(1, n_problems + 1):
+        env = op.mbm_env(mbm_scene("panda", f"table_pick_panda/scene{k:04d}.yaml"))
+        start, goal = mbm_request("panda", f"table_pick_panda/request{k:04d}.yaml", 7)
+        ok, n, tm, cm = interp_validate(cc, start[None], goal[None], (0, 0, 0), envnp_of(env), rs)
+        for key, v in env.arrays().items():
+            out[f"p{k}_env_{key}"] = v
+        out.update({f"p{k}_start": start, f"p{k}_goal": goal, f"p{k}_ok": ok, f"p{k}_n": n.astype(np.int32),
+                    f"p{k}_test_margin": tm.astype(F), f"p{k}_cull_margin": cm.astype(F)})
+    np.savez_compressed(out_path("panda_table_pick_problems.npz"), n_problems=np.int32(n_problems), **out)
+    print("panda_table_pick_problems.npz", [bool(out[f"p{k}_ok"][0]) for k in range(1, n_problems + 1)])
 
 
 def make_fetch(rng):
@@ -437,6 +473,9 @@ def main():
         return
     if "--fetch" in sys.argv:
         make_fetch(np.random.default_rng(20261016))
+        return
+    if "--panda-mbm" in sys.argv:
+        make_panda_mbm(np.random.default_rng(20261024))
         return
     if "--attach-fetch" in sys.argv:
         make_attach_robot(np.random.default_rng(20261022), "fetch", "table_pick_fetch/scene0001.yaml")
