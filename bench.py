@@ -57,9 +57,11 @@ def parse():
                     help="edges checked against the scalar oracle (the CPU rake checks every edge)")
     ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
-    ap.add_argument("--workload", default="validate", choices=["validate", "capt", "fetch_prm", "prm_edges", "pair"],
+    ap.add_argument("--workload", default="validate",
+                    choices=["validate", "capt", "fetch_prm", "prm_edges", "pair", "rrtc"],
                     help="validate: BASELINE configs[1] (the headline); capt: configs[2]; fetch_prm: configs[3] "
-                         "vertex stage; prm_edges: configs[3] edge stage; pair: configs[4] two-Panda composite edges")
+                         "vertex stage; prm_edges: configs[3] edge stage; pair: configs[4] two-Panda composite edges; "
+                         "rrtc: configs[0] RRT-Connect on MBM table_pick (CPU rake)")
     ap.add_argument("--vertices", type=int, default=100_000,
                     help="prm_edges: roadmap vertices (RoadmapSettings::max_samples default, roadmap.hh:170)")
     ap.add_argument("--draws", type=int, default=4_000_000, help="fetch_prm: Halton draws per step (whole job)")
@@ -553,6 +555,83 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     print(json.dumps(line))
 
 
+def run_rrtc(a, torch, dist, rank, world, dev, stream, ctx, vamp):
+    """BASELINE configs[0]: Panda RRT-Connect (planning/rrtc.hh) on the
+    MotionBenchMaker table_pick problems (scene + request 1..16, resolved into
+    tests/golden/panda_table_pick_problems.npz), CPU only -- the planner and its validate_vector
+    checks on the CPU rake, one core, RRTCSettings range 1.0 / 1e6 iterations, Halton<7> reset per
+    problem (scripts/evaluate_mbm.py:95-96), PandaBase<0,0,0> (the scenes are origin-centred) and
+    the fork's default Panda (2,2,0) on problem 1.  One step = one solve of every problem; the
+    value is the median planning time (PlanningResult.nanoseconds).  Every solved path's segments
+    are re-checked on the GPU (vgpu_validate_motions) against the CPU rake.  N ranks = replicas."""
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "panda_table_pick_problems.npz"), allow_pickle=False)
+    P = int(fx["n_problems"])
+    envs, starts, goals = [], [], []
+    for k in range(1, P + 1):
+        env = vamp.Environment()
+        for row in fx[f"p{k}_env_spheres"]:
+            env.add_sphere(vamp.Sphere(row[0:3], float(row[3])))
+        for row in np.concatenate([fx[f"p{k}_env_cuboids"], fx[f"p{k}_env_zcuboids"]]):
+            env.add_cuboid(vamp.Cuboid.from_axes(row[0:3], row[3:6], row[6:9], row[9:12], row[12:15]))
+        for row in np.concatenate([fx[f"p{k}_env_capsules"], fx[f"p{k}_env_zcapsules"]]):
+            p1 = np.array(row[0:3], np.float32)
+            env.add_capsule(vamp.Cylinder(p1, (p1 + np.array(row[3:6], np.float32)).astype(np.float32), float(row[6])))
+        envs.append(env)
+        starts.append(fx[f"p{k}_start"])
+        goals.append(fx[f"p{k}_goal"])
+    settings = vamp.RRTCSettings(range=1.0, max_iterations=1000000, max_samples=1000000)
+    runs = [(vamp.panda_0_0, k) for k in range(P)] + [(vamp.panda, 0)]
+    results = []
+
+    def step():
+        results.clear()
+        for robot, k in runs:
+            results.append(robot.rrtc(starts[k], goals[k], envs[k], settings, robot.halton()))
+
+    wall = timed_steps(a, torch, dist, dev, world, step)
+    wall_max, _ = reduce_over_ranks(dist, torch, wall, 0.0, dev, world)
+    if rank != 0:
+        return
+    ns = np.array([r.nanoseconds for r in results[:P]], np.float64)
+    its = np.array([r.iterations for r in results[:P]])
+    # the solved paths' segments through the GPU batch path vs the CPU rake (same edges)
+    seg_s = np.concatenate([r.path[:-1] for r in results[:P] if r.solved])
+    seg_g = np.concatenate([r.path[1:] for r in results[:P] if r.solved])
+    owner = np.concatenate([np.full(len(r.path) - 1, i) for i, r in enumerate(results[:P]) if r.solved])
+    gpu_ok = np.zeros(len(seg_s), bool)
+    cpu_ok = np.zeros(len(seg_s), bool)
+    for i in range(P):
+        m = owner == i
+        if m.any():
+            gpu_ok[m] = vamp.panda_0_0.validate_batch(seg_s[m], seg_g[m], envs[i], ctx)[0]
+            cpu_ok[m] = vamp.panda_0_0.cpu_validate_batch(seg_s[m], seg_g[m], envs[i], threads=1)[0]
+    med_us = float(np.median(ns)) / 1e3
+    b220 = results[P]
+    line = {
+        "metric": "Panda MBM RRT-Connect planning time, median (CPU rake)", "value": med_us, "unit": "us",
+        "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": wall_max / a.steps * 1e3,
+        "higher_is_better": False, "scaling": "replicas", "vs_baseline": med_us / 35.0, "dtype": "f32",
+        "data": "MotionBenchMaker table_pick_panda scene/request 0001-0016 (resources/panda/problems.tar.bz2, resolved "
+                "into tests/golden/panda_table_pick_problems.npz)",
+        "config": {"workload": f"BASELINE configs[0]: Panda 7-DOF RRT-Connect, {P} MBM table_pick problems, CPU only",
+                   "robot": "PandaBase<0,0,0> (+ Panda (2,2,0) on problem 1)", "planner": "RRTC<Panda, 8, 32>",
+                   "settings": "range 1.0, dynamic domain, balanced, 1e6 iterations/samples, Halton<7> reset per problem",
+                   "parallelism": "one core per problem (replicas over ranks)"},
+        "baseline_note": "vs_baseline = median / 35 us, the reference README's median over all MBM problems on one "
+                         "desktop core (BASELINE.md); this run: table_pick only, GPU box host core",
+        "problems": [{"problem": k + 1, "solved": bool(r.solved), "ns": int(r.nanoseconds), "iterations": int(r.iterations),
+                      "path_len": int(len(r.path)), "cost": float(r.cost), "trees": list(r.size)}
+                     for k, r in enumerate(results[:P])],
+        "panda_2_2_0_problem1": {"solved": bool(b220.solved), "ns": int(b220.nanoseconds),
+                                  "iterations": int(b220.iterations)},
+        "solved": int(sum(r.solved for r in results[:P])), "iterations_median": float(np.median(its)),
+        "path_segments": {"count": int(len(seg_s)), "gpu_valid": int(gpu_ok.sum()),
+                          "gpu_vs_cpu_rake_mismatches": int((gpu_ok != cpu_ok).sum())},
+        "cpu_baseline": None, "cpu_model": cpu_model(),
+    }
+    print(json.dumps(line))
+
+
 def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     """BASELINE configs[2]: Panda vs a 10k-point CAPT (points on the 14
     cage spheres, r_min 0.012, r_max 0.06, r_point 0.0025), per-configuration fkcc of 2^20 uniform
@@ -645,7 +724,8 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     if a.workload != "validate":
-        {"fetch_prm": run_fetch_prm, "prm_edges": run_prm_edges, "pair": run_pair, "capt": run_capt}[a.workload](
+        {"fetch_prm": run_fetch_prm, "prm_edges": run_prm_edges, "pair": run_pair, "capt": run_capt,
+         "rrtc": run_rrtc}[a.workload](
             a, torch, dist, rank, world, dev, stream, ctx, vamp)
         if world > 1:
             dist.destroy_process_group()
