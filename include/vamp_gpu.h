@@ -243,6 +243,11 @@ int vgpu_cpu_fkcc_attach(const vgpu_robot *robot, vgpu_env *env, const float *q,
 int vgpu_cpu_validate_motions(const vgpu_robot *robot, vgpu_env *env, const float *starts, const float *goals,
                               size_t n_edges, uint8_t *ok, int32_t *n_blocks, int32_t *n_evaluated, int threads);
 
+/* Robot::eefk(q) (panda/fk.hh:11399-11650, fetch.hh:47, ur5.hh:48; bindings/common.hh:342-352): the
+ * end-effector pose in the robot frame for each q[n][dim]: pose[n][7] = x y z, quaternion x y z w.
+ * Double precision internally, as the reference's generated eefk.  Panda, Fetch, UR5 (the Baxter's
+ * reference eefk is empty, the composite has none: VGPU_ERR_UNSUPPORTED). */
+int vgpu_cpu_eefk(const vgpu_robot *robot, const float *q, size_t n, float *pose);
 /* planning::validate_vector<Robot, 8, Robot::resolution>(start, vector, distance, env)
  * (validate.hh:23-65): the caller's distance sets the back-step count (RRT-Connect, rrtc.hh:139). */
 int vgpu_cpu_validate_vector(const vgpu_robot *robot, vgpu_env *env, const float *start, const float *vector,

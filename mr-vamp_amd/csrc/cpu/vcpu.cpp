@@ -150,9 +150,90 @@ int resolve_threads(int threads)
     return hw ? (int)hw : 1;
 }
 
+// Robot::eefk (panda/fk.hh:11399-11650, fetch/fk.hh:30993, ur5/fk.hh:5868): the end-effector
+// frame's pose in the robot frame (no base offset: PandaBase<...>::eefk = panda::eefk).  The
+// reference's generated eefk computes in double (its temporaries are float * double literals,
+// std::sin / std::cos of the half angles) and narrows the result to float; this walks the same
+// chain in double from the model data (csrc/gen/cpu/eefk_tables.inc).
+struct EeFrame {
+    int parent;
+    double qf[4];  // w x y z
+    double t[3];
+    int dof, prismatic;
+    double axis[3];
+};
+#include "../gen/cpu/eefk_tables.inc"
+
+static void qmul_d(const double* a, const double* b, double* o)
+{
+    o[0] = a[0] * b[0] - a[1] * b[1] - a[2] * b[2] - a[3] * b[3];
+    o[1] = a[0] * b[1] + a[1] * b[0] + a[2] * b[3] - a[3] * b[2];
+    o[2] = a[0] * b[2] - a[1] * b[3] + a[2] * b[0] + a[3] * b[1];
+    o[3] = a[0] * b[3] + a[1] * b[2] - a[2] * b[1] + a[3] * b[0];
+}
+static void rot_d(const double* q, const double* v, double* o)  // R(q) v
+{
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    o[0] = (1 - 2 * (y * y + z * z)) * v[0] + 2 * (x * y - w * z) * v[1] + 2 * (x * z + w * y) * v[2];
+    o[1] = 2 * (x * y + w * z) * v[0] + (1 - 2 * (x * x + z * z)) * v[1] + 2 * (y * z - w * x) * v[2];
+    o[2] = 2 * (x * z - w * y) * v[0] + 2 * (y * z + w * x) * v[1] + (1 - 2 * (x * x + y * y)) * v[2];
+}
+
 }  // namespace vcpu
 
 using namespace vcpu;
+
+extern "C" int vgpu_cpu_eefk(const vgpu_robot* robot, const float* q, size_t n, float* pose)
+{
+    if (!robot || (n && (!q || !pose))) return VGPU_ERR_INVALID_ARG;
+    Bound b;
+    if (int rc = bind(robot, b)) return rc;
+    int len = 0;
+    const EeFrame* chain = ee_chain(robot->kind, &len);
+    if (!chain) return VGPU_ERR_UNSUPPORTED;  // the composite has none; Baxter's eefk is empty (baxter/fk.hh)
+    const int D = b.R->dim;
+    std::vector<double> Q(4 * (size_t)len), P(3 * (size_t)len);
+    for (size_t i = 0; i < n; ++i) {
+        const float* qi = q + (size_t)D * i;
+        for (int f = 0; f < len; ++f) {
+            const EeFrame& fr = chain[f];
+            double* qc = &Q[4 * (size_t)f];
+            double* pc = &P[3 * (size_t)f];
+            if (fr.parent < 0) {
+                qc[0] = 1, qc[1] = qc[2] = qc[3] = 0;
+                pc[0] = pc[1] = pc[2] = 0;
+                continue;
+            }
+            const double* qp = &Q[4 * (size_t)fr.parent];
+            const double* pp = &P[3 * (size_t)fr.parent];
+            double a[4], tv[3];
+            qmul_d(qp, fr.qf, a);
+            rot_d(qp, fr.t, tv);
+            for (int k = 0; k < 3; ++k) pc[k] = pp[k] + tv[k];
+            if (fr.dof >= 0 && fr.prismatic) {
+                const double d[3] = {(double)qi[fr.dof] * fr.axis[0], (double)qi[fr.dof] * fr.axis[1],
+                                     (double)qi[fr.dof] * fr.axis[2]};
+                double dv[3];
+                rot_d(a, d, dv);
+                for (int k = 0; k < 3; ++k) pc[k] += dv[k];
+                std::copy(a, a + 4, qc);
+            } else if (fr.dof >= 0) {
+                const double h = (double)qi[fr.dof] * 0.5;
+                const double s = std::sin(h);
+                const double j[4] = {std::cos(h), s * fr.axis[0], s * fr.axis[1], s * fr.axis[2]};
+                qmul_d(a, j, qc);
+            } else {
+                std::copy(a, a + 4, qc);
+            }
+        }
+        const double* qe = &Q[4 * (size_t)(len - 1)];
+        const double* pe = &P[3 * (size_t)(len - 1)];
+        float* o = pose + 7 * i;  // x y z, quaternion x y z w (bindings/common.hh:342-352)
+        o[0] = (float)pe[0], o[1] = (float)pe[1], o[2] = (float)pe[2];
+        o[3] = (float)qe[1], o[4] = (float)qe[2], o[5] = (float)qe[3], o[6] = (float)qe[0];
+    }
+    return VGPU_OK;
+}
 
 extern "C" int vgpu_cpu_fkcc_block(const vgpu_robot* robot, vgpu_env* env, const float* block, int* valid)
 {

@@ -603,6 +603,19 @@ class Robot:
                                               s.ctypes.data_as(_lib.F32P), g.ctypes.data_as(_lib.F32P), C.byref(v)))
         return bool(v.value)
 
+    def eefk(self, configuration):
+        """vamp.<robot>.eefk(q) (bindings/common.hh:342-352): (position [3], quaternion x y z w [4])."""
+        p = self.eefk_batch(np.asarray(configuration, np.float32)[None])[0]
+        return p[:3].copy(), p[3:].copy()
+
+    def eefk_batch(self, q) -> np.ndarray:
+        """Robot::eefk of each q[n][dim]: [n][7] (x y z, qx qy qz qw), robot frame."""
+        q = np.ascontiguousarray(q, np.float32).reshape(-1, self.dimension())
+        out = np.empty((q.shape[0], 7), np.float32)
+        check(load().vgpu_cpu_eefk(C.byref(self.c_robot), q.ctypes.data_as(_lib.F32P), q.shape[0],
+                                   out.ctypes.data_as(_lib.F32P)))
+        return out
+
     def halton(self) -> Halton:
         """vamp.<robot>.halton(): a fresh Halton<dimension> sampler."""
         return Halton(self.dimension())

@@ -281,6 +281,20 @@ def make_panda_mbm(rng, n_problems=16):
     print("panda_table_pick_problems.npz", [bool(out[f"p{k}_ok"][0]) for k in range(1, n_problems + 1)])
 
 
+def make_eefk(rng, n=1024):
+    """Robot::eefk fixtures: the reference's generated eefk (robots/<robot>/fk.hh) evaluated in
+    double by tools/eefk_ref.py at uniform configurations, Panda / Fetch / UR5."""
+    import eefk_ref
+    out = {}
+    for robot in ("panda", "fetch", "ur5"):
+        dim, run = eefk_ref.make_eval(robot)
+        q = op.robot_scale(robot, rng.random((n, dim), dtype=F))
+        out[f"{robot}_q"] = q
+        out[f"{robot}_pose"] = run(q)
+    np.savez_compressed(out_path("eefk.npz"), **out)
+    print("eefk.npz")
+
+
 def make_fetch(rng):
     make_robot(rng, "fetch", "table_pick_fetch/scene0001.yaml", "fetch_table_pick.npz")
 
@@ -473,6 +487,9 @@ def main():
         return
     if "--fetch" in sys.argv:
         make_fetch(np.random.default_rng(20261016))
+        return
+    if "--eefk" in sys.argv:
+        make_eefk(np.random.default_rng(20261025))
         return
     if "--panda-mbm" in sys.argv:
         make_panda_mbm(np.random.default_rng(20261024))
