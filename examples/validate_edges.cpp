@@ -18,12 +18,12 @@ using namespace vamp_gpu;
 {
     const robots::Fetch::Configuration qf{0.1f, 0.0f, 0.5f, 0.0f, 1.0f, 0.0f, 1.0f, 0.0f};
     const robots::Panda_Pair::Configuration qp{};
-    const bool a = robots::Fetch::fkcc(env, qf);
+    const bool a = robots::Fetch::fkcc_batch(env, {qf})[0] != 0;
     const auto b = planning::validate_motions<robots::Fetch>(env, {qf}, {qf});
-    const bool c = planning::validate_motion<robots::Panda_Pair>(env, qp, qp);
-    const bool d = robots::UR5::fkcc(env, robots::UR5::Configuration{});
-    const bool e = planning::validate_motion<robots::Baxter>(env, robots::Baxter::Configuration{},
-                                                             robots::Baxter::Configuration{});
+    const bool c = planning::validate_motion<robots::Panda_Pair, 8, 32>(qp, qp, env);
+    const bool d = robots::UR5::fkcc_batch(env, {robots::UR5::Configuration{}})[0] != 0;
+    const bool e = planning::validate_motion<robots::Baxter, 8, 64>(robots::Baxter::Configuration{},
+                                                                    robots::Baxter::Configuration{}, env);
     return (a ? 1u : 0u) + b.size() + (c ? 1u : 0u) + (d ? 1u : 0u) + (e ? 1u : 0u);
 }
 
@@ -33,7 +33,7 @@ using namespace vamp_gpu;
     collision::Attachment held({0.0f, 0.0f, 0.1f}, {0.0f, 0.0f, 0.0f, 1.0f});
     held.add_sphere({0.0f, 0.0f, 0.05f}, 0.03f);
     env.attach(held);
-    const auto m = robots::Panda_0_0::fkcc_attach(env, std::vector<robots::Panda_0_0::Configuration>(4));
+    const auto m = robots::Panda_0_0::fkcc_attach_batch(env, std::vector<robots::Panda_0_0::Configuration>(4));
     env.detach();
     const auto rm = planning::build_roadmap_edges<robots::Fetch>(
         env, std::vector<robots::Fetch::Configuration>(16), 269832.265625);
@@ -75,7 +75,8 @@ int main(int argc, char **argv)
         const auto ok = planning::validate_motions<Robot>(env, starts, goals, &n);
         std::size_t valid = 0;
         for (auto v : ok) valid += v;
-        const bool single = planning::validate_motion<Robot>(env, starts[0], goals[0]);
+        // the reference-shaped single edge: the CPU rake (same result as the GPU batch)
+        const bool single = planning::validate_motion<Robot, 8, Robot::resolution>(starts[0], goals[0], env);
         std::FILE *o = std::fopen(argv[2], "wb");
         std::fwrite(ok.data(), 1, ok.size(), o);
         std::fclose(o);

@@ -284,7 +284,15 @@ int vgpu_cpu_rrtc(const vgpu_robot *robot, vgpu_env *env, const float *start, co
                   const vgpu_rrtc_settings *settings, uint64_t *rng_index, float *path, size_t path_cap,
                   vgpu_plan_result *result);
 
+/* FloatVector<dim>::l2_norm (vector/interface.hh:402-410): squares summed in the AVX hsum lane order
+ * (avx.hh:441-452; above 8 lanes the two registers first as fma(lo, lo, hi * hi), pinned by ref_probe
+ * "l2norm"), then std::sqrt.  dim <= 16.  The distance of every planner and NN (nn.hh:53-57). */
+float vgpu_l2_norm(const float *v, int dim);
+
 /* ---- robot metadata ------------------------------------------------------------------------ */
+/* Robot::scale_configuration / descale_configuration constants (robots/<robot>/fk.hh, e.g. panda/fk.hh:14-
+ * 62): q_scaled = fma(q, s_m, s_a), q_unit = (q - s_a) * d_m; dimension floats each (any may be NULL). */
+int vgpu_robot_scale_params(const vgpu_robot *robot, float *s_m, float *s_a, float *d_m);
 /* dimension, resolution, n_spheres of a robot kind (robots/panda_base.hh:19-23) */
 /* Point-cloud filter (replaces vamp::collision::filter_pointcloud, collision/filter.hh:175-268,
  * bound as vamp.filter_pointcloud in bindings/common.hh). pc: n x 3 f32 (device for the first,

@@ -10,6 +10,7 @@
 // (tools/gen_kernels.py), the host's own _mm256_rsqrt_ps cull, the reference rake arithmetic.
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <thread>
 #include <vector>
 
@@ -182,6 +183,24 @@ static void rot_d(const double* q, const double* v, double* o)  // R(q) v
 }  // namespace vcpu
 
 using namespace vcpu;
+
+extern "C" float vgpu_l2_norm(const float* v, int dim)
+{
+    if (!v || dim < 1 || dim > 16) return std::numeric_limits<float>::quiet_NaN();
+    return l2_norm(v, dim);
+}
+
+extern "C" int vgpu_robot_scale_params(const vgpu_robot* robot, float* s_m, float* s_a, float* d_m)
+{
+    Bound b;
+    if (int rc = bind(robot, b)) return rc;
+    for (int j = 0; j < b.R->dim; ++j) {
+        if (s_m) s_m[j] = b.R->s_m[j];
+        if (s_a) s_a[j] = b.R->s_a[j];
+        if (d_m) d_m[j] = b.R->d_m[j];
+    }
+    return VGPU_OK;
+}
 
 extern "C" int vgpu_cpu_eefk(const vgpu_robot* robot, const float* q, size_t n, float* pose)
 {

@@ -16,7 +16,7 @@ void sphere_fk(const V* q, const float*, V* out) { baxter_sphere_fk_store(VCPU_Q
 
 const RobotCpu* robot_baxter()
 {
-    static const RobotCpu r{14, 64, 75, fkcc, fkcc, sphere_fk, baxter_s_m, baxter_s_a};
+    static const RobotCpu r{14, 64, 75, fkcc, fkcc, sphere_fk, baxter_s_m, baxter_s_a, baxter_d_m};
     return &r;
 }
 }  // namespace vcpu

@@ -22,7 +22,7 @@ void sphere_fk(const V* q, const float*, V* out) { fetch_sphere_fk_store(VCPU_Q8
 
 const RobotCpu* robot_fetch()
 {
-    static const RobotCpu r{8, 32, 111, fkcc, fkcc_attach, sphere_fk, fetch_s_m, fetch_s_a};  // fetch.hh:12-14
+    static const RobotCpu r{8, 32, 111, fkcc, fkcc_attach, sphere_fk, fetch_s_m, fetch_s_a, fetch_d_m};  // fetch.hh:12-14
     return &r;
 }
 }  // namespace vcpu

@@ -23,7 +23,7 @@ void sphere_fk(const V* q, const float* b, V* out) { panda_sphere_fk_store(VCPU_
 
 const RobotCpu* robot_panda()
 {
-    static const RobotCpu r{7, 32, 59, fkcc, fkcc_attach, sphere_fk, panda_s_m, panda_s_a};  // panda_base.hh:19-23
+    static const RobotCpu r{7, 32, 59, fkcc, fkcc_attach, sphere_fk, panda_s_m, panda_s_a, panda_d_m};  // panda_base.hh:19-23
     return &r;
 }
 }  // namespace vcpu

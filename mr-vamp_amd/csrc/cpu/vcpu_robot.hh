@@ -24,6 +24,7 @@ struct RobotCpu {
     // Robot::scale_configuration q * s_m + s_a (contracted to one fma per joint, ref_probe "scale")
     const float* s_m;
     const float* s_a;
+    const float* d_m;  // descale_configuration (q - s_a) * d_m
 };
 
 // a bound robot (vgpu_robot -> op table + base offsets) and a host environment view (vcpu.cpp)

@@ -21,7 +21,7 @@ void sphere_fk(const V* q, const float*, V* out) { ur5_sphere_fk_store(VCPU_Q6(q
 
 const RobotCpu* robot_ur5()
 {
-    static const RobotCpu r{6, 32, 36, fkcc, fkcc_attach, sphere_fk, ur5_s_m, ur5_s_a};
+    static const RobotCpu r{6, 32, 36, fkcc, fkcc_attach, sphere_fk, ur5_s_m, ur5_s_a, ur5_d_m};
     return &r;
 }
 }  // namespace vcpu

@@ -108,6 +108,8 @@ SIGNATURES = {
     "vgpu_cpu_fkcc_attach": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P, C.c_int]),
     "vgpu_cpu_validate_motions": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P, I32P,
                                             C.c_int]),
+    "vgpu_l2_norm": (C.c_float, [F32P, C.c_int]),
+    "vgpu_robot_scale_params": (C.c_int, [C.POINTER(VgpuRobot), F32P, F32P, F32P]),
     "vgpu_cpu_eefk": (C.c_int, [C.POINTER(VgpuRobot), F32P, C.c_size_t, F32P]),
     "vgpu_cpu_validate_vector": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_float, C.POINTER(C.c_int)]),
     "vgpu_cpu_rrtc": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, C.POINTER(VgpuRrtcSettings),

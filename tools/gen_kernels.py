@@ -674,6 +674,8 @@ def main():
         consts.append(f"__device__ constexpr float {name}_{key}[{len(model[key])}] = {{{vals}}};")
     out = "\n".join(consts) + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
     if TY["cpu"]:  # CPU restatement: scale constants, sphere_fk + monolithic fkcc (one rake block per call)
+        vals = ", ".join(f"{float(np.float32(v)).hex()}f" for v in model["d_m"])
+        consts.append(f"constexpr float {name}_d_m[{len(model['d_m'])}] = {{{vals}}};  // descale (q - s_a) * d_m")
         out = "\n".join(consts).replace("__device__ constexpr", "constexpr") + "\n\n" + g.gen_sphere_fk() + "\n" + g.gen_fkcc()
         if "att_checks" in model:
             out = g.gen_fkcc()
