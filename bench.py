@@ -62,6 +62,10 @@ def parse():
                     help="validate: BASELINE configs[1] (the headline); capt: configs[2]; fetch_prm: configs[3] "
                          "vertex stage; prm_edges: configs[3] edge stage; pair: configs[4] two-Panda composite edges; "
                          "rrtc: configs[0] RRT-Connect on MBM table_pick (CPU rake)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="validate / pair: weak = --edges per GPU, each rank its own shard resident in HBM; strong = "
+                         "one fixed batch of --edges split into contiguous ranges over the ranks, each step copying "
+                         "its range in from pinned host memory and the results back (H2D + kernels + D2H timed)")
     ap.add_argument("--vertices", type=int, default=100_000,
                     help="prm_edges: roadmap vertices (RoadmapSettings::max_samples default, roadmap.hh:170)")
     ap.add_argument("--draws", type=int, default=4_000_000, help="fetch_prm: Halton draws per step (whole job)")
@@ -183,6 +187,31 @@ def traffic_record(path):
             return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+def strong_slice(n, rank, world):
+    """contiguous range of a fixed batch of n units owned by `rank` (strong scaling)"""
+    lo = n * rank // world
+    return lo, n * (rank + 1) // world - lo
+
+
+class PinnedShard:
+    """Strong-scaling step of one rank: its edge range lives in pinned host memory; a step copies
+    it to the device, validates it and copies the results back (the serving path)."""
+
+    def __init__(self, torch, starts, goals, dev):
+        self.h_s = starts.cpu().pin_memory()
+        self.h_g = goals.cpu().pin_memory()
+        self.d_s = torch.empty_like(starts)
+        self.d_g = torch.empty_like(goals)
+        self.h_ok = torch.empty(starts.shape[0], dtype=torch.uint8).pin_memory()
+
+    def step(self, robot, env, ok, nb, ctx):
+        self.d_s.copy_(self.h_s, non_blocking=True)
+        self.d_g.copy_(self.h_g, non_blocking=True)
+        robot.validate_device(self.d_s.data_ptr(), self.d_g.data_ptr(), self.d_s.shape[0], env, ok.data_ptr(),
+                              nb.data_ptr(), ctx)
+        self.h_ok.copy_(ok, non_blocking=True)
 
 
 def shard_seed(rank):
@@ -472,9 +501,10 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     for row in oenv.cuboids + oenv.zcuboids:
         env.add_cuboid(vamp.Cuboid.from_axes(row[0:3], row[3:6], row[6:9], row[9:12], row[12:15]))
     robot = vamp.panda_pair
+    strong = a.scaling == "strong"
     E = a.edges
     g = torch.Generator(device=dev)
-    g.manual_seed(shard_seed(rank))
+    g.manual_seed(shard_seed(0 if strong else rank))
     sm = torch.tensor(S_M * 2, device=dev)
     sa = torch.tensor(S_A * 2, device=dev)
     pool, have = [], 0
@@ -494,11 +524,18 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         sc = torch.clamp(1.0 / torch.clamp(d, min=1e-9), max=1.0).float()
         goals[:, sl] = starts[:, sl] + (goals[:, sl] - starts[:, sl]) * sc[:, None]
     goals = goals.contiguous()
+    if strong:  # one fixed batch, this rank's contiguous range, through pinned host memory
+        lo, E = strong_slice(a.edges, rank, world)
+        starts, goals = starts[lo:lo + E].contiguous(), goals[lo:lo + E].contiguous()
+        pinned = PinnedShard(torch, starts, goals, dev)
     okd = torch.empty(E, dtype=torch.uint8, device=dev)
     nb = torch.empty(E, dtype=torch.int32, device=dev)
 
     def step():
-        robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, env, okd.data_ptr(), nb.data_ptr(), ctx)
+        if strong:
+            pinned.step(robot, env, okd, nb, ctx)
+        else:
+            robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, env, okd.data_ptr(), nb.data_ptr(), ctx)
 
     wall = timed_steps(a, torch, dist, dev, world, step)
     # rake/early-exit units from the CPU rake on the same edges (bit-identical results), as configs[1]
@@ -539,9 +576,11 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     line = contract_line(
         a, world, wall_max, units_all,
         "validated edge-interpolants/sec (2x Panda 14-DOF composite FK+CC with inter-robot collision)",
-        "interpolants/s", "weak",
+        "interpolants/s", a.scaling,
         "synthetic (seeded uniform composite configurations; collision-free endpoints, each arm's sub-edge capped at 1.0)",
-        {"workload": f"BASELINE configs[4]: PandaBase<0,0,0> + PandaBase<100,0,0>, {E} edges per GPU, table + 3 spheres",
+        {"workload": f"BASELINE configs[4]: PandaBase<0,0,0> + PandaBase<100,0,0>, {E} edges per GPU, table + 3 spheres"
+                     if not strong else f"BASELINE configs[4] strong scaling: {a.edges} composite edges split over "
+                                        f"{world} GPU(s), H2D from pinned host memory + validate + D2H per step",
          "robot": "panda_pair", "edges_per_gpu": E, "interpolants_per_gpu": units,
          "edge_valid_fraction": float(okd.float().mean().item()),
          "parallelism": f"dp{world} (independent edge shards, no collective)"},
@@ -735,13 +774,24 @@ def main():
         env.add_sphere(vamp.Sphere(c, 0.2))
     robot = vamp.panda_0_0
 
-    E = a.edges
-    starts, goals = make_edges(torch, vamp, env, robot, E, seed=shard_seed(rank), dev=dev)
+    strong = a.scaling == "strong"
+    if strong:  # one fixed batch (the same seed on every rank), this rank's contiguous range
+        s_full, g_full = make_edges(torch, vamp, env, robot, a.edges, seed=shard_seed(0), dev=dev)
+        lo, E = strong_slice(a.edges, rank, world)
+        starts, goals = s_full[lo:lo + E].contiguous(), g_full[lo:lo + E].contiguous()
+        del s_full, g_full
+        pinned = PinnedShard(torch, starts, goals, dev)
+    else:
+        E = a.edges
+        starts, goals = make_edges(torch, vamp, env, robot, E, seed=shard_seed(rank), dev=dev)
     ok = torch.empty(E, dtype=torch.uint8, device=dev)
     nb = torch.empty(E, dtype=torch.int32, device=dev)
 
     def step():
-        robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, env, ok.data_ptr(), nb.data_ptr(), ctx)
+        if strong:
+            pinned.step(robot, env, ok, nb, ctx)
+        else:
+            robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, env, ok.data_ptr(), nb.data_ptr(), ctx)
 
     for _ in range(a.warmup):
         step()
@@ -843,18 +893,21 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": ms_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": a.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded uniform Panda configurations; collision-free endpoints, edges capped at 1.0)",
             "config": {
-                "workload": "BASELINE configs[1]: Panda 7-DOF, 2^20 edges per GPU, 14-sphere cage, "
-                            "validate_motion (rake 8, resolution 32, early exit)",
+                "workload": ("BASELINE configs[1]: Panda 7-DOF, 2^20 edges per GPU, 14-sphere cage, "
+                             "validate_motion (rake 8, resolution 32, early exit)") if not strong else
+                            (f"BASELINE configs[1] strong scaling: one batch of {a.edges} Panda edges split over "
+                             f"{world} GPU(s); each step H2D from pinned host memory + validate + D2H of the results"),
                 "robot": "PandaBase<0,0,0>",
                 "edges_per_gpu": E,
                 "interpolants_per_gpu": units_local,
                 "edge_valid_fraction": ok_frac,
-                "parallelism": f"dp{world} (independent edge shards, no collective)",
+                "parallelism": f"dp{world} (independent edge shards, no collective)" if not strong else
+                               f"dp{world} (contiguous ranges of one batch, no collective)",
             },
             "counting": "rake_early_exit: 8 x rake blocks the reference evaluates (through an edge's first invalid "
                         "block); value_full_mask_count counts 8 * n_e of every edge, evaluated or not",
