@@ -852,6 +852,34 @@ def main():
                   "frac": gbs / HBM_PEAK_GBS, "bytes_per_config": 736}
         del q, out
 
+    # full-mask mode: every rake block of every edge evaluated and kept -- its own
+    # timed pass over the same (device-resident) edges, HIP events on the launch stream
+    full_mask = None
+    if not strong:
+        cap = int(units_full_local // 8) + 64
+        blk = torch.empty(cap, dtype=torch.uint8, device=dev)
+        okm = torch.empty(E, dtype=torch.uint8, device=dev)
+
+        def mask_step():
+            return robot.validate_mask_device(starts.data_ptr(), goals.data_ptr(), E, env, okm.data_ptr(), 0,
+                                              blk.data_ptr(), cap, ctx)
+
+        for _ in range(max(1, a.warmup)):
+            total_blocks = mask_step()
+        m0, m1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        m0.record(stream)
+        for _ in range(a.steps):
+            mask_step()
+        m1.record(stream)
+        torch.cuda.synchronize(dev)
+        mask_ms = m0.elapsed_time(m1) / a.steps
+        full_mask = {"ms_per_step": mask_ms, "blocks": total_blocks, "interpolants": 8 * total_blocks,
+                     "value": 8 * total_blocks / (mask_ms * 1e-3), "unit": "interpolants/s",
+                     "edge_results_equal_early_exit": bool(torch.equal(okm, ok)),
+                     "note": "vgpu_validate_motions_mask: every block of every edge evaluated (no early exit), each "
+                             "block's result kept; includes its one block-count read-back"}
+        del blk, okm
+
     # per-phase kernel time (HIP events inside the library, separate untimed pass)
     ctx.set_profiling(True)
     for _ in range(a.steps):
@@ -932,6 +960,7 @@ def main():
                                "tail": f_tail * E / (max(tail_ms, 1e-9) * 1e-3) / 1e12 / FP32_PEAK_TFLOPS},
             },
             "roofline_hbm_fk": fk_leg,
+            "full_mask": full_mask,
             "cpu_baseline": cpu,
             "parity": parity,
         }

@@ -150,6 +150,15 @@ int vgpu_fkcc_attach(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, cons
 int vgpu_validate_motions(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *starts,
                           const float *goals, size_t n_edges, uint8_t *ok, int32_t *n_blocks);
 
+/* Full-mask mode: validate_motion's rake blocks ALL evaluated, with no early exit
+ * across an edge's blocks, and every block's result kept: block_ok[total] holds edge 0's blocks
+ * 0 .. n_0 - 1, then edge 1's, ...; ok[i] = AND of edge i's blocks (== vgpu_validate_motions' ok).
+ * *n_total = sum of n_e; fails with VGPU_ERR_INVALID_ARG when block_cap < *n_total (call again with a
+ * larger buffer).  Synchronises once (the block count).  Panda only; no attachments. */
+int vgpu_validate_motions_mask(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *starts,
+                               const float *goals, size_t n_edges, uint8_t *ok, int32_t *n_blocks, uint8_t *block_ok,
+                               size_t block_cap, size_t *n_total);
+
 /* ---- host-pointer conveniences (copy + synchronise) ---------------------------------------- */
 /* Raw sphere queries against point cloud `index`: simd = 0 -> CAPT::collides(center, r)
  * (capt.hh:403-443); simd = 1 -> one lane of CAPT::collides_simd (capt.hh:457-541).
@@ -240,6 +249,10 @@ int vgpu_cpu_validate_motion(const vgpu_robot *robot, vgpu_env *env, const float
 int vgpu_cpu_fkcc(const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n, uint8_t *valid, int threads);
 int vgpu_cpu_fkcc_attach(const vgpu_robot *robot, vgpu_env *env, const float *q, size_t n, uint8_t *valid,
                          int threads);
+/* full-mask form (as vgpu_validate_motions_mask): every block evaluated, block_ok[*n_total] edge-major */
+int vgpu_cpu_validate_motions_mask(const vgpu_robot *robot, vgpu_env *env, const float *starts, const float *goals,
+                                   size_t n_edges, uint8_t *ok, int32_t *n_blocks, uint8_t *block_ok, size_t block_cap,
+                                   size_t *n_total, int threads);
 int vgpu_cpu_validate_motions(const vgpu_robot *robot, vgpu_env *env, const float *starts, const float *goals,
                               size_t n_edges, uint8_t *ok, int32_t *n_blocks, int32_t *n_evaluated, int threads);
 

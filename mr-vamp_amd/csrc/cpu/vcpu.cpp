@@ -117,6 +117,32 @@ bool validate_vector_one(const Bound& b, const Env& env, const float* start, con
     return valid;
 }
 
+// full-mask mode: every block of the edge evaluated (no early exit), block_ok[0 .. n_e - 1]
+bool validate_all_blocks(const Bound& b, const Env& env, const float* start, const float* goal, uint8_t* block_ok)
+{
+    const RobotCpu& R = *b.R;
+    const int D = R.dim;
+    float v[kMaxDim];
+    for (int j = 0; j < D; ++j) v[j] = goal[j] - start[j];
+    const float distance = l2_norm(v, D);
+    const V pct = _mm256_setr_ps(1.0f / 8, 2.0f / 8, 3.0f / 8, 4.0f / 8, 5.0f / 8, 6.0f / 8, 7.0f / 8, 1.0f);
+    V block[kMaxDim];
+    for (int j = 0; j < D; ++j) block[j] = fma(V(v[j]), pct, V(start[j]));
+    float nf = std::ceil(distance / 8.0f * (float)R.resolution);
+    if (!(nf > 1.0f)) nf = 1.0f;
+    const int32_t ne = nf < 2147483520.0f ? (int32_t)nf : 2147483520;
+    bool all = block_ok[0] = (env.attached && R.fkcc_attach) ? R.fkcc_attach(block, env.v, b.base, env.ext)
+                                                              : R.fkcc(block, env.v, b.base, env.ext);
+    V back[kMaxDim];
+    for (int j = 0; j < D; ++j) back[j] = V(v[j] / (float)(8 * (int64_t)ne));
+    for (int32_t i = 1; i < ne; ++i) {
+        for (int j = 0; j < D; ++j) block[j] = block[j] - back[j];
+        block_ok[i] = R.fkcc(block, env.v, b.base, env.ext) ? 1 : 0;
+        all = all && block_ok[i];
+    }
+    return all;
+}
+
 // validate_motion<Robot, 8, Robot::resolution> (planning/validate.hh:67-75)
 bool validate_one(const Bound& b, const Env& env, const float* start, const float* goal, int32_t* n,
                   int32_t* evaluated)
@@ -356,6 +382,36 @@ extern "C" int vgpu_cpu_fkcc_attach(const vgpu_robot* robot, vgpu_env* env, cons
         for (size_t i = lo; i < hi; ++i) {
             for (int j = 0; j < D; ++j) blk[j] = V(q[(size_t)D * i + j]);
             valid[i] = b.R->fkcc_attach(blk, e.v, b.base, e.ext) ? 1 : 0;
+        }
+    });
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_cpu_validate_motions_mask(const vgpu_robot* robot, vgpu_env* env, const float* starts,
+                                              const float* goals, size_t n, uint8_t* ok, int32_t* n_blocks,
+                                              uint8_t* block_ok, size_t block_cap, size_t* n_total, int threads)
+{
+    Bound b;
+    Env e;
+    if (!n_total || (n && (!starts || !goals || !ok))) return VGPU_ERR_INVALID_ARG;
+    if (int rc = bind(robot, b)) return rc;
+    if (int rc = view(env, e)) return rc;
+    if (e.attached && !b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
+    const int D = b.R->dim;
+    std::vector<size_t> off(n + 1, 0);  // n_e of every edge first (validate.hh:41), then their offsets
+    for (size_t i = 0; i < n; ++i) {
+        float v[kMaxDim];
+        for (int j = 0; j < D; ++j) v[j] = goals[(size_t)D * i + j] - starts[(size_t)D * i + j];
+        float nf = std::ceil(l2_norm(v, D) / 8.0f * (float)b.R->resolution);
+        if (!(nf > 1.0f)) nf = 1.0f;
+        off[i + 1] = off[i] + (size_t)(nf < 2147483520.0f ? nf : 2147483520.0f);
+    }
+    *n_total = off[n];
+    if (!block_ok || block_cap < off[n]) return VGPU_ERR_INVALID_ARG;
+    parallel_for(n, resolve_threads(threads), [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+            ok[i] = validate_all_blocks(b, e, starts + (size_t)D * i, goals + (size_t)D * i, block_ok + off[i]) ? 1 : 0;
+            if (n_blocks) n_blocks[i] = (int32_t)(off[i + 1] - off[i]);
         }
     });
     return VGPU_OK;

@@ -65,6 +65,7 @@ const RobotOps* vgpu_ur5_ops(void);
 const RobotOps* vgpu_baxter_ops(void);
 hipError_t vgpu_launch_fetch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
                                          int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
+hipError_t vgpu_launch_mask_finish(size_t n_edges, const uint32_t* off, uint8_t* ok, uint8_t* block_ok, hipStream_t st);
 hipError_t vgpu_launch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
                                    int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
 hipError_t vgpu_launch_capt_query(const float* centers, const float* radii, size_t n, const EnvView* env, int index,
@@ -1211,6 +1212,54 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
         c->acc[2] += t2;  // scatter + panda_validate_tail_kernel
         c->acc[3] += 1.0f;
     }
+    return VGPU_OK;
+}
+
+// Full-mask mode (SURVEY §8(d) "full-mask: every interpolant evaluated"): every rake block of every
+// edge is evaluated -- no early exit across an edge's blocks -- and each block's result is kept.
+extern "C" int vgpu_validate_motions_mask(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* starts,
+                                          const float* goals, size_t n_edges, uint8_t* ok, int32_t* n_blocks,
+                                          uint8_t* block_ok, size_t block_cap, size_t* n_total)
+{
+    if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
+    float b[3];
+    int rc = check_robot(c, r, b);
+    if (rc) return rc;
+    if (n_total) *n_total = 0;
+    if (n_edges == 0) return VGPU_OK;
+    if (!starts || !goals || !ok || !n_total) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if (r->kind != VGPU_ROBOT_PANDA || !c->staged)
+        return fail(c, VGPU_ERR_UNSUPPORTED, "full-mask validate: Panda (staged pipeline) only");
+    if (e->attached) return fail(c, VGPU_ERR_UNSUPPORTED, "full-mask validate: no attachments");
+    if (n_edges >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many edges in one call (< 2^31)");
+    if ((rc = vgpu_env_upload(e))) return rc;
+    const EnvView v = make_view(e);
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t *cnt, *off;
+    void* tmp;
+    size_t tmp_bytes;
+    if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
+    if ((rc = staged_pass(c, kPandaStaged, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
+    HIPCHK(c, vgpu_launch_tail_counts(starts, goals, n_edges, nullptr, n_blocks, cnt, c->cur));  // every back-step
+    HIPCHK(c, vgpu_launch_scan(cnt, off, n_edges, tmp, tmp_bytes, c->cur));
+    HIPCHK(c, hipMemcpyAsync(c->total_host, off + n_edges, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    const size_t n_items = *c->total_host;
+    *n_total = n_items + n_edges;
+    if (!block_ok || block_cap < *n_total)
+        return fail(c, VGPU_ERR_INVALID_ARG, "block_ok capacity < total blocks (*n_total)");
+    if (n_items > c->items_cap) {
+        if (c->items) HIPCHK(c, hipFree(c->items));
+        c->items = nullptr;
+        const size_t cap = std::max(n_items, (size_t)1 << 20);
+        HIPCHK(c, hipMalloc(&c->items, cap * sizeof(uint32_t)));
+        c->items_cap = cap;
+    }
+    if (n_items) {
+        HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
+        if ((rc = staged_pass(c, kPandaStaged, 4, starts, goals, c->items, off, 0, n_items, &v, b, block_ok))) return rc;
+    }
+    HIPCHK(c, vgpu_launch_mask_finish(n_edges, off, ok, block_ok, c->cur));
     return VGPU_OK;
 }
 

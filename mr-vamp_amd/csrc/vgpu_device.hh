@@ -173,6 +173,9 @@ struct EnvView {
     // x y z qx qy qz qw (+1 pad), then n_att spheres x y z r relative to it (kAttHdr floats in)
     const VGPU_CONST float* att;
     int n_att;
+    // levels of the first point cloud's split tree staged in this workgroup's LDS by
+    // capt_stage_lds (0: none -- the host-built view, and kernels that do not stage)
+    int pc_lds_levels;
 };
 constexpr int kAttHdr = 8;
 constexpr int kExtHdr = 16;
@@ -304,12 +307,43 @@ __device__ __forceinline__ bool hf_lane(const VGPU_CONST float* h, const float* 
     return signbit_f((z - r) - __builtin_fmaf(h[HF_ZS], zh, h[HF_Z]));
 }
 
+// The top VGPU_CAPT_LDS_LEVELS levels of a point cloud's split tree (tests[0 .. 2^L - 2]) staged in
+// LDS per workgroup: the descent's first L dependent loads become LDS reads instead of divergent
+// L2 gathers (SURVEY §8(a) a10 / north_star: "CAPT split planes staged in LDS").
+#ifndef VGPU_CAPT_LDS_LEVELS
+#define VGPU_CAPT_LDS_LEVELS 12
+#endif
+constexpr uint32_t kCaptLdsNodes = VGPU_CAPT_LDS_LEVELS > 0 ? (1u << VGPU_CAPT_LDS_LEVELS) - 1u : 1u;
+
+__device__ __forceinline__ float* capt_lds()
+{
+    __shared__ float top[kCaptLdsNodes];  // one per workgroup of every kernel that stages
+    return top;
+}
+
+// Cooperative copy of the first point cloud's top levels; every thread of the workgroup must call
+// it (it ends in a barrier) before any early return.
+__device__ __forceinline__ void capt_stage_lds(EnvView& env)
+{
+    if (VGPU_CAPT_LDS_LEVELS > 0 && env.n_pc > 0) {
+        const uint32_t nlog2 = hdr_u(env.pc, PC_NLOG2);
+        const uint32_t L = nlog2 < (uint32_t)VGPU_CAPT_LDS_LEVELS ? nlog2 : (uint32_t)VGPU_CAPT_LDS_LEVELS;
+        const uint32_t nodes = (1u << L) - 1u;
+        const float* __restrict__ t = env.base + hdr_u(env.pc, PC_TESTS);
+        float* top = capt_lds();
+        for (uint32_t i = threadIdx.x; i < nodes; i += blockDim.x) top[i] = t[i];
+        env.pc_lds_levels = (int)L;
+    }
+    __syncthreads();
+}
+
 // one lane of CAPT::collides_simd (capt.hh:457-541): top-box test inflated by r, descent of
 // the implicit split tree (axis cycles x, y, z), leaf point-volume box test with
 // (r + r_point)^2, then the leaf's affordance vectors, inclusive distance test.  Sums of
 // squares in the FloatVector form fma(d0, d0, fma(d2, d2, d1 * d1)) (ref_probe "sql2").
+// lds_levels > 0: the tree's first lds_levels levels are read from capt_lds().
 __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float* __restrict__ base, float x, float y,
-                                          float z, float r)
+                                          float z, float r, int lds_levels = 0)
 {
     if (!((x + r >= h[0]) && (x - r <= h[3]) && (y + r >= h[1]) && (y - r <= h[4]) && (z + r >= h[2]) &&
           (z - r <= h[5])))
@@ -318,7 +352,18 @@ __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float
     const float* __restrict__ tests = base + hdr_u(h, PC_TESTS);
     uint32_t idx = 0;
     float a = x, b = y, c = z;  // the axis of level i is i % 3
-    for (int i = 0; i < nlog2; ++i) {
+    int i = 0;
+    if (lds_levels > 0) {
+        const float* top = capt_lds();
+        for (; i < lds_levels; ++i) {
+            idx = 2u * idx + 1u + ((a >= top[idx]) ? 1u : 0u);
+            const float t = a;
+            a = b;
+            b = c;
+            c = t;
+        }
+    }
+    for (; i < nlog2; ++i) {
         idx = 2u * idx + 1u + ((a >= tests[idx]) ? 1u : 0u);
         const float t = a;
         a = b;
@@ -410,7 +455,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
         for (int i = 0; i < env.n_hf; ++i)
             if (!hit) hit = hf_lane(env.hf + kExtHdr * i, env.base, x, y, z, r);
         for (int i = 0; i < env.n_pc; ++i)
-            if (!hit) hit = capt_lane(env.pc + kExtHdr * i, env.base, x, y, z, r);
+            if (!hit) hit = capt_lane(env.pc + kExtHdr * i, env.base, x, y, z, r, i == 0 ? env.pc_lds_levels : 0);
         if (hit) acc |= 0x80000000u;
     }
     return acc;

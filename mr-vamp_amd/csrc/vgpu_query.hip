@@ -61,11 +61,13 @@ __global__ __launch_bounds__(256) void capt_query_kernel(const float* __restrict
                                                          const float* __restrict__ radii, size_t n, EnvView env,
                                                          int index, int simd, uint8_t* __restrict__ out)
 {
+    if (index == 0) capt_stage_lds(env);  // before any return: it ends in a barrier
     const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= n) return;
     const float x = centers[3 * i], y = centers[3 * i + 1], z = centers[3 * i + 2], r = radii[i];
     const VGPU_CONST float* h = env.pc + kExtHdr * index;
-    out[i] = (simd ? capt_lane(h, env.base, x, y, z, r) : capt_scalar(h, env.base, x, y, z, r)) ? 1 : 0;
+    out[i] = (simd ? capt_lane(h, env.base, x, y, z, r, index == 0 ? env.pc_lds_levels : 0)
+                   : capt_scalar(h, env.base, x, y, z, r)) ? 1 : 0;
 }
 
 // rng::Halton<dim>::next draws first .. first + n - 1, one lane per draw (random/halton.hh:73-104)

@@ -106,6 +106,24 @@ struct SrcTailT {  // validate tail: item g = (edge, back-step k), result into t
     __device__ uint32_t out(uint32_t g) const { return item_edge[g]; }
 };
 
+template <class R>
+struct SrcTailMaskT {  // full-mask mode: item g = (edge, back-step k), result into its own block slot
+    static constexpr int G = 8;
+    static constexpr bool kInit = true;  // every block gets its own flag
+    const float* starts;
+    const float* goals;
+    const uint32_t* item_edge;
+    const uint32_t* off;
+    __device__ void load(uint32_t g, int lane, float v[R::D]) const
+    {
+        const uint32_t e = item_edge[g];
+        const int k = (int)(g - off[e]) + 1;
+        R::tail(starts + R::D * (size_t)e, goals + R::D * (size_t)e, lane, k, v);
+    }
+    // block k of edge e sits at off[e] + e + k (edges laid out block 0 .. n_e - 1 in edge order)
+    __device__ uint32_t out(uint32_t g) const { return g + item_edge[g] + 1u; }
+};
+
 template <int G>
 struct GrpOf;
 template <>
@@ -171,6 +189,7 @@ __global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void bound_kernel(Src
 {
     using Grp = typename GrpOf<Src::G>::T;
     using M = typename R::Mask;
+    if constexpr (EXT) capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
     const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
     const uint32_t g = (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);
@@ -267,6 +286,7 @@ __global__ __launch_bounds__(kStagedBlock, R::kChildWavesPerEU) void children_ke
                                                                                 float bz, uint8_t* __restrict__ valid)
 {
     using Grp = typename GrpOf<Src::G>::T;
+    if constexpr (EXT) capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
     const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
     const uint32_t item = (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);
@@ -350,7 +370,8 @@ struct StagedHost {
     }
 
     // dispatch on the source kind: 0 configurations (s0 = q), 1 Halton samples (first, s0 = q_out
-    // or NULL), 2 validate head (s0 = starts, s1 = goals), 3 validate tail (+ s2 = item_edge, s3 = off)
+    // or NULL), 2 validate head (s0 = starts, s1 = goals), 3 validate tail (+ s2 = item_edge, s3 = off),
+    // 4 full-mask tail (as 3, one result per block)
     template <class Fn>
     static hipError_t with_source(int kind, const void* s0, const void* s1, const void* s2, const void* s3,
                                   uint64_t first, Fn fn)
@@ -364,6 +385,8 @@ struct StagedHost {
             return fn(SrcHeadT<R>{(const float*)s0, (const float*)s1});
         case 3:
             return fn(SrcTailT<R>{(const float*)s0, (const float*)s1, (const uint32_t*)s2, (const uint32_t*)s3});
+        case 4:
+            return fn(SrcTailMaskT<R>{(const float*)s0, (const float*)s1, (const uint32_t*)s2, (const uint32_t*)s3});
         }
         return hipErrorInvalidValue;
     }

@@ -52,12 +52,36 @@ __global__ __launch_bounds__(kBlock) void tail_counts_kernel(const float* __rest
     if (e >= n_edges) return;
     const Rake rk = rake_setup(starts + 7 * e, goals + 7 * e);
     if (n_blocks) n_blocks[e] = rk.n;
-    cnt[e] = (ok[e] && rk.n > 1) ? (uint32_t)(rk.n - 1) : 0u;
+    cnt[e] = ((!ok || ok[e]) && rk.n > 1) ? (uint32_t)(rk.n - 1) : 0u;  // ok = NULL: every back-step (full mask)
+}
+
+// full-mask mode: edge e's blocks at off[e] + e .. (+ n_e - 1); block 0 is the head's result, and the
+// edge is valid when all of its blocks are
+__global__ __launch_bounds__(kBlock) void mask_finish_kernel(size_t n_edges, const uint32_t* __restrict__ off,
+                                                             uint8_t* __restrict__ ok, uint8_t* __restrict__ block_ok)
+{
+    const size_t e = (size_t)blockIdx.x * kBlock + threadIdx.x;
+    if (e >= n_edges) return;
+    const size_t base = (size_t)off[e] + e;
+    const uint32_t nb = off[e + 1] - off[e] + 1u;
+    uint8_t all = ok[e];
+    block_ok[base] = all;
+    for (uint32_t k = 1; k < nb; ++k) all &= block_ok[base + k];
+    ok[e] = all;
 }
 
 }  // namespace vgpu
 
 VGPU_STAGED_EXPORTS(vgpu::PandaR, panda)
+
+extern "C" hipError_t vgpu_launch_mask_finish(size_t n_edges, const uint32_t* off, uint8_t* ok, uint8_t* block_ok,
+                                               hipStream_t st)
+{
+    if (n_edges == 0) return hipSuccess;
+    const unsigned grid = (unsigned)((n_edges + vgpu::kBlock - 1) / vgpu::kBlock);
+    hipLaunchKernelGGL(vgpu::mask_finish_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, n_edges, off, ok, block_ok);
+    return hipGetLastError();
+}
 
 extern "C" hipError_t vgpu_launch_tail_counts(const float* starts, const float* goals, size_t n_edges,
                                               const uint8_t* ok, int32_t* n_blocks, uint32_t* cnt, hipStream_t st)

@@ -682,6 +682,26 @@ class Robot:
                  out.ctypes.data_as(_lib.U8P), int(threads)))
         return out.astype(bool)
 
+    def cpu_validate_mask(self, starts, goals, environment: Environment, threads: int = 0):
+        """Full-mask validate on the CPU rake: (ok, n_e, block_ok [sum n_e], block offsets [n+1])."""
+        s = np.ascontiguousarray(starts, np.float32).reshape(-1, self.dimension())
+        g = np.ascontiguousarray(goals, np.float32).reshape(-1, self.dimension())
+        n = s.shape[0]
+        ok = np.empty(n, np.uint8)
+        nb = np.empty(n, np.int32)
+        tot = C.c_size_t()
+        lib = load()
+        args = (C.byref(self.c_robot), environment.host_handle(), s.ctypes.data_as(_lib.F32P),
+                g.ctypes.data_as(_lib.F32P), n, ok.ctypes.data_as(_lib.U8P), nb.ctypes.data_as(_lib.I32P))
+        rc = lib.vgpu_cpu_validate_motions_mask(*args, None, 0, C.byref(tot), int(threads))
+        if rc != _lib.VGPU_OK and tot.value == 0 and n:
+            check(rc)
+        blk = np.empty(max(tot.value, 1), np.uint8)
+        check(lib.vgpu_cpu_validate_motions_mask(*args, blk.ctypes.data_as(_lib.U8P), blk.size, C.byref(tot),
+                                                 int(threads)))
+        off = np.concatenate([[0], np.cumsum(nb.astype(np.int64))])
+        return ok.astype(bool), nb, blk[:tot.value].astype(bool), off
+
     def cpu_validate_batch(self, starts, goals, environment: Environment, threads: int = 0):
         """validate_motion of every edge on the CPU rake: (ok, n_e, blocks evaluated)."""
         s = np.ascontiguousarray(starts, np.float32).reshape(-1, self.dimension())
@@ -768,6 +788,18 @@ class Robot:
         ctx = ctx or context()
         check(load().vgpu_fkcc(ctx.h, C.byref(self.c_robot), environment.handle(ctx), C.c_void_p(q_ptr), n,
                                C.c_void_p(valid_ptr)), ctx.h)
+
+    def validate_mask_device(self, starts_ptr: int, goals_ptr: int, n: int, environment: Environment, ok_ptr: int,
+                             nblocks_ptr: int, block_ok_ptr: int, block_cap: int, ctx: Optional[Context] = None) -> int:
+        """Full-mask validate (every rake block evaluated, each block's result kept): returns the
+        number of blocks written to block_ok (edge-major, block 0 .. n_e - 1)."""
+        ctx = ctx or context()
+        total = C.c_size_t()
+        check(load().vgpu_validate_motions_mask(ctx.h, C.byref(self.c_robot), environment.handle(ctx),
+                                                C.c_void_p(starts_ptr), C.c_void_p(goals_ptr), n, C.c_void_p(ok_ptr),
+                                                C.c_void_p(nblocks_ptr or 0), C.c_void_p(block_ok_ptr), block_cap,
+                                                C.byref(total)), ctx.h)
+        return int(total.value)
 
     def validate_device(self, starts_ptr: int, goals_ptr: int, n: int, environment: Environment, ok_ptr: int,
                         nblocks_ptr: int = 0, ctx: Optional[Context] = None):

@@ -83,6 +83,8 @@ SIGNATURES = {
     "vgpu_sphere_fk": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, C.c_size_t, VP, C.c_size_t]),
     "vgpu_fkcc": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, C.c_size_t, VP]),
     "vgpu_validate_motions": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, VP, C.c_size_t, VP, VP]),
+    "vgpu_validate_motions_mask": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, VP, VP, C.c_size_t, VP, VP, VP, C.c_size_t,
+                                             C.POINTER(C.c_size_t)]),
     "vgpu_sphere_fk_host": (C.c_int, [VP, C.POINTER(VgpuRobot), F32P, C.c_size_t, F32P]),
     "vgpu_fkcc_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P]),
     "vgpu_validate_motions_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P]),
@@ -106,6 +108,8 @@ SIGNATURES = {
     "vgpu_cpu_validate_motion": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.POINTER(C.c_int)]),
     "vgpu_cpu_fkcc": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P, C.c_int]),
     "vgpu_cpu_fkcc_attach": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.c_size_t, U8P, C.c_int]),
+    "vgpu_cpu_validate_motions_mask": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P, U8P,
+                                                 C.c_size_t, C.POINTER(C.c_size_t), C.c_int]),
     "vgpu_cpu_validate_motions": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P, I32P,
                                             C.c_int]),
     "vgpu_l2_norm": (C.c_float, [F32P, C.c_int]),

@@ -202,3 +202,35 @@ def test_single_calls_and_errors(vamp, oracle):
     assert lib.vgpu_cpu_fkcc_attach_block(C.byref(vamp.panda_0_0.c_robot), env.host_handle(),
                                           blk.ctypes.data_as(_lib.F32P), C.byref(v)) == -1  # nothing attached
     assert vamp.panda_0_0.cpu_fkcc_batch(np.zeros((0, 7), F), env).shape == (0,)
+
+
+def rake_blocks(s, g, n):
+    """the rake blocks validate_vector enumerates (validate.hh:31-56): block 0 = fma(v, (l+1)/8, s),
+    then n - 1 back-steps of v / (8 n); returns [n][8][dim]"""
+    v = (g - s).astype(F)
+    pct = np.arange(1, 9, dtype=np.float64) / 8.0
+    b = (v.astype(np.float64)[None, :] * pct[:, None] + s.astype(np.float64)[None, :]).astype(F)  # exact fma here
+    back = (v / F(8 * n)).astype(F)
+    out = [b]
+    for _ in range(1, n):
+        b = (b - back[None, :]).astype(F)
+        out.append(b)
+    return np.stack(out)
+
+
+def test_full_mask_blocks(vamp, oracle):
+    """full-mask mode: every block of every edge, each block's result == the oracle's fkcc of that
+    8-lane block (group semantics); the edge result == the early-exit validate_motion."""
+    fx = host_fixture("edges_panda_cage.npz", oracle)
+    oenv = oracle.sphere_cage_env()
+    env = gpu_env_from_oracle(vamp, oenv)
+    s, g = fx["starts"][:600], fx["goals"][:600]
+    ok, n, blk, off = vamp.panda_0_0.cpu_validate_mask(s, g, env, threads=4)
+    ook, on = oracle.validate_motions(oenv, s, g, (0, 0, 0))
+    assert np.array_equal(ok, ook) and np.array_equal(n, on) and off[-1] == blk.size == n.sum()
+    for e in range(0, 600, 7):
+        want = oracle.fkcc(oenv, rake_blocks(s[e], g[e], int(n[e])).reshape(-1, 7), (0, 0, 0), G=8)
+        assert np.array_equal(blk[off[e]:off[e + 1]], want), e
+    # a rejected edge may have valid later blocks: the full mask evaluates them anyway
+    tails = [blk[off[e] + 1:off[e + 1]] for e in np.flatnonzero(~ok) if n[e] > 1]
+    assert any(t.any() for t in tails)

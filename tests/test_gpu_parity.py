@@ -169,3 +169,36 @@ def test_large_batch_properties(vamp, oracle):
     idx = rng.choice(len(q), 65536, replace=False)
     assert np.array_equal(v_cage[idx], oracle.fkcc_threads(oenv, q[idx], (0, 0, 0)))
     assert 0.15 < v_cage.mean() < 0.21
+
+
+def test_full_mask_mode(vamp, oracle):
+    """vgpu_validate_motions_mask (every block evaluated, each block's result kept) == the CPU rake's
+    full mask (itself == the oracle per block, tests/test_cpu_rake.py), and its edge results == the
+    early-exit validate_motions."""
+    import torch
+    rng = np.random.default_rng(21)
+    oenv = oracle.sphere_cage_env()
+    env = gpu_env_from_oracle(vamp, oenv)
+    s = oracle.scale(rng.random((20000, 7), dtype=F))
+    g = oracle.scale(rng.random((20000, 7), dtype=F))
+    g[:10000] = s[:10000] + (g[:10000] - s[:10000]) * F(0.2)
+    g[:5] = s[:5]
+    ok_c, n_c, blk_c, _ = vamp.panda_0_0.cpu_validate_mask(s, g, env)
+    dev = torch.device("cuda", 0)
+    ds, dg = torch.from_numpy(s).to(dev), torch.from_numpy(g).to(dev)
+    ok = torch.empty(len(s), dtype=torch.uint8, device=dev)
+    nb = torch.empty(len(s), dtype=torch.int32, device=dev)
+    blk = torch.empty(int(n_c.sum()) + 7, dtype=torch.uint8, device=dev)
+    ctx = vamp.context(0)
+    total = vamp.panda_0_0.validate_mask_device(ds.data_ptr(), dg.data_ptr(), len(s), env, ok.data_ptr(),
+                                                nb.data_ptr(), blk.data_ptr(), blk.numel(), ctx)
+    ctx.sync()
+    assert total == int(n_c.sum())
+    assert np.array_equal(nb.cpu().numpy(), n_c)
+    assert np.array_equal(ok.cpu().numpy().astype(bool), ok_c)
+    assert np.array_equal(blk[:total].cpu().numpy().astype(bool), blk_c)
+    ok_e, _ = vamp.panda_0_0.validate_batch(s, g, env)
+    assert np.array_equal(ok_e, ok_c)
+    with pytest.raises(vamp.VgpuError):  # capacity below the block count
+        vamp.panda_0_0.validate_mask_device(ds.data_ptr(), dg.data_ptr(), len(s), env, ok.data_ptr(), 0,
+                                            blk.data_ptr(), 10, ctx)
