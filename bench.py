@@ -726,6 +726,17 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                "sample": f"{m} configurations of the same workload, mr-vamp_amd/csrc/cpu AVX2 rake fkcc (broadcast "
                          f"block per configuration, CAPT collides_simd), {threads} threads, {dt:.1f} s",
                "cpu_model": cpu_model()}
+    # HBM bytes per fkcc call from the committed PMC passes of the same workload (tools/gpu_capt_pmc.sh):
+    # (2 * FETCH_SIZE + WRITE_SIZE) KB of the bound + children kernels (FETCH_SIZE doubled per
+    # MI355X_MICROARCH.md; gathers are narrower than the streaming reads it was calibrated on, so
+    # this is an upper estimate), plus their L2 hit rates
+    pmc = traffic_record(os.path.join(ROOT, "profiles", "r02_capt_pmc.json"))
+    traffic, l2 = None, None
+    if pmc:
+        ks = [v for k, v in pmc["kernels"].items() if k.startswith(("bound_kernel", "children_kernel"))]
+        if ks and all("FETCH_SIZE" in v and "WRITE_SIZE" in v for v in ks):
+            traffic = sum(2 * v["FETCH_SIZE"] + v["WRITE_SIZE"] for v in ks) * 1024.0
+        l2 = {k.split("<")[0]: v.get("L2_hit_rate") for k, v in pmc["kernels"].items()}
     line = contract_line(
         a, world, wall_max, units_all, "CAPT point-cloud collision queries/sec (Panda 7-DOF fkcc vs 10k-point cloud)",
         "configs/s", "weak", "synthetic (10k points on the cage spheres, seed 1; uniform Panda configurations)",
@@ -733,9 +744,12 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "robot": "PandaBase<0,0,0>", "configs_per_gpu": N, "valid_fraction": float(ok.float().mean().item()),
          "parallelism": f"dp{world} (independent shards, no collective)"},
         {"kernel": "fkcc (staged, point-cloud ext path)", "bound": "valu", "achieved": achieved,
-         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None,
-         "algorithmic_flops_per_config": f_cfg, "step_ms": kern_s * 1e3,
-         "note": "gather/latency-bound descent + affordance scan; CAPT arrays (~4.7 MB) L2/MALL resident"},
+         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
+         "algorithmic_flops_per_config": f_cfg, "step_ms": kern_s * 1e3, "l2_hit_rate": l2,
+         "traffic_source": "profiles/r02_capt_pmc.json (tools/gpu_capt_pmc.sh: rocprofv3 --pmc FETCH_SIZE, "
+                           "WRITE_SIZE, TCC_HIT_sum/TCC_MISS_sum in separate passes)",
+         "note": "gather/latency-bound descent + affordance scan; split tree's top 12 levels staged in LDS per "
+                 "workgroup; CAPT arrays (~4.7 MB) L2/MALL resident"},
         cpu)
     line["parity"] = parity
     print(json.dumps(line))

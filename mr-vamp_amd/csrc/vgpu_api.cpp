@@ -234,6 +234,11 @@ struct vgpu_ctx {
     // roadmap kNN chunk lists (vgpu_roadmap.hip)
     uint32_t* knn_part = nullptr;
     size_t knn_part_cap = 0;
+    // roadmap kNN spatial index (vgpu_knn_index.hip): 0 auto (index from kKnnIndexMin vertices),
+    // 1 brute force, 2 index; its scratch pool
+    int knn_mode = 0;
+    uint32_t* knn_idx = nullptr;
+    size_t knn_idx_cap = 0;
     // optional phase timing
     bool prof = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -297,6 +302,7 @@ extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
     }
     c->cur = c->own;
     if (const char* s = std::getenv("VAMP_AMD_STAGED")) c->staged = std::strcmp(s, "0") != 0;
+    if (const char* s = std::getenv("VAMP_AMD_KNN")) c->knn_mode = std::atoi(s);
     if (const char* s = std::getenv("VAMP_AMD_ROUNDS")) {  // A/B: comma-separated check bit masks
         for (const char* p = s; *p;) {
             char* end = nullptr;
@@ -337,6 +343,7 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->st_cnt) (void)hipFree(c->st_cnt);
     if (c->st_items) (void)hipFree(c->st_items);
     if (c->knn_part) (void)hipFree(c->knn_part);
+    if (c->knn_idx) (void)hipFree(c->knn_idx);
     if (c->st_host) (void)hipHostFree(c->st_host);
     if (c->total_host) (void)hipHostFree(c->total_host);
     for (auto& ev : c->ev)
@@ -1609,7 +1616,23 @@ extern "C" int vgpu_prm_neighbor_params(int dim, double space_measure, double ga
     return VGPU_OK;
 }
 
+extern "C" size_t vgpu_knn_index_bytes(int dim, uint32_t n, uint32_t q_count);
+extern "C" hipError_t vgpu_launch_knn_index(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
+                                            const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr,
+                                            float* dist, uint32_t* cnt, void* pool, size_t pool_bytes,
+                                            hipStream_t st);
+
 static bool knn_dim_ok(int dim) { return dim == 6 || dim == 7 || dim == 8 || dim == 14; }
+
+// below this many vertices the brute-force scan is as fast as building the index
+static constexpr size_t kKnnIndexMin = 16384;
+
+extern "C" int vgpu_set_knn_mode(vgpu_ctx* c, int mode)
+{
+    if (!c || mode < 0 || mode > 2) return VGPU_ERR_INVALID_ARG;
+    c->knn_mode = mode;
+    return VGPU_OK;
+}
 
 extern "C" int vgpu_roadmap_knn_range(vgpu_ctx* c, int dim, const float* V, size_t n, size_t q_first, size_t q_count,
                                       const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr, float* dist,
@@ -1623,11 +1646,20 @@ extern "C" int vgpu_roadmap_knn_range(vgpu_ctx* c, int dim, const float* V, size
     if (n && (!V || !k || !r || !nbr || !dist || !cnt)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
     HIPCHK(c, hipSetDevice(c->device));
     if (q_count == 0) return VGPU_OK;
+    int rc;
+    const bool index = c->knn_mode == 2 || (c->knn_mode == 0 && n >= kKnnIndexMin);
+    if (index) {
+        const size_t bytes = vgpu_knn_index_bytes(dim, (uint32_t)n, (uint32_t)q_count);
+        if (!bytes) return fail(c, VGPU_ERR_HIP, "roadmap kNN index: scratch size query failed");
+        if ((rc = grow(c, &c->knn_idx, &c->knn_idx_cap, (bytes + 3) / 4))) return rc;
+        HIPCHK(c, vgpu_launch_knn_index(dim, V, (uint32_t)n, (uint32_t)q_first, (uint32_t)q_count, k, r, kmax, nbr,
+                                        dist, cnt, c->knn_idx, c->knn_idx_cap * 4, c->cur));
+        return VGPU_OK;
+    }
     uint32_t S = 0;
     const size_t C = vgpu_knn_chunks(n, &S);
     // chunk lists (context-owned, grown on demand): distances, indices, counts
     const size_t cells = q_count * C, need = cells * (2 * (size_t)kmax + 1);
-    int rc;
     if ((rc = grow(c, &c->knn_part, &c->knn_part_cap, need))) return rc;
     float* pd = (float*)c->knn_part;
     uint32_t* pi = c->knn_part + cells * kmax;

@@ -1,0 +1,480 @@
+// vgpu_knn_index.hip -- the roadmap neighbour queries (planning/prm.hh:264-266, NN::nearest over
+// vertices 0 .. i-1; nn.hh:89-95) through a spatial index, for roadmaps far beyond what the
+// brute-force scan of vgpu_roadmap.hip reaches (BASELINE configs[3]: ~2.7M Fetch vertices; the
+// brute force is O(n^2) pair tests).
+//
+// Index (rebuilt per call, all on the stream, no host sync):
+//   1. per-dimension min/max of the vertices (block partials, one final block);
+//   2. a Morton key per vertex: 64/dim bits per dimension, interleaved (dim 8: 8 bits each);
+//   3. a stable radix sort of (key, vertex) -> perm (sorted position -> vertex);
+//   4. tiles of 64 consecutive sorted positions: the tile's coordinates (row-major, vertex
+//      order = sorted order), its axis-aligned box and its smallest vertex index.
+// Query: one wave = 64 queries that are consecutive in sorted order (spatially close).  The wave
+// visits the tiles outward from its own (home, home+1, home-1, ...) so its lists fill early;
+// a tile is skipped when no lane can take anything from it: its smallest vertex index is not
+// below the lane's vertex (the causal prefix), or the box's squared distance exceeds the lane's
+// squared bound (k-th key or r) by more than a relative 1e-4 (the box bound is computed in
+// another summation order than the candidate distance; float differences and squares are
+// monotone, so the margin only has to cover the sum's rounding, <= 14 * 2^-24 relative).
+// Candidates of a visited tile are held one per lane and broadcast with v_readlane; the test,
+// the correctly rounded sqrt and the register top-K list are those of vgpu_roadmap.hip.
+// Candidates arrive in tile order, not index order, so admission compares full keys (distance,
+// index): the list ends as the k smallest keys of {j < i : d(i, j) <= r}, exactly the brute
+// force's result (which scans in index order, where "strictly closer" is the same key order).
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+
+#include "vgpu_device.hh"
+
+namespace vgpu {
+namespace knnidx {
+
+constexpr int kTile = 64;      // candidates per tile = one wave
+constexpr int kQBlock = 256;   // four query waves per block
+constexpr int kBuf = 8;        // buffered candidates per lane between insertion passes
+constexpr int kMinMaxBlocks = 256;
+
+template <int D>
+constexpr int bits_per_dim() { return 64 / D; }
+
+// l2_norm of a - b before its sqrt, in the AVX hsum order (vgpu_roadmap.hip config_sumsq)
+template <int D>
+__device__ __forceinline__ float sumsq(const float* a, const float* b)
+{
+    float v[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) v[j] = a[j] - b[j];
+    float sq[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const float lo = j < D ? v[j < D ? j : 0] : 0.0f;
+        if (D <= 8) {
+            sq[j] = lo * lo;
+        } else {
+            const float hi = (j + 8 < D) ? v[(j + 8 < D) ? j + 8 : 0] : 0.0f;
+            sq[j] = __builtin_fmaf(lo, lo, hi * hi);
+        }
+    }
+    return ((sq[0] + sq[4]) + (sq[2] + sq[6])) + ((sq[1] + sq[5]) + (sq[3] + sq[7]));
+}
+
+template <int K>
+__device__ __forceinline__ void list_insert(float (&bd)[K], uint32_t (&bi)[K], float cd, uint32_t ci)
+{
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        const bool lt = cd < bd[m] || (cd == bd[m] && ci < bi[m]);
+        const float td = bd[m];
+        const uint32_t ti = bi[m];
+        bd[m] = lt ? cd : td;
+        bi[m] = lt ? ci : ti;
+        cd = lt ? td : cd;
+        ci = lt ? ti : ci;
+    }
+}
+
+__device__ __forceinline__ float wave_min(float v)
+{
+    for (int o = 32; o >= 1; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v)
+{
+    for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_umin(uint32_t v)
+{
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+// per-block partial min/max of every dimension: part[block][2D] = (min[D], max[D])
+template <int D>
+__global__ __launch_bounds__(256) void minmax_kernel(const float* __restrict__ V, uint32_t n, float* __restrict__ part)
+{
+    float lo[D], hi[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        lo[d] = __builtin_inff();
+        hi[d] = -__builtin_inff();
+    }
+    for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float x = V[(size_t)i * D + d];
+            lo[d] = fminf(lo[d], x);
+            hi[d] = fmaxf(hi[d], x);
+        }
+    }
+    __shared__ float s[4][2 * D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        lo[d] = wave_min(lo[d]);
+        hi[d] = wave_max(hi[d]);
+    }
+    if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            s[threadIdx.x >> 6][d] = lo[d];
+            s[threadIdx.x >> 6][D + d] = hi[d];
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2 * D) {
+        const int e = threadIdx.x;
+        float v = s[0][e];
+        for (int w = 1; w < 4; ++w) v = e < D ? fminf(v, s[w][e]) : fmaxf(v, s[w][e]);
+        part[(size_t)blockIdx.x * 2 * D + e] = v;
+    }
+}
+
+// ls[0..D) = per-dimension origin, ls[D..2D) = scale to [0, 2^B - 1] (0 for a flat or non-finite range)
+template <int D>
+__global__ __launch_bounds__(64) void scale_kernel(const float* __restrict__ part, uint32_t nparts, float* __restrict__ ls)
+{
+    const int d = threadIdx.x;
+    if (d >= D) return;
+    float lo = __builtin_inff(), hi = -__builtin_inff();
+    for (uint32_t b = 0; b < nparts; ++b) {
+        lo = fminf(lo, part[(size_t)b * 2 * D + d]);
+        hi = fmaxf(hi, part[(size_t)b * 2 * D + D + d]);
+    }
+    const float top = (float)((1u << bits_per_dim<D>()) - 1u);
+    const float span = hi - lo;
+    const bool ok = span > 0.0f && span < __builtin_inff();
+    ls[d] = ok ? lo : 0.0f;
+    ls[D + d] = ok ? top / span : 0.0f;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void key_kernel(const float* __restrict__ V, uint32_t n, const float* __restrict__ ls,
+                                                  uint64_t* __restrict__ key, uint32_t* __restrict__ id)
+{
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    constexpr int B = bits_per_dim<D>();
+    const float top = (float)((1u << B) - 1u);
+    uint64_t k = 0;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float f = fminf(fmaxf((V[(size_t)i * D + d] - ls[d]) * ls[D + d], 0.0f), top);  // NaN -> 0
+        const uint32_t q = (uint32_t)f;
+#pragma unroll
+        for (int b = 0; b < B; ++b) k |= (uint64_t)((q >> b) & 1u) << (b * D + d);
+    }
+    key[i] = k;
+    id[i] = i;
+}
+
+// one wave per tile: sorted coordinates, the box and the smallest vertex index
+template <int D>
+__global__ __launch_bounds__(64) void tile_kernel(const float* __restrict__ V, const uint32_t* __restrict__ perm,
+                                                  uint32_t n, float* __restrict__ Vs, float* __restrict__ tbox,
+                                                  uint32_t* __restrict__ tmin)
+{
+    const uint32_t t = blockIdx.x;
+    const uint32_t p = t * kTile + threadIdx.x;
+    const bool ok = p < n;
+    const uint32_t j = ok ? perm[p] : 0xFFFFFFFFu;
+    float lo[D], hi[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float x = ok ? V[(size_t)j * D + d] : 0.0f;
+        if (ok) Vs[(size_t)p * D + d] = x;
+        lo[d] = wave_min(ok ? x : __builtin_inff());
+        hi[d] = wave_max(ok ? x : -__builtin_inff());
+    }
+    const uint32_t jm = wave_umin(j);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            tbox[(size_t)t * 2 * D + d] = lo[d];
+            tbox[(size_t)t * 2 * D + D + d] = hi[d];
+        }
+        tmin[t] = jm;
+    }
+}
+
+// sorted positions of the queries q_first .. q_end-1 (flag for the select)
+__global__ __launch_bounds__(256) void qflag_kernel(const uint32_t* __restrict__ perm, uint32_t n, uint32_t q_first,
+                                                    uint32_t q_end, uint8_t* __restrict__ flag)
+{
+    const uint32_t p = blockIdx.x * 256 + threadIdx.x;
+    if (p >= n) return;
+    const uint32_t i = perm[p];
+    flag[p] = (i >= q_first && i < q_end) ? 1 : 0;
+}
+
+__device__ __forceinline__ float bcast(float v, uint32_t lane)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), (int)lane));
+}
+__device__ __forceinline__ uint32_t bcast(uint32_t v, uint32_t lane)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)lane);
+}
+
+template <int D, int K>
+__global__ __launch_bounds__(kQBlock) void query_kernel(const float* __restrict__ Vs, const uint32_t* __restrict__ perm,
+                                                        uint32_t n, uint32_t T, const float* __restrict__ tbox,
+                                                        const uint32_t* __restrict__ tmin,
+                                                        const uint32_t* __restrict__ qlist, uint32_t q_first,
+                                                        uint32_t q_count, const uint32_t* __restrict__ kq,
+                                                        const float* __restrict__ rq, uint32_t kmax,
+                                                        uint32_t* __restrict__ nbr, float* __restrict__ dist,
+                                                        uint32_t* __restrict__ cnt)
+{
+    __shared__ float buf_d[kBuf][kQBlock];
+    __shared__ uint32_t buf_i[kBuf][kQBlock];
+    const uint32_t wave = blockIdx.x * (kQBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t slot = threadIdx.x;
+    if (wave * 64 >= q_count) return;  // wave-uniform; the kernel has no block barrier
+    const uint32_t qo = wave * 64 + lane;
+    const bool inq = qo < q_count;
+    const uint32_t p = inq ? (qlist ? qlist[qo] : qo) : 0u;
+    const uint32_t i = inq ? perm[p] : 0xFFFFFFFFu;
+    const bool live = inq && i >= 2;  // vertices 0, 1 (start, goal) query nothing (prm.hh:228-233)
+    float me[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) me[d] = inq ? Vs[(size_t)p * D + d] : 0.0f;
+    const uint32_t k = live ? min(kq[i], (uint32_t)K) : 0u;
+    const float r = live ? rq[i] : -1.0f;
+    float bd[K];
+    uint32_t bi[K];
+#pragma unroll
+    for (int m = 0; m < K; ++m) {
+        bd[m] = __builtin_inff();
+        bi[m] = 0xFFFFFFFFu;
+    }
+    uint32_t c = 0, nb = 0;
+    float worst = r;            // admission bound: r while fewer than k are held, else the k-th key
+    uint32_t worst_i = 0xFFFFFFFFu;
+    float thr = live && k ? r * r * 1.000001f : -1.0f;  // sqrt plausibility bound (vgpu_roadmap.hip)
+    auto flush = [&]() {
+        for (uint32_t m = 0; __builtin_amdgcn_ballot_w64(m < nb) != 0ull; ++m) {
+            const bool has = m < nb;
+            list_insert<K>(bd, bi, has ? buf_d[has ? m : 0][slot] : __builtin_inff(),
+                           has ? buf_i[has ? m : 0][slot] : 0xFFFFFFFFu);
+        }
+        c = min(c + nb, k);
+        nb = 0;
+        float kth = r;
+        uint32_t kth_i = 0xFFFFFFFFu;
+#pragma unroll
+        for (int m = 0; m < K; ++m)
+            if ((uint32_t)m + 1 == k) {
+                kth = bd[m];
+                kth_i = bi[m];
+            }
+        worst = (c == k) ? kth : r;
+        worst_i = (c == k) ? kth_i : 0xFFFFFFFFu;
+        thr = live && k ? worst * worst * 1.000001f : -1.0f;
+    };
+    auto consider = [&](bool need, uint32_t j, float s) {
+        const bool pre = need && j < i && s <= thr;
+        if (__builtin_amdgcn_ballot_w64(pre) == 0ull) return;
+        const float dd = __builtin_sqrtf(s);
+        // nn query semantics: distance <= r; once k are held, only a smaller key displaces the k-th
+        const bool take = pre && (c < k ? dd <= worst : (dd < worst || (dd == worst && j < worst_i)));
+        if (take) {
+            buf_d[nb][slot] = dd;
+            buf_i[nb][slot] = j;
+            ++nb;
+        }
+    };
+    const uint32_t home = __builtin_amdgcn_readfirstlane(p) / kTile;
+    for (uint32_t s = 0; s < 2 * T; ++s) {
+        const int64_t t64 = (s & 1u) ? (int64_t)home + (int64_t)((s + 1) / 2) : (int64_t)home - (int64_t)(s / 2);
+        if (t64 < 0 || t64 >= (int64_t)T) continue;
+        const uint32_t t = (uint32_t)t64;
+        const float* bx = tbox + (size_t)t * 2 * D;
+        float lb = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            const float g = fmaxf(fmaxf(bx[d] - me[d], me[d] - bx[D + d]), 0.0f);
+            lb = __builtin_fmaf(g, g, lb);
+        }
+        const bool need = live && tmin[t] < i && lb <= thr * 1.0001f;
+        if (__builtin_amdgcn_ballot_w64(need) == 0ull) continue;
+        const uint32_t cp = t * kTile + lane;
+        float cv[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d) cv[d] = cp < n ? Vs[(size_t)cp * D + d] : 0.0f;
+        const uint32_t cj = cp < n ? perm[cp] : 0xFFFFFFFFu;  // a missing candidate is never < i
+        for (uint32_t u = 0; u < (uint32_t)kTile; u += 4) {
+            float s4[4];
+            uint32_t j4[4];
+            bool any = false;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                float cc[D];
+#pragma unroll
+                for (int d = 0; d < D; ++d) cc[d] = bcast(cv[d], u + h);
+                j4[h] = bcast(cj, u + h);
+                s4[h] = sumsq<D>(cc, me);
+                any |= need && j4[h] < i && s4[h] <= thr;
+            }
+            if (__builtin_amdgcn_ballot_w64(any) == 0ull) continue;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) consider(need, j4[h], s4[h]);
+            if (__builtin_amdgcn_ballot_w64(nb > kBuf - 4) != 0ull) flush();
+        }
+        if (__builtin_amdgcn_ballot_w64(nb != 0) != 0ull) flush();
+    }
+    if (inq) {
+        const size_t o = (size_t)(i - q_first);
+        cnt[o] = c;
+#pragma unroll
+        for (int m = 0; m < K; ++m) {
+            if ((uint32_t)m < c) {
+                nbr[o * kmax + m] = bi[m];
+                dist[o * kmax + m] = bd[m];
+            }
+        }
+    }
+}
+
+inline size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+
+struct Layout {
+    size_t part, ls, key0, key1, id0, perm, Vs, tbox, tmin, flag, qlist, nsel, tmp, total;
+};
+
+template <int D>
+hipError_t layout(uint32_t n, uint32_t q_count, Layout& L)
+{
+    const uint32_t T = (n + kTile - 1) / kTile;
+    size_t tsort = 0, tsel = 0;
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                                                      (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n, 0,
+                                                      D * bits_per_dim<D>());
+    if (e != hipSuccess) return e;
+    e = hipcub::DeviceSelect::Flagged(nullptr, tsel, hipcub::CountingInputIterator<uint32_t>(0), (uint8_t*)nullptr,
+                                      (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n);
+    if (e != hipSuccess) return e;
+    size_t o = 0;
+    auto take = [&](size_t bytes) {
+        const size_t at = o;
+        o += al256(bytes ? bytes : 1);
+        return at;
+    };
+    L.part = take((size_t)kMinMaxBlocks * 2 * D * 4);
+    L.ls = take(2 * D * 4);
+    L.key0 = take((size_t)n * 8);
+    L.key1 = take((size_t)n * 8);
+    L.id0 = take((size_t)n * 4);
+    L.perm = take((size_t)n * 4);
+    L.Vs = take((size_t)n * D * 4);
+    L.tbox = take((size_t)T * 2 * D * 4);
+    L.tmin = take((size_t)T * 4);
+    L.flag = take(n);
+    L.qlist = take((size_t)q_count * 4);
+    L.nsel = take(4);
+    L.tmp = take(std::max(tsort, tsel));
+    L.total = o;
+    return hipSuccess;
+}
+
+template <int D, int K>
+hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, const uint32_t* k, const float* r,
+               uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, char* pool, size_t pool_bytes, hipStream_t st)
+{
+    Layout L;
+    hipError_t e = layout<D>(n, q_count, L);
+    if (e != hipSuccess) return e;
+    if (pool_bytes < L.total) return hipErrorInvalidValue;
+    const uint32_t T = (n + kTile - 1) / kTile;
+    float* part = (float*)(pool + L.part);
+    float* ls = (float*)(pool + L.ls);
+    uint64_t* key0 = (uint64_t*)(pool + L.key0);
+    uint64_t* key1 = (uint64_t*)(pool + L.key1);
+    uint32_t* id0 = (uint32_t*)(pool + L.id0);
+    uint32_t* perm = (uint32_t*)(pool + L.perm);
+    float* Vs = (float*)(pool + L.Vs);
+    float* tbox = (float*)(pool + L.tbox);
+    uint32_t* tmin = (uint32_t*)(pool + L.tmin);
+    uint8_t* flag = (uint8_t*)(pool + L.flag);
+    uint32_t* qlist = (uint32_t*)(pool + L.qlist);
+    uint32_t* nsel = (uint32_t*)(pool + L.nsel);
+    void* tmp = pool + L.tmp;
+    const size_t tbytes = pool_bytes - L.tmp;
+    const unsigned mmb = (unsigned)std::min<size_t>(kMinMaxBlocks, std::max<size_t>(1, (n + 255) / 256));
+    hipLaunchKernelGGL((minmax_kernel<D>), dim3(mmb), dim3(256), 0, st, V, n, part);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL((scale_kernel<D>), dim3(1), dim3(64), 0, st, part, (uint32_t)mmb, ls);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    hipLaunchKernelGGL((key_kernel<D>), dim3((n + 255) / 256), dim3(256), 0, st, V, n, ls, key0, id0);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    size_t tb = tbytes;
+    e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, key0, key1, id0, perm, (int)n, 0, D * bits_per_dim<D>(), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL((tile_kernel<D>), dim3(T), dim3(kTile), 0, st, V, perm, n, Vs, tbox, tmin);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t* ql = nullptr;
+    if (!(q_first == 0 && q_count == n)) {
+        hipLaunchKernelGGL(qflag_kernel, dim3((n + 255) / 256), dim3(256), 0, st, perm, n, q_first, q_first + q_count,
+                           flag);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        tb = tbytes;
+        e = hipcub::DeviceSelect::Flagged(tmp, tb, hipcub::CountingInputIterator<uint32_t>(0), flag, qlist, nsel,
+                                          (int)n, st);
+        if (e != hipSuccess) return e;
+        ql = qlist;  // exactly q_count entries: perm is a permutation of 0 .. n-1
+    }
+    const unsigned grid = (unsigned)((q_count + kQBlock - 1) / kQBlock);
+    hipLaunchKernelGGL((query_kernel<D, K>), dim3(grid), dim3(kQBlock), 0, st, Vs, perm, n, T, tbox, tmin, ql, q_first,
+                       q_count, k, r, kmax, nbr, dist, cnt);
+    return hipGetLastError();
+}
+
+template <int D>
+hipError_t run_dim(const float* V, uint32_t n, uint32_t qf, uint32_t qc, const uint32_t* k, const float* r,
+                   uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, char* pool, size_t pb, hipStream_t st)
+{
+    if (kmax <= 16) return run<D, 16>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, st);
+    if (kmax <= 32) return run<D, 32>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, st);
+    if (kmax <= 48) return run<D, 48>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, st);
+    return run<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, st);
+}
+
+}  // namespace knnidx
+}  // namespace vgpu
+
+extern "C" {
+
+// pool bytes the indexed query of n vertices / q_count queries needs (0: unsupported dim)
+size_t vgpu_knn_index_bytes(int dim, uint32_t n, uint32_t q_count)
+{
+    using namespace vgpu::knnidx;
+    Layout L;
+    hipError_t e = hipErrorInvalidValue;
+    switch (dim) {
+    case 6: e = layout<6>(n, q_count, L); break;
+    case 7: e = layout<7>(n, q_count, L); break;
+    case 8: e = layout<8>(n, q_count, L); break;
+    case 14: e = layout<14>(n, q_count, L); break;
+    default: return 0;
+    }
+    return e == hipSuccess ? L.total : 0;
+}
+
+// kmax <= 64, dim in {6, 7, 8, 14}, n >= 1, q_count >= 1 (checked by the caller)
+hipError_t vgpu_launch_knn_index(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
+                                 const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr, float* dist,
+                                 uint32_t* cnt, void* pool, size_t pool_bytes, hipStream_t st)
+{
+    using namespace vgpu::knnidx;
+    char* p = (char*)pool;
+    switch (dim) {
+    case 6: return run_dim<6>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, st);
+    case 7: return run_dim<7>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, st);
+    case 8: return run_dim<8>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, st);
+    case 14: return run_dim<14>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+}  // extern "C"

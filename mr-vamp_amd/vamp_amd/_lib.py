@@ -96,6 +96,7 @@ SIGNATURES = {
     "vgpu_sample_fkcc_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, C.c_uint64, C.c_size_t, F32P, U8P]),
     "vgpu_robot_info": (C.c_int, [C.c_int32, I32P, I32P, I32P]),
     "vgpu_prm_neighbor_params": (C.c_int, [C.c_int, C.c_double, C.c_double, C.c_size_t, U32P, F32P]),
+    "vgpu_set_knn_mode": (C.c_int, [VP, C.c_int]),
     "vgpu_roadmap_knn": (C.c_int, [VP, C.c_int, VP, C.c_size_t, VP, VP, C.c_uint32, VP, VP, VP]),
     "vgpu_roadmap_knn_range": (C.c_int, [VP, C.c_int, VP, C.c_size_t, C.c_size_t, C.c_size_t, VP, VP, C.c_uint32,
                                          VP, VP, VP]),

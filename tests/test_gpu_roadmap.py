@@ -18,37 +18,46 @@ def vamp():
     return vamp_amd
 
 
-def knn_gpu(vamp, V, sm, kmax=None):
+def knn_gpu(vamp, V, sm, kmax=None, mode=0, q_first=0, q_count=None):
+    """vgpu_roadmap_knn_range on the GPU with the context's kNN method set to `mode` (0 auto, 1 brute
+    force, 2 spatial index); rows are indexed from q_first"""
     import torch
     from vamp_amd import roadmap
     n, dim = V.shape
+    q_count = n - q_first if q_count is None else q_count
     k, r = roadmap.prm_neighbor_params(dim, sm, n)
     kmax = kmax or int(max(1, k.max()))
     dev = torch.device("cuda", 0)
     tV = torch.from_numpy(V).to(dev)
     tk = torch.from_numpy(k.view(np.int32)).to(dev)
     tr = torch.from_numpy(r).to(dev)
-    nbr = torch.zeros((n, kmax), dtype=torch.int32, device=dev)
-    dist = torch.zeros((n, kmax), dtype=torch.float32, device=dev)
-    cnt = torch.zeros(n, dtype=torch.int32, device=dev)
+    nbr = torch.zeros((max(q_count, 1), kmax), dtype=torch.int32, device=dev)
+    dist = torch.zeros((max(q_count, 1), kmax), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(max(q_count, 1), dtype=torch.int32, device=dev)
     ctx = vamp.context(0)
     ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
     from vamp_amd._lib import check, load
-    check(load().vgpu_roadmap_knn(ctx.h, dim, tV.data_ptr(), n, tk.data_ptr(), tr.data_ptr(), kmax,
-                                  nbr.data_ptr(), dist.data_ptr(), cnt.data_ptr()), ctx.h)
-    torch.cuda.synchronize()
+    check(load().vgpu_set_knn_mode(ctx.h, mode), ctx.h)
+    try:
+        check(load().vgpu_roadmap_knn_range(ctx.h, dim, tV.data_ptr(), n, q_first, q_count, tk.data_ptr(),
+                                            tr.data_ptr(), kmax, nbr.data_ptr(), dist.data_ptr(), cnt.data_ptr()),
+              ctx.h)
+        torch.cuda.synchronize()
+    finally:
+        load().vgpu_set_knn_mode(ctx.h, 0)
     return nbr.cpu().numpy().view(np.uint32), dist.cpu().numpy(), cnt.cpu().numpy().view(np.uint32)
 
 
+@pytest.mark.parametrize("mode", [1, 2], ids=["brute", "index"])
 @pytest.mark.parametrize("robot,dim,n", [("panda", 7, 20000), ("fetch", 8, 6000), ("ur5", 6, 3000),
                                          ("baxter", 14, 3000)])
-def test_knn_equals_oracle(vamp, oracle, robot, dim, n):
+def test_knn_equals_oracle(vamp, oracle, robot, dim, n, mode):
     rng = np.random.default_rng(21)
     V = oracle.robot_scale(robot, rng.random((n, dim), dtype=F))
     V[n // 2] = V[n // 3]  # duplicate vertex (distance 0)
     sm = oracle.SPACE_MEASURE[robot]
     onb, od, oc = oracle.roadmap_knn(V, sm)
-    gnb, gd, gc = knn_gpu(vamp, V, sm, onb.shape[1])
+    gnb, gd, gc = knn_gpu(vamp, V, sm, onb.shape[1], mode=mode)
     assert np.array_equal(gc, oc)
     mask = np.arange(onb.shape[1])[None, :] < oc[:, None]
     assert np.array_equal(gnb[mask], onb[mask]) and np.array_equal(gd[mask], od[mask])
@@ -106,3 +115,44 @@ def test_sharded_edges_single_process_equals_oracle(vamp, oracle):
     edges, _ = oracle.build_roadmap_edges("fetch", oenv, V)
     assert rm.edges == edges
     assert np.array_equal(rm.component, oracle.components(len(V), edges))
+
+
+def _same_lists(a, b):
+    (an, ad, ac), (bn, bd, bc) = a, b
+    assert np.array_equal(ac, bc)
+    mask = np.arange(an.shape[1])[None, :] < ac[:, None]
+    assert np.array_equal(an[mask], bn[mask]) and np.array_equal(ad[mask], bd[mask])
+
+
+def test_knn_index_halton_ties_and_ranges(vamp, oracle):
+    """Spatial index vs the oracle on Halton vertices (the PRM vertex sequence: regular spacing,
+    many near-equal distances) with exact duplicate clusters (distance-0 ties resolved by index),
+    a clump of identical points larger than a tile, and query sub-ranges (one rank's share)."""
+    dim, n = 8, 12000
+    V = oracle.robot_scale("fetch", oracle.halton(8, range(1, n + 1)).astype(F))
+    V[5000:5100] = V[4000]  # 100 copies of one vertex: one tile's box degenerates to a point
+    V[7001] = V[17]
+    sm = oracle.SPACE_MEASURE["fetch"]
+    want = oracle.roadmap_knn(V, sm)
+    kmax = want[0].shape[1]
+    _same_lists(knn_gpu(vamp, V, sm, kmax, mode=2), want)
+    for qf, qc in [(0, 1), (1, 5), (4990, 300), (n - 777, 777)]:
+        got = knn_gpu(vamp, V, sm, kmax, mode=2, q_first=qf, q_count=qc)
+        _same_lists(got, tuple(x[qf:qf + qc] for x in want))
+
+
+def test_knn_index_equals_brute_force_large(vamp, oracle):
+    """At 2e5 Fetch vertices (beyond the oracle's reach in a test) the indexed query equals the
+    GPU brute force, which equals the oracle at the smaller sizes above."""
+    import time
+    n = 200000
+    V = oracle.robot_scale("fetch", oracle.halton(8, range(1, n + 1)).astype(F))
+    sm = oracle.SPACE_MEASURE["fetch"]
+    t = time.perf_counter()
+    idx = knn_gpu(vamp, V, sm, mode=2)
+    t_idx = time.perf_counter() - t
+    t = time.perf_counter()
+    bf = knn_gpu(vamp, V, sm, mode=1)
+    t_bf = time.perf_counter() - t
+    print(f"knn 2e5 Fetch vertices: index {t_idx * 1e3:.1f} ms, brute force {t_bf * 1e3:.1f} ms (incl. transfers)")
+    _same_lists(idx, bf)
