@@ -43,19 +43,23 @@ hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, s
     int vgpu_##NAME##_staged_checks(void);                                                                           \
     uint64_t vgpu_##NAME##_staged_env_checks(void);                                                                  \
     int vgpu_##NAME##_staged_mask_bytes(void);                                                                       \
+    int vgpu_##NAME##_staged_class(int c);                                                                           \
+    size_t vgpu_##NAME##_staged_plan_bytes(void);                                                                    \
     uint32_t vgpu_##NAME##_staged_blocks(int kind, uint32_t n_groups);                                               \
     hipError_t vgpu_##NAME##_staged_bound(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by, \
-                                          float bz, void* mask, uint8_t* valid, uint32_t* counts, hipStream_t st);   \
+                                          float bz, void* mask, uint8_t* valid, hipStream_t st);                     \
     hipError_t vgpu_##NAME##_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \
                                           uint32_t* counts, hipStream_t st);                                         \
+    hipError_t vgpu_##NAME##_staged_plan(const uint32_t* offs, uint32_t nb, uint32_t W, uint64_t set, void* plan,    \
+                                         hipStream_t st);                                                            \
     hipError_t vgpu_##NAME##_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
-                                          const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \
-                                          const uint32_t* offs, const uint32_t* seg, uint32_t* items,                \
-                                          uint32_t n_items, hipStream_t st);                                         \
+                                          const void* mask, uint32_t n_groups, uint64_t set, const void* plan,       \
+                                          const uint8_t* valid, const uint32_t* offs, uint32_t* items,               \
+                                          hipStream_t st);                                                           \
     hipError_t vgpu_##NAME##_staged_children(int kind, const void* s0, const void* s1, const void* s2,               \
-                                             const void* s3, uint64_t first, const uint32_t* seg,                    \
+                                             const void* s3, uint64_t first, const void* plan, const uint32_t* ub,   \
                                              const uint32_t* items, const EnvView* env, float bx, float by,          \
                                              float bz, uint8_t* valid, hipStream_t st);
 VGPU_STAGED_DECL(panda)
@@ -228,7 +232,7 @@ struct vgpu_ctx {
     size_t st_q_cap = 0;
     uint32_t* st_cnt = nullptr;   // per-(check, block) counts, then their exclusive scan, + scan temp
     size_t st_cnt_cap = 0;
-    uint32_t* st_host = nullptr;  // pinned: the 33 segment boundaries of the scan
+    uint32_t* st_host = nullptr;  // pinned: the first round's segment boundaries of a staged pass
     uint32_t* st_items = nullptr;
     size_t st_items_cap = 0;
     // roadmap kNN chunk lists (vgpu_roadmap.hip)
@@ -342,9 +346,9 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->st_q) (void)hipFree(c->st_q);
     if (c->st_cnt) (void)hipFree(c->st_cnt);
     if (c->st_items) (void)hipFree(c->st_items);
+    if (c->st_host) (void)hipHostFree(c->st_host);
     if (c->knn_part) (void)hipFree(c->knn_part);
     if (c->knn_idx) (void)hipFree(c->knn_idx);
-    if (c->st_host) (void)hipHostFree(c->st_host);
     if (c->total_host) (void)hipHostFree(c->total_host);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -932,21 +936,25 @@ struct StagedOps {
     int (*checks)(void);
     uint64_t (*env_checks)(void);
     int (*mask_bytes)(void);
+    int (*child_class)(int);
+    size_t (*plan_bytes)(void);
     uint32_t (*blocks)(int, uint32_t);
     hipError_t (*bound)(int, const void*, const void*, const void*, const void*, uint64_t, uint32_t, const EnvView*,
-                        float, float, float, void*, uint8_t*, uint32_t*, hipStream_t);
+                        float, float, float, void*, uint8_t*, hipStream_t);
     hipError_t (*count)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
                         const uint8_t*, uint32_t*, hipStream_t);
+    hipError_t (*plan)(const uint32_t*, uint32_t, uint32_t, uint64_t, void*, hipStream_t);
     hipError_t (*queue)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
-                        const uint8_t*, const uint32_t*, const uint32_t*, uint32_t*, uint32_t, hipStream_t);
-    hipError_t (*children)(int, const void*, const void*, const void*, const void*, uint64_t, const uint32_t*,
-                           const uint32_t*, const EnvView*, float, float, float, uint8_t*, hipStream_t);
+                        const void*, const uint8_t*, const uint32_t*, uint32_t*, hipStream_t);
+    hipError_t (*children)(int, const void*, const void*, const void*, const void*, uint64_t, const void*,
+                           const uint32_t*, const uint32_t*, const EnvView*, float, float, float, uint8_t*, hipStream_t);
 };
 #define VGPU_STAGED_OPS(NAME)                                                                                        \
     StagedOps                                                                                                        \
     {                                                                                                                \
         vgpu_##NAME##_staged_checks, vgpu_##NAME##_staged_env_checks, vgpu_##NAME##_staged_mask_bytes,               \
-            vgpu_##NAME##_staged_blocks, vgpu_##NAME##_staged_bound, vgpu_##NAME##_staged_count,                     \
+            vgpu_##NAME##_staged_class, vgpu_##NAME##_staged_plan_bytes, vgpu_##NAME##_staged_blocks,                \
+            vgpu_##NAME##_staged_bound, vgpu_##NAME##_staged_count, vgpu_##NAME##_staged_plan,                       \
             vgpu_##NAME##_staged_queue, vgpu_##NAME##_staged_children                                                \
     }
 static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda);
@@ -964,6 +972,12 @@ static const RobotOps* generic_ops(int32_t kind)
 }
 static const StagedOps* generic_staged(int32_t kind) { return kind == VGPU_ROBOT_UR5 ? &kUr5Staged : nullptr; }
 
+// One staged pass (vgpu_staged.hh) over n groups:
+//   bound -> count(all checks) -> scan -> [read back the per-check counts: the pass's ONE sync]
+//   -> per round: (count -> scan, later rounds) -> plan -> queue -> children per class.
+// The first round's per-check counts bound every later round's (groups only ever become invalid),
+// so they size all item buffers and children grids; the exact per-round layout is computed on the
+// device (plan_kernel) and read there by queue and children.
 static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* s0, const void* s1, const void* s2,
                        const void* s3, uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid)
 {
@@ -975,46 +989,27 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
     const size_t cells = (size_t)checks * nb;
     const size_t scan_bytes = vgpu_validate_scan_bytes(cells);
     const size_t cells_al = (cells + 1 + 63) & ~(size_t)63;
+    const size_t plan_words = ((ops.plan_bytes() + 3) / 4 + 63) & ~(size_t)63;  // keeps tmp 256-B aligned
     int rc;
     if ((rc = grow(c, &c->st_mask, &c->st_mask_cap, n * (size_t)ops.mask_bytes() / 4))) return rc;
-    if ((rc = grow(c, &c->st_cnt, &c->st_cnt_cap, 2 * cells_al + scan_bytes / 4 + 64))) return rc;
+    if ((rc = grow(c, &c->st_cnt, &c->st_cnt_cap, 2 * cells_al + scan_bytes / 4 + 64 + plan_words))) return rc;
     if (!c->st_host) HIPCHK(c, hipHostMalloc((void**)&c->st_host, 128 * sizeof(uint32_t), hipHostMallocDefault));
     uint32_t* counts = c->st_cnt;
     uint32_t* offs = c->st_cnt + cells_al;
-    void* tmp = c->st_cnt + 2 * cells_al;
+    void* plan = c->st_cnt + 2 * cells_al;
+    void* tmp = c->st_cnt + 2 * cells_al + plan_words;
     HIPCHK(c, hipMemsetAsync(counts + cells, 0, sizeof(uint32_t), c->cur));
-    HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, b[0], b[1], b[2], c->st_mask, valid, counts,
-                        c->cur));
+    HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, b[0], b[1], b[2], c->st_mask, valid, c->cur));
     const uint64_t all = checks >= 64 ? ~0ull : ((1ull << checks) - 1ull);
     const uint64_t env_bits = ops.env_checks();
-    // counts of every check's fired groups (all groups are valid at this point)
-    auto count_round = [&](uint64_t set, uint32_t fired[64], bool have_counts) -> int {
-        if (!have_counts)
-            HIPCHK(c, ops.count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, counts, c->cur));
-        HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
-        // segment boundaries offs[k * nb], k = 0..checks (the last one is the total)
-        HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t),
-                                   checks + 1, hipMemcpyDeviceToHost, c->cur));
-        HIPCHK(c, hipStreamSynchronize(c->cur));
-        for (int k = 0; k < checks; ++k) fired[k] = c->st_host[k + 1] - c->st_host[k];
-        return VGPU_OK;
-    };
-    // queue + children for the checks of `set`, with `fired` counted under the current flags
-    auto run_round = [&](uint64_t set, const uint32_t fired[64]) -> int {
-        uint32_t seg[65];
-        seg[0] = 0;
-        for (int k = 0; k < checks; ++k) seg[k + 1] = seg[k] + (((set >> k) & 1u) ? (fired[k] + W - 1) / W * W : 0u);
-        const size_t total = seg[checks];
-        if (total == 0) return VGPU_OK;
-        int r = grow(c, &c->st_items, &c->st_items_cap, total);
-        if (r) return r;
-        HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, offs, seg, c->st_items,
-                            (uint32_t)total, c->cur));
-        HIPCHK(c, ops.children(kind, s0, s1, s2, s3, first, seg, c->st_items, v, b[0], b[1], b[2], valid, c->cur));
-        return VGPU_OK;
-    };
+    // every check's fired groups (all groups valid here): segment boundaries offs[k * nb], k = 0..checks
+    HIPCHK(c, ops.count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, all, valid, counts, c->cur));
+    HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
+    HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t), checks + 1,
+                               hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
     uint32_t fired[64];
-    if ((rc = count_round(all, fired, true))) return rc;  // the bound kernel counted every check
+    for (int k = 0; k < checks; ++k) fired[k] = c->st_host[k + 1] - c->st_host[k];
     std::vector<uint64_t> rounds(c->rounds.begin(), c->rounds.end());
     if (rounds.empty()) {
         // Rounds from this batch's bounding statistics: (1) the first three environment checks
@@ -1029,13 +1024,25 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
             if (!((env_bits >> k) & 1u) && fired[k] >= n - n / 100) r3 |= 1ull << k;
         rounds = {r1, all & ~r1 & ~r3, r3};
     }
-    bool counted = true;  // `fired` is valid for the first round (no group invalidated yet)
+    size_t items_ub = 0;  // items of any round at most
+    for (int k = 0; k < checks; ++k) items_ub += (fired[k] + W - 1) / W * W;
+    if (items_ub >= ((size_t)1 << 32)) return fail(c, VGPU_ERR_INVALID_ARG, "staged pass: more than 2^32 items");
+    if ((rc = grow(c, &c->st_items, &c->st_items_cap, items_ub + 1))) return rc;
+    bool first_round = true;  // its counts are the ones read back
     for (uint64_t set : rounds) {
         set &= all;
-        if (!set) continue;
-        if (!counted && (rc = count_round(set, fired, false))) return rc;
-        counted = false;
-        if ((rc = run_round(set, fired))) return rc;
+        uint32_t ub[4] = {0, 0, 0, 0};  // per children class, from the first round's counts
+        for (int k = 0; k < checks; ++k)
+            if ((set >> k) & 1u) ub[ops.child_class(k)] += (fired[k] + W - 1) / W * W;
+        if (!(ub[0] | ub[1] | ub[2] | ub[3])) continue;
+        if (!first_round) {
+            HIPCHK(c, ops.count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, counts, c->cur));
+            HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
+        }
+        first_round = false;
+        HIPCHK(c, ops.plan(offs, (uint32_t)nb, W, set, plan, c->cur));
+        HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, plan, valid, offs, c->st_items, c->cur));
+        HIPCHK(c, ops.children(kind, s0, s1, s2, s3, first, plan, ub, c->st_items, v, b[0], b[1], b[2], valid, c->cur));
     }
     return VGPU_OK;
 }

@@ -34,11 +34,39 @@
 namespace vgpu {
 
 constexpr int kStagedBlock = 256;
-constexpr uint32_t kNoItem = 0xFFFFFFFFu;
 
+// The device-side segment layout of one round of a staged pass (written by plan_kernel after the
+// round's count + scan): each check's item segment [start, end) (wave-aligned; items [fill, end)
+// are padding), laid out class-major so each children class covers one contiguous range [lo, hi).
+// The host reads only the FIRST round's per-check counts back (one sync per pass): they bound
+// every later round's counts, which sizes every children grid without another read-back.
+constexpr int kPlanMaxChecks = 64;
+constexpr int kPlanMaxClasses = 4;
+struct StagedPlan {
+    uint32_t start[kPlanMaxChecks], end[kPlanMaxChecks], fill[kPlanMaxChecks];
+    uint32_t lo[kPlanMaxClasses], hi[kPlanMaxClasses];
+    uint32_t total;
+};
+
+// Children register classes.  A children kernel's VGPR budget is the maximum over the checks it can
+// run, so one kernel over every check spills for all of them (Panda: 105 VGPRs for check 21 against
+// a 72-VGPR budget at 7 waves/EU, 224 B/lane of scratch).  A robot may split its checks into
+// classes (R::kClasses, R::kClassOf[c], R::kClassWaves[k]): one children kernel per class, each
+// with its own occupancy.  Without them every check is class 0 at R::kChildWavesPerEU.
+template <class R, class = void>
+struct ChildClasses {
+    static constexpr int n = 1;
+    static constexpr bool split = false;
+    __host__ __device__ static constexpr int of(int) { return 0; }
+    __host__ __device__ static constexpr int waves(int) { return R::kChildWavesPerEU; }
+};
 template <class R>
-struct SegTableT {
-    uint32_t start[R::kChecks + 1];  // check c owns items [start[c], start[c+1]), wave-aligned
+struct ChildClasses<R, std::void_t<decltype(R::kClassOf)>> {
+    static_assert(R::kClasses <= kPlanMaxClasses, "too many children classes");
+    static constexpr int n = R::kClasses;
+    static constexpr bool split = true;
+    __host__ __device__ static constexpr int of(int c) { return R::kClassOf[c]; }
+    __host__ __device__ static constexpr int waves(int k) { return R::kClassWaves[k]; }
 };
 
 // ---- group sources ----------------------------------------------------------------------------
@@ -47,13 +75,13 @@ struct SrcConfigsT {  // fkcc: one configuration per group
     static constexpr int G = 1;
     static constexpr bool kInit = true;
     const float* q;
-    __device__ void load(uint32_t g, int, float v[R::D]) const
+    __device__ __forceinline__ void load(uint32_t g, int, float v[R::D]) const
     {
         const float* p = q + R::D * (size_t)g;
 #pragma unroll
         for (int j = 0; j < R::D; ++j) v[j] = p[j];
     }
-    __device__ uint32_t out(uint32_t g) const { return g; }
+    __device__ __forceinline__ uint32_t out(uint32_t g) const { return g; }
 };
 
 template <class R>
@@ -63,7 +91,7 @@ struct SrcSamplesT {  // Halton draw first + g, scaled
     uint64_t first;
     float* q_out;       // bound stage: copy of the sample (optional)
     const float* q_in;  // children stage: the bound stage's copy (else the draw is recomputed)
-    __device__ void load(uint32_t g, int, float v[R::D]) const
+    __device__ __forceinline__ void load(uint32_t g, int, float v[R::D]) const
     {
         if (q_in) {
             const float* p = q_in + R::D * (size_t)g;
@@ -73,7 +101,7 @@ struct SrcSamplesT {  // Halton draw first + g, scaled
             R::sample(first + g, v);
         }
     }
-    __device__ uint32_t out(uint32_t g) const { return g; }
+    __device__ __forceinline__ uint32_t out(uint32_t g) const { return g; }
 };
 
 template <class R>
@@ -82,11 +110,11 @@ struct SrcHeadT {  // validate head: block 0 of edge g
     static constexpr bool kInit = true;
     const float* starts;
     const float* goals;
-    __device__ void load(uint32_t g, int lane, float v[R::D]) const
+    __device__ __forceinline__ void load(uint32_t g, int lane, float v[R::D]) const
     {
         R::head(starts + R::D * (size_t)g, goals + R::D * (size_t)g, lane, v);
     }
-    __device__ uint32_t out(uint32_t g) const { return g; }
+    __device__ __forceinline__ uint32_t out(uint32_t g) const { return g; }
 };
 
 template <class R>
@@ -97,13 +125,13 @@ struct SrcTailT {  // validate tail: item g = (edge, back-step k), result into t
     const float* goals;
     const uint32_t* item_edge;
     const uint32_t* off;
-    __device__ void load(uint32_t g, int lane, float v[R::D]) const
+    __device__ __forceinline__ void load(uint32_t g, int lane, float v[R::D]) const
     {
         const uint32_t e = item_edge[g];
         const int k = (int)(g - off[e]) + 1;
         R::tail(starts + R::D * (size_t)e, goals + R::D * (size_t)e, lane, k, v);
     }
-    __device__ uint32_t out(uint32_t g) const { return item_edge[g]; }
+    __device__ __forceinline__ uint32_t out(uint32_t g) const { return item_edge[g]; }
 };
 
 template <class R>
@@ -114,14 +142,14 @@ struct SrcTailMaskT {  // full-mask mode: item g = (edge, back-step k), result i
     const float* goals;
     const uint32_t* item_edge;
     const uint32_t* off;
-    __device__ void load(uint32_t g, int lane, float v[R::D]) const
+    __device__ __forceinline__ void load(uint32_t g, int lane, float v[R::D]) const
     {
         const uint32_t e = item_edge[g];
         const int k = (int)(g - off[e]) + 1;
         R::tail(starts + R::D * (size_t)e, goals + R::D * (size_t)e, lane, k, v);
     }
     // block k of edge e sits at off[e] + e + k (edges laid out block 0 .. n_e - 1 in edge order)
-    __device__ uint32_t out(uint32_t g) const { return g + item_edge[g] + 1u; }
+    __device__ __forceinline__ uint32_t out(uint32_t g) const { return g + item_edge[g] + 1u; }
 };
 
 template <int G>
@@ -184,48 +212,41 @@ template <class R, class Src, bool EXT>
 __global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
                                                                              float bx, float by, float bz,
                                                                              typename R::Mask* __restrict__ mask,
-                                                                             uint8_t* __restrict__ valid,
-                                                                             uint32_t* __restrict__ counts)
+                                                                             uint8_t* __restrict__ valid)
 {
     using Grp = typename GrpOf<Src::G>::T;
-    using M = typename R::Mask;
     if constexpr (EXT) capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
     const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
     const uint32_t g = (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);
-    M m = 0u;
-    if (g < n_groups) {  // group-uniform
-        float v[R::D];
-        src.load(g, lane, v);
-        if constexpr (std::is_same<Src, SrcSamplesT<R>>::value) {
-            if (src.q_out) {
+    if (g >= n_groups) return;  // group-uniform
+    float v[R::D];
+    src.load(g, lane, v);
+    if constexpr (std::is_same<Src, SrcSamplesT<R>>::value) {
+        if (src.q_out) {
 #pragma unroll
-                for (int j = 0; j < R::D; ++j) src.q_out[R::D * (size_t)g + j] = v[j];
-            }
-        }
-        m = R::template bound<Grp, EXT>(v, env, bx, by, bz);
-        if (lane == 0) {
-            mask[g] = m;
-            if constexpr (Src::kInit) valid[src.out(g)] = 1;
+            for (int j = 0; j < R::D; ++j) src.q_out[R::D * (size_t)g + j] = v[j];
         }
     }
-    // the first round's per-(check, block) counts: every group is still valid here (tail items
-    // exist only for edges that passed the head)
-    if (lane != 0) m = 0u;
-    block_counts<R>(m, counts);
+    const typename R::Mask m = R::template bound<Grp, EXT>(v, env, bx, by, bz);
+    if (lane == 0) {
+        mask[g] = m;
+        if constexpr (Src::kInit) valid[src.out(g)] = 1;
+    }
 }
 
 // ---- rounds: the fired (group, check) pairs of a set of checks, for groups still valid ----------
 // Checks run in rounds (e.g. the environment checks, then the self checks): a group invalidated by
 // an earlier round contributes no work to later ones, which recovers the reference's early exit.
-// Both kernels use the bound kernel's grid; per-(check, block) counts are stored check-major,
+// count and queue run one thread per GROUP (not per lane: they only read the group's mask and
+// flag), kStagedBlock groups per block; per-(check, block) counts are stored check-major,
 // counts[c * blocks + block], for one flat exclusive scan.
 template <class R, class Src>
 __device__ __forceinline__ typename R::Mask round_bits(const Src& src, const typename R::Mask* __restrict__ mask,
                                                        uint32_t n_groups, typename R::Mask set,
-                                                       const uint8_t* __restrict__ valid, uint32_t g, bool lead)
+                                                       const uint8_t* __restrict__ valid, uint32_t g)
 {
-    if (!lead || g >= n_groups) return 0u;
+    if (g >= n_groups) return 0u;
     const typename R::Mask m = mask[g] & set;
     return (m && valid[src.out(g)]) ? m : (typename R::Mask)0u;
 }
@@ -236,26 +257,52 @@ __global__ __launch_bounds__(kStagedBlock) void count_kernel(Src src, const type
                                                              const uint8_t* __restrict__ valid,
                                                              uint32_t* __restrict__ counts)
 {
-    const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
-    const uint32_t g = (uint32_t)(tid / Src::G);
-    const typename R::Mask m = round_bits<R>(src, mask, n_groups, set, valid, g, (tid % Src::G) == 0);
-    block_counts<R>(m, counts);
+    const uint32_t g = blockIdx.x * kStagedBlock + threadIdx.x;
+    block_counts<R>(round_bits<R>(src, mask, n_groups, set, valid, g), counts);
+}
+
+// After a round's count + scan: fired[c] = offs[(c+1)*nb] - offs[c*nb]; the round's segments,
+// class-major.  One lane per check computes its fired count, lane 0 lays them out.
+template <class R>
+__global__ __launch_bounds__(64) void plan_kernel(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t W,
+                                                  uint64_t set, StagedPlan* __restrict__ plan)
+{
+    using CC = ChildClasses<R>;
+    __shared__ uint32_t fired[R::kChecks];
+    for (int k = threadIdx.x; k < R::kChecks; k += 64)
+        fired[k] = offs[(size_t)(k + 1) * nb] - offs[(size_t)k * nb];
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    uint32_t total = 0;
+    for (int cls = 0; cls < CC::n; ++cls) {
+        plan->lo[cls] = total;
+        for (int k = 0; k < R::kChecks; ++k) {
+            if (CC::of(k) != cls) continue;
+            const bool on = (set >> k) & 1u;
+            plan->start[k] = total;
+            plan->fill[k] = total + (on ? fired[k] : 0u);
+            if (on) total += (fired[k] + W - 1) / W * W;
+            plan->end[k] = total;
+        }
+        plan->hi[cls] = total;
+    }
+    plan->total = total;
 }
 
 // Position of group g in check c's segment:
-//   seg.start[c] + (offs[c*nb + block] - offs[c*nb]) + rank of g among the block's groups with bit c
+//   start[c] + (offs[c*nb + block] - offs[c*nb]) + rank of g among the block's groups with bit c
 // -- ascending group order within each segment, no atomics.
 template <class R, class Src>
 __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const typename R::Mask* __restrict__ mask,
                                                              uint32_t n_groups, typename R::Mask set,
+                                                             const StagedPlan* __restrict__ plan,
                                                              const uint8_t* __restrict__ valid,
-                                                             const uint32_t* __restrict__ offs, SegTableT<R> seg,
+                                                             const uint32_t* __restrict__ offs,
                                                              uint32_t* __restrict__ items)
 {
     using M = typename R::Mask;
-    const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
-    const uint32_t g = (uint32_t)(tid / Src::G);
-    const M m = round_bits<R>(src, mask, n_groups, set, valid, g, (tid % Src::G) == 0);
+    const uint32_t g = blockIdx.x * kStagedBlock + threadIdx.x;
+    const M m = round_bits<R>(src, mask, n_groups, set, valid, g);
     const int w = threadIdx.x >> 6;
     __shared__ uint32_t wcnt[kStagedBlock / 64][R::kChecks];
     for (int i = threadIdx.x; i < (kStagedBlock / 64) * R::kChecks; i += kStagedBlock) (&wcnt[0][0])[i] = 0u;
@@ -272,34 +319,64 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
     for (M a = any; a; a &= a - 1) {
         const int c = mask_ctz(a);
         const uint64_t b = __builtin_amdgcn_ballot_w64((m >> c) & 1u);
-        uint32_t base = seg.start[c] + (offs[(size_t)c * nb + blockIdx.x] - offs[(size_t)c * nb]);
+        uint32_t base = plan->start[c] + (offs[(size_t)c * nb + blockIdx.x] - offs[(size_t)c * nb]);
         for (int i = 0; i < w; ++i) base += wcnt[i][c];
         if ((m >> c) & 1u) items[base + (uint32_t)__builtin_popcountll(b & below)] = g;
     }
 }
 
 // ---- stage 2: children, one check per wave ------------------------------------------------------
-template <class R, class Src, bool EXT>
-__global__ __launch_bounds__(kStagedBlock, R::kChildWavesPerEU) void children_kernel(Src src, SegTableT<R> seg,
-                                                                                const uint32_t* __restrict__ items,
-                                                                                EnvView env, float bx, float by,
-                                                                                float bz, uint8_t* __restrict__ valid)
+// A class's kernel covers the class's item range [lo, hi) of the plan; its grid is sized by the
+// host from an upper bound (the first round's counts), so waves past hi exit at once.  The check of
+// a wave is found by scanning the class's checks (compile-time list, scalar compares against the
+// plan); the generated switch folds to that one case, so the kernel's registers cover only its class.
+template <class R, int K, class Grp, bool EXT, int C = 0>
+__device__ __forceinline__ int children_of_class(uint32_t item0, const StagedPlan* __restrict__ plan, const float* v,
+                                                 const EnvView& env, float bx, float by, float bz)
+{
+    if constexpr (C == R::kChecks) {
+        return -1;
+    } else {
+        if constexpr (ChildClasses<R>::of(C) == K) {
+            if (item0 >= plan->start[C] && item0 < plan->end[C])
+                return R::template children<Grp, EXT>(C, v, env, bx, by, bz) ? 1 : 0;
+        }
+        return children_of_class<R, K, Grp, EXT, C + 1>(item0, plan, v, env, bx, by, bz);
+    }
+}
+
+template <class R, class Src, bool EXT, int K>
+__global__ __launch_bounds__(kStagedBlock, ChildClasses<R>::waves(K)) void children_kernel(
+    Src src, const StagedPlan* __restrict__ plan, const uint32_t* __restrict__ items, EnvView env, float bx, float by,
+    float bz, uint8_t* __restrict__ valid)
 {
     using Grp = typename GrpOf<Src::G>::T;
     if constexpr (EXT) capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
     const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
-    const uint32_t item = (uint32_t)(tid / Src::G);
+    const uint32_t item = plan->lo[K] + (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);
-    if (item >= seg.start[R::kChecks]) return;  // wave-uniform (segments are wave-aligned)
+    if (item >= plan->hi[K]) return;  // wave-uniform (segments are wave-aligned)
     const uint32_t item0 = __builtin_amdgcn_readfirstlane(item);
     int c = 0;
-    while (item0 >= seg.start[c + 1]) ++c;  // scalar: every wave holds one check
+    uint32_t fill = 0;
+    if constexpr (!ChildClasses<R>::split) {
+        while (!(item0 >= plan->start[c] && item0 < plan->end[c])) ++c;  // scalar: every wave holds one check
+        fill = plan->fill[c];
+    } else {
+#pragma unroll
+        for (int k = 0; k < R::kChecks; ++k)
+            if (ChildClasses<R>::of(k) == K && item0 >= plan->start[k] && item0 < plan->end[k]) fill = plan->fill[k];
+    }
+    if (item >= fill) return;  // segment padding (group-uniform)
     const uint32_t g = items[item];
-    if (g == kNoItem) return;  // segment padding (group-uniform)
     float v[R::D];
     src.load(g, lane, v);
-    if (R::template children<Grp, EXT>(c, v, env, bx, by, bz) && lane == 0)
-        valid[src.out(g)] = 0;  // every writer stores 0: the race is benign
+    bool hit;
+    if constexpr (ChildClasses<R>::split)
+        hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bx, by, bz) > 0;
+    else
+        hit = R::template children<Grp, EXT>(c, v, env, bx, by, bz);
+    if (hit && lane == 0) valid[src.out(g)] = 0;  // every writer stores 0: the race is benign
 }
 
 // ---- host-side launch helpers ------------------------------------------------------------------
@@ -313,18 +390,20 @@ struct StagedHost {
         return (unsigned)(((size_t)n_groups * Src::G + kStagedBlock - 1) / kStagedBlock);
     }
 
+    static unsigned group_blocks(uint32_t n_groups) { return (n_groups + kStagedBlock - 1) / kStagedBlock; }
+
     template <class Src>
     static hipError_t bound(const Src& src, uint32_t n_groups, const EnvView* env, float bx, float by, float bz,
-                            M* mask, uint8_t* valid, uint32_t* counts, hipStream_t st)
+                            M* mask, uint8_t* valid, hipStream_t st)
     {
         if (n_groups == 0) return hipSuccess;
         const unsigned grid = grid_of<Src>(n_groups);
         if (env->n_hf > 0 || env->n_pc > 0)
             hipLaunchKernelGGL((bound_kernel<R, Src, true>), dim3(grid), dim3(kStagedBlock), 0, st, src, n_groups,
-                               *env, bx, by, bz, mask, valid, counts);
+                               *env, bx, by, bz, mask, valid);
         else
             hipLaunchKernelGGL((bound_kernel<R, Src, false>), dim3(grid), dim3(kStagedBlock), 0, st, src, n_groups,
-                               *env, bx, by, bz, mask, valid, counts);
+                               *env, bx, by, bz, mask, valid);
         return hipGetLastError();
     }
 
@@ -332,40 +411,53 @@ struct StagedHost {
     static hipError_t count(const Src& src, const M* mask, uint32_t n_groups, M set, const uint8_t* valid,
                             uint32_t* counts, hipStream_t st)
     {
-        hipLaunchKernelGGL((count_kernel<R, Src>), dim3(grid_of<Src>(n_groups)), dim3(kStagedBlock), 0, st, src, mask,
+        hipLaunchKernelGGL((count_kernel<R, Src>), dim3(group_blocks(n_groups)), dim3(kStagedBlock), 0, st, src, mask,
                            n_groups, set, valid, counts);
         return hipGetLastError();
     }
 
     template <class Src>
-    static hipError_t queue(const Src& src, const M* mask, uint32_t n_groups, M set, const uint8_t* valid,
-                            const uint32_t* offs, const uint32_t* seg, uint32_t* items, uint32_t n_items,
-                            hipStream_t st)
+    static hipError_t queue(const Src& src, const M* mask, uint32_t n_groups, M set, const StagedPlan* plan,
+                            const uint8_t* valid, const uint32_t* offs, uint32_t* items, hipStream_t st)
     {
-        hipError_t err = hipMemsetAsync(items, 0xFF, (size_t)n_items * sizeof(uint32_t), st);
-        if (err != hipSuccess) return err;
-        SegTableT<R> t;
-        for (int c = 0; c <= R::kChecks; ++c) t.start[c] = seg[c];
-        hipLaunchKernelGGL((queue_kernel<R, Src>), dim3(grid_of<Src>(n_groups)), dim3(kStagedBlock), 0, st, src, mask,
-                           n_groups, set, valid, offs, t, items);
+        hipLaunchKernelGGL((queue_kernel<R, Src>), dim3(group_blocks(n_groups)), dim3(kStagedBlock), 0, st, src, mask,
+                           n_groups, set, plan, valid, offs, items);
         return hipGetLastError();
     }
 
-    template <class Src>
-    static hipError_t children(const Src& src, const uint32_t* seg, const uint32_t* items, const EnvView* env,
-                               float bx, float by, float bz, uint8_t* valid, hipStream_t st)
+    // one launch per class with items; ub[k] = upper bound of class k's item count this round
+    template <class Src, bool EXT, int K = 0>
+    static hipError_t children_classes(const Src& src, const StagedPlan* plan, const uint32_t* ub,
+                                       const uint32_t* items, const EnvView* env, float bx, float by, float bz,
+                                       uint8_t* valid, hipStream_t st)
     {
-        SegTableT<R> t;
-        for (int c = 0; c <= R::kChecks; ++c) t.start[c] = seg[c];
-        const size_t threads = (size_t)t.start[R::kChecks] * Src::G;
-        if (threads == 0) return hipSuccess;
-        const unsigned grid = (unsigned)((threads + kStagedBlock - 1) / kStagedBlock);
+        if constexpr (K == ChildClasses<R>::n) {
+            return hipSuccess;
+        } else {
+            const size_t threads = (size_t)ub[K] * Src::G;
+            if (threads > 0) {
+                const unsigned grid = (unsigned)((threads + kStagedBlock - 1) / kStagedBlock);
+                hipLaunchKernelGGL((children_kernel<R, Src, EXT, K>), dim3(grid), dim3(kStagedBlock), 0, st, src,
+                                   plan, items, *env, bx, by, bz, valid);
+                const hipError_t err = hipGetLastError();
+                if (err != hipSuccess) return err;
+            }
+            return children_classes<Src, EXT, K + 1>(src, plan, ub, items, env, bx, by, bz, valid, st);
+        }
+    }
+
+    template <class Src>
+    static hipError_t children(const Src& src, const StagedPlan* plan, const uint32_t* ub, const uint32_t* items,
+                               const EnvView* env, float bx, float by, float bz, uint8_t* valid, hipStream_t st)
+    {
         if (env->n_hf > 0 || env->n_pc > 0)
-            hipLaunchKernelGGL((children_kernel<R, Src, true>), dim3(grid), dim3(kStagedBlock), 0, st, src, t, items,
-                               *env, bx, by, bz, valid);
-        else
-            hipLaunchKernelGGL((children_kernel<R, Src, false>), dim3(grid), dim3(kStagedBlock), 0, st, src, t, items,
-                               *env, bx, by, bz, valid);
+            return children_classes<Src, true>(src, plan, ub, items, env, bx, by, bz, valid, st);
+        return children_classes<Src, false>(src, plan, ub, items, env, bx, by, bz, valid, st);
+    }
+
+    static hipError_t plan(const uint32_t* offs, uint32_t nb, uint32_t W, M set, StagedPlan* plan, hipStream_t st)
+    {
+        hipLaunchKernelGGL((plan_kernel<R>), dim3(1), dim3(64), 0, st, offs, nb, W, (uint64_t)set, plan);
         return hipGetLastError();
     }
 
@@ -400,18 +492,19 @@ struct StagedHost {
     int vgpu_##NAME##_staged_checks(void) { return R::kChecks; }                                                     \
     uint64_t vgpu_##NAME##_staged_env_checks(void) { return (uint64_t)R::kEnvChecks; }                             \
     int vgpu_##NAME##_staged_mask_bytes(void) { return (int)sizeof(typename R::Mask); }                              \
-    uint32_t vgpu_##NAME##_staged_blocks(int kind, uint32_t n_groups)                                                \
+    int vgpu_##NAME##_staged_class(int c) { return vgpu::ChildClasses<R>::of(c); }                                   \
+    size_t vgpu_##NAME##_staged_plan_bytes(void) { return sizeof(vgpu::StagedPlan); }                               \
+    uint32_t vgpu_##NAME##_staged_blocks(int, uint32_t n_groups)                                                     \
     {                                                                                                                \
-        const size_t G = kind >= 2 ? 8 : 1;                                                                          \
-        return (uint32_t)(((size_t)n_groups * G + vgpu::kStagedBlock - 1) / vgpu::kStagedBlock);                     \
+        return vgpu::StagedHost<R>::group_blocks(n_groups); /* count / queue grid: one thread per group */          \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_bound(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by, \
-                                          float bz, void* mask, uint8_t* valid, uint32_t* counts, hipStream_t st)    \
+                                          float bz, void* mask, uint8_t* valid, hipStream_t st)                      \
     {                                                                                                                \
         using H = vgpu::StagedHost<R>;                                                                               \
         return H::with_source(kind, s0, s1, s2, s3, first, [&](auto src) {                                          \
-            return H::bound(src, n_groups, env, bx, by, bz, (typename R::Mask*)mask, valid, counts, st);             \
+            return H::bound(src, n_groups, env, bx, by, bz, (typename R::Mask*)mask, valid, st);                     \
         });                                                                                                          \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
@@ -424,20 +517,25 @@ struct StagedHost {
             return H::count(src, (const typename R::Mask*)mask, n_groups, (typename R::Mask)set, valid, counts, st); \
         });                                                                                                          \
     }                                                                                                                \
+    hipError_t vgpu_##NAME##_staged_plan(const uint32_t* offs, uint32_t nb, uint32_t W, uint64_t set, void* plan,    \
+                                         hipStream_t st)                                                             \
+    {                                                                                                                \
+        return vgpu::StagedHost<R>::plan(offs, nb, W, (typename R::Mask)set, (vgpu::StagedPlan*)plan, st);           \
+    }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
-                                          const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \
-                                          const uint32_t* offs, const uint32_t* seg, uint32_t* items,                \
-                                          uint32_t n_items, hipStream_t st)                                          \
+                                          const void* mask, uint32_t n_groups, uint64_t set, const void* plan,       \
+                                          const uint8_t* valid, const uint32_t* offs, uint32_t* items,               \
+                                          hipStream_t st)                                                            \
     {                                                                                                                \
         using H = vgpu::StagedHost<R>;                                                                               \
         if (n_groups == 0) return hipSuccess;                                                                        \
         return H::with_source(kind, s0, s1, s2, s3, 0, [&](auto src) {                                              \
-            return H::queue(src, (const typename R::Mask*)mask, n_groups, (typename R::Mask)set, valid, offs, seg,   \
-                            items, n_items, st);                                                                     \
+            return H::queue(src, (const typename R::Mask*)mask, n_groups, (typename R::Mask)set,                     \
+                            (const vgpu::StagedPlan*)plan, valid, offs, items, st);                                  \
         });                                                                                                          \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_children(int kind, const void* s0, const void* s1, const void* s2,               \
-                                             const void* s3, uint64_t first, const uint32_t* seg,                    \
+                                             const void* s3, uint64_t first, const void* plan, const uint32_t* ub,   \
                                              const uint32_t* items, const EnvView* env, float bx, float by,          \
                                              float bz, uint8_t* valid, hipStream_t st)                               \
     {                                                                                                                \
@@ -447,7 +545,7 @@ struct StagedHost {
                 src.q_in = src.q_out; /* the samples the bound stage wrote */                                         \
                 src.q_out = nullptr;                                                                                 \
             }                                                                                                        \
-            return H::children(src, seg, items, env, bx, by, bz, valid, st);                                         \
+            return H::children(src, (const vgpu::StagedPlan*)plan, ub, items, env, bx, by, bz, valid, st);           \
         });                                                                                                          \
     }                                                                                                                \
     }

@@ -4,12 +4,25 @@
 #include "vgpu_panda.hh"
 #include "vgpu_staged.hh"
 
+#ifndef VGPU_BOUND_WAVES_PER_EU
+#define VGPU_BOUND_WAVES_PER_EU VGPU_WAVES_PER_EU
+#endif
+#ifndef VGPU_PANDA_CLASS0_WAVES
+#define VGPU_PANDA_CLASS0_WAVES 7
+#endif
+#ifndef VGPU_PANDA_CLASS1_WAVES
+#define VGPU_PANDA_CLASS1_WAVES 7
+#endif
+#ifndef VGPU_PANDA_CLASS2_WAVES
+#define VGPU_PANDA_CLASS2_WAVES 4
+#endif
+
 namespace vgpu {
 
 struct PandaR {
     static constexpr int D = 7;
     static constexpr int kChecks = panda_n_checks;
-    static constexpr int kWavesPerEU = VGPU_WAVES_PER_EU;
+    static constexpr int kWavesPerEU = VGPU_BOUND_WAVES_PER_EU;  // the bound kernels
 #ifdef VGPU_CHILD_WAVES_PER_EU
     static constexpr int kChildWavesPerEU = VGPU_CHILD_WAVES_PER_EU;
 #else
@@ -17,6 +30,13 @@ struct PandaR {
 #endif
     using Mask = panda_mask_t;
     static constexpr Mask kEnvChecks = panda_env_check_bits;
+    // children register classes (ChildClasses): VGPRs per check when compiled alone (Grp8, gfx950):
+    // most <= 49; 6, 7, 19, 20: 59-65; 15, 21: 90, 105
+    static constexpr int kClasses = 3;
+    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 0, 0, 2,
+                                              0, 0, 0, 1, 1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    static constexpr int kClassWaves[kClasses] = {VGPU_PANDA_CLASS0_WAVES, VGPU_PANDA_CLASS1_WAVES,
+                                                  VGPU_PANDA_CLASS2_WAVES};
     __device__ static __forceinline__ void sample(uint64_t k, float v[7]) { panda_sample(k, v); }
     __device__ static __forceinline__ void head(const float* s, const float* g, int lane, float v[7])
     {
