@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--oracle-edges", type=int, default=1 << 18,
                     help="edges checked against the scalar oracle (the CPU rake checks every edge)")
     ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     ap.add_argument("--workload", default="validate",
                     choices=["validate", "capt", "fetch_prm", "prm_edges", "pair", "rrtc"],
                     help="validate: BASELINE configs[1] (the headline); capt: configs[2]; fetch_prm: configs[3] "

@@ -12,9 +12,16 @@
  * Conventions
  *   - Every function returns int: VGPU_OK (0) or a negative VGPU_ERR_* code; the message
  *     is available from vgpu_last_error(ctx).  No C++ exception crosses this boundary.
- *   - Batch functions take DEVICE pointers and enqueue asynchronously on the context's
- *     stream (vgpu_ctx_set_stream / vgpu_sync).  The *_host variants copy in and out and
- *     synchronise (convenience; they measure PCIe, not the kernels).
+ *   - Batch functions take DEVICE pointers and are stream-ordered on the context's stream
+ *     (vgpu_ctx_set_stream / vgpu_sync): inputs are read and outputs written by work enqueued
+ *     on that stream.  Work sizes that depend on the data are read back with a blocking 4-byte
+ *     copy, so these calls are NOT fully asynchronous: a staged pass (fkcc, sample_fkcc, the
+ *     head and tail of validate_motions) reads its first round's per-check counts once (the
+ *     later rounds' layout is computed on the device), and validate_motions reads its
+ *     back-step item count once -- 3 host syncs per staged validate_motions call.  The
+ *     monolithic robots (Baxter, the composite) sync once per validate_motions call.
+ *     The *_host variants copy in and out and synchronise (convenience; they measure PCIe,
+ *     not the kernels).
  *   - Configurations are row-major float32 [n][dim] (reference ConfigurationArray).
  *   - Results use the reference's polarity: 1 = valid (collision-free), 0 = in collision.
  *   - A context is bound to one HIP device and must be used from one host thread at a time.

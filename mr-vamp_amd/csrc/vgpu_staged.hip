@@ -4,11 +4,16 @@
 #include "vgpu_panda.hh"
 #include "vgpu_staged.hh"
 
+// bound kernels: 86 VGPRs when unconstrained (Grp8 sources); at 7 waves/EU (72 VGPRs) they spilled
+// 56 B/lane (~0.95 GB of scratch traffic per validate call), at 5 waves/EU none -- same speed on
+// MI355X (A/B 3.31-3.40 vs 3.32-3.37 ms per 2^20-edge call), so the spill-free budget is the default
 #ifndef VGPU_BOUND_WAVES_PER_EU
-#define VGPU_BOUND_WAVES_PER_EU VGPU_WAVES_PER_EU
+#define VGPU_BOUND_WAVES_PER_EU 5
 #endif
+// children classes (A/B on MI355X, 2^20 cage edges): class 0 at 8 waves/EU 1.5-3 % faster than 7;
+// class 2 at 4 (112 VGPRs, no spill) as fast as 7 (spilling)
 #ifndef VGPU_PANDA_CLASS0_WAVES
-#define VGPU_PANDA_CLASS0_WAVES 7
+#define VGPU_PANDA_CLASS0_WAVES 8
 #endif
 #ifndef VGPU_PANDA_CLASS1_WAVES
 #define VGPU_PANDA_CLASS1_WAVES 7

@@ -29,16 +29,25 @@ for c in ("FETCH_SIZE", "WRITE_SIZE"):
         byd = collections.defaultdict(float)
         name = {}
         for r in rows:
-            byd[r["Dispatch_Id"]] += float(r["Counter_Value"])
-            name[r["Dispatch_Id"]] = (r["Kernel_Name"].split("(")[0].replace("void ", "").replace("vgpu::", ""),
-                                      r["Grid_Size"])
+            byd[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+            name[int(r["Dispatch_Id"])] = (r["Kernel_Name"].split("(")[0].replace("void ", "").replace("vgpu::", ""),
+                                           r["Grid_Size"])
         for d, v in byd.items():
             per[name[d]][c].append(v)
-            if "sphere_fk" not in name[d][0]:
-                step_bytes[c] += v
+        # one validate_motions call = the dispatches from a head bound kernel up to the next one;
+        # calls of the full-mask mode (they contain SrcTailMaskT kernels) and the FK leg are skipped
+        order = sorted(byd)
+        starts = [i for i, d in enumerate(order) if name[d][0].startswith("bound_kernel<") and "SrcHead" in name[d][0]]
+        n_calls = 0
+        for j, i0 in enumerate(starts):
+            i1 = starts[j + 1] if j + 1 < len(starts) else len(order)
+            seg = [order[i] for i in range(i0, i1) if "sphere_fk" not in name[order[i]][0]]
+            if any("SrcTailMask" in name[d][0] or "mask_finish" in name[d][0] for d in seg):
+                continue
+            step_bytes[c] += sum(byd[d] for d in seg)
+            n_calls += 1
         if c == "FETCH_SIZE":
-            calls = sum(1 for d in byd if name[d][0].startswith("bound_kernel<") and "SrcHead" in name[d][0]) or \
-                sum(1 for d in byd if name[d][0].startswith("panda_validate_head_kernel"))
+            calls = n_calls
 out = {"source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE separate passes (tools/profile_round.sh {R}), "
                   "bench.py 2^20-edge cage workload, every validate_motions kernel; "
                   "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 "
