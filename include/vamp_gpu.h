@@ -117,6 +117,13 @@ int vgpu_env_add_heightfield(vgpu_env *env, const float center[3], const float s
  * builds a CAPT (collision/capt.hh:327-398) on the host; *build_ns (optional) = build time. */
 int vgpu_env_add_pointcloud(vgpu_env *env, const float *points, size_t n, float r_min, float r_max,
                             float r_point, int64_t *build_ns);
+/* The same CAPT built on the DEVICE (vgpu_capt_build.hip) from device points
+ * (n x 3 float32, finite -- not checked), e.g. straight from vgpu_filter_pointcloud's output: the
+ * median splits, affordance lists and leaf packing run level by level on ctx's stream, and the
+ * arrays (bit-identical to vgpu_env_add_pointcloud's) are appended to env (ctx's environment or a
+ * host-only one).  Synchronises the stream (array sizes are data-dependent). */
+int vgpu_env_add_pointcloud_device(vgpu_ctx *ctx, vgpu_env *env, const float *points, size_t n, float r_min,
+                                   float r_max, float r_point, int64_t *build_ns);
 /* counts[0] = heightfields, counts[1] = point clouds */
 int vgpu_env_ext_counts(const vgpu_env *env, int32_t counts[2]);
 /* the built CAPT of point cloud `index`: 2^nlog2 leaves, n_aff affordance vectors, top box */

@@ -614,6 +614,27 @@ extern "C" int vgpu_env_add_pointcloud(vgpu_env* e, const float* points, size_t 
     return VGPU_OK;
 }
 
+namespace vgpu {
+hipError_t capt_build_device(const float* points, size_t n, float r_min, float r_max, float r_point, hipStream_t st,
+                             CaptTree& out);  // vgpu_capt_build.hip
+}
+
+extern "C" int vgpu_env_add_pointcloud_device(vgpu_ctx* c, vgpu_env* e, const float* points, size_t n, float r_min,
+                                              float r_max, float r_point, int64_t* build_ns)
+{
+    // env: this context's, or a host-only one (ctx NULL); the build runs on ctx's device and stream
+    if (!c || !e || (e->ctx && e->ctx != c) || (n && !points))
+        return fail(c, VGPU_ERR_INVALID_ARG, "bad add_pointcloud_device");
+    if (n == 0 || n > ((size_t)1 << 26)) return fail(c, VGPU_ERR_INVALID_ARG, "point cloud size");
+    HIPCHK(c, hipSetDevice(c->device));
+    vgpu::CaptTree t;
+    HIPCHK(c, vgpu::capt_build_device(points, n, r_min, r_max, r_point, c->cur, t));
+    if (build_ns) *build_ns = t.build_ns;
+    e->pointclouds.push_back(std::move(t));
+    e->dirty = e->host_dirty = true;
+    return VGPU_OK;
+}
+
 extern "C" int vgpu_env_ext_counts(const vgpu_env* e, int32_t counts[2])
 {
     if (!e || !counts) return VGPU_ERR_INVALID_ARG;

@@ -291,6 +291,25 @@ class Environment:
         self._changed()
         return int(ns.value)
 
+    def add_pointcloud_device(self, points_ptr: int, n: int, r_min: float, r_max: float, r_point: float,
+                              ctx: Optional[Context] = None) -> int:
+        """Environment::add_pointcloud with the CAPT built on the GPU (vgpu_capt_build.hip) from
+        DEVICE points (n x 3 float32, e.g. a filtered cloud already in HBM); the same arrays as
+        add_pointcloud.  The points must stay valid while this environment is used (device
+        environments of other contexts rebuild from them).  Returns the build time in ns."""
+        ctx = ctx or context()
+        lib = load()
+        if self._host is None:
+            h = C.c_void_p()
+            check(lib.vgpu_env_create(None, C.byref(h)))
+            self._host = h
+        ns = C.c_int64()
+        args = (C.c_void_p(int(points_ptr)), int(n), float(r_min), float(r_max), float(r_point))
+        check(lib.vgpu_env_add_pointcloud_device(ctx.h, self._host, *args, C.byref(ns)), ctx.h)
+        self._ops.append(("pointcloud_device", (ctx, args)))
+        self._changed()
+        return int(ns.value)
+
     def pointcloud_arrays(self, index: int = 0) -> dict:
         """The built CAPT's arrays (tests, aabbs, aff_starts, affordances [n][3][8], top box)."""
         lib = load()
@@ -371,6 +390,9 @@ class Environment:
             elif kind == "pointcloud":
                 rc = lib.vgpu_env_add_pointcloud(h, s.points.ctypes.data_as(_lib.F32P), s.points.shape[0], s.r_min,
                                                  s.r_max, s.r_point, None)
+            elif kind == "pointcloud_device":
+                bctx, args = s
+                rc = lib.vgpu_env_add_pointcloud_device(bctx.h, h, *args, None)
             else:
                 if s.center is None:
                     rc = lib.vgpu_env_add_capsule_endpoints(h, _f3(s.p1), _f3(s.p2), float(np.float32(s.r)))
