@@ -1652,8 +1652,10 @@ extern "C" hipError_t vgpu_launch_knn_index(int dim, const float* V, uint32_t n,
 
 static bool knn_dim_ok(int dim) { return dim == 6 || dim == 7 || dim == 8 || dim == 14; }
 
-// below this many vertices the brute-force scan is as fast as building the index
-static constexpr size_t kKnnIndexMin = 16384;
+// below this many vertices the brute-force scan is faster (MI355X, Fetch Halton vertices,
+// tools/knn_scale.py: 100k brute 11.8 / index 18.3 ms, 400k 95 / 104 ms, 2.7M index 1.40 s vs
+// ~4.3 s extrapolated brute)
+static constexpr size_t kKnnIndexMin = 1000000;
 
 extern "C" int vgpu_set_knn_mode(vgpu_ctx* c, int mode)
 {
