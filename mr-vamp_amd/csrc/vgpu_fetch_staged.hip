@@ -9,6 +9,18 @@
 #ifndef VGPU_FETCH_STAGED_WAVES_PER_EU
 #define VGPU_FETCH_STAGED_WAVES_PER_EU 6
 #endif
+// children register classes (ChildClasses, vgpu_staged.hh): VGPRs per check compiled alone
+// (gfx950, Grp8 and Grp1 alike): <= 62 except checks 8, 17, 27, 48, 51, 56, 59 (65-70) and 23 (89);
+// one kernel over all 63 at 6 waves/EU (80 VGPRs) spilled 84-116 B/lane
+#ifndef VGPU_FETCH_CLASS0_WAVES
+#define VGPU_FETCH_CLASS0_WAVES 8
+#endif
+#ifndef VGPU_FETCH_CLASS1_WAVES
+#define VGPU_FETCH_CLASS1_WAVES 7
+#endif
+#ifndef VGPU_FETCH_CLASS2_WAVES
+#define VGPU_FETCH_CLASS2_WAVES 5
+#endif
 
 namespace vgpu {
 
@@ -20,6 +32,12 @@ struct FetchR {
     static constexpr int kChildWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
     using Mask = fetch_mask_t;
     static constexpr Mask kEnvChecks = fetch_env_check_bits;
+    static constexpr int kClasses = 3;
+    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0,
+                                              0, 0, 2, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
+                                              0, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0};
+    static constexpr int kClassWaves[kClasses] = {VGPU_FETCH_CLASS0_WAVES, VGPU_FETCH_CLASS1_WAVES,
+                                                  VGPU_FETCH_CLASS2_WAVES};
     __device__ static __forceinline__ void sample(uint64_t k, float v[8]) { sample_d<8>(k, fetch_s_m, fetch_s_a, v); }
     __device__ static __forceinline__ void head(const float* s, const float* g, int lane, float v[8])
     {

@@ -56,7 +56,6 @@ struct StagedPlan {
 template <class R, class = void>
 struct ChildClasses {
     static constexpr int n = 1;
-    static constexpr bool split = false;
     __host__ __device__ static constexpr int of(int) { return 0; }
     __host__ __device__ static constexpr int waves(int) { return R::kChildWavesPerEU; }
 };
@@ -64,7 +63,6 @@ template <class R>
 struct ChildClasses<R, std::void_t<decltype(R::kClassOf)>> {
     static_assert(R::kClasses <= kPlanMaxClasses, "too many children classes");
     static constexpr int n = R::kClasses;
-    static constexpr bool split = true;
     __host__ __device__ static constexpr int of(int c) { return R::kClassOf[c]; }
     __host__ __device__ static constexpr int waves(int k) { return R::kClassWaves[k]; }
 };
@@ -357,25 +355,17 @@ __global__ __launch_bounds__(kStagedBlock, ChildClasses<R>::waves(K)) void child
     const int lane = (int)(tid % Src::G);
     if (item >= plan->hi[K]) return;  // wave-uniform (segments are wave-aligned)
     const uint32_t item0 = __builtin_amdgcn_readfirstlane(item);
-    int c = 0;
+    // the owning check's fill (unrolled scalar compares against the plan, constant offsets: the
+    // loads batch; a data-dependent scan over checks would chain one memory latency per check)
     uint32_t fill = 0;
-    if constexpr (!ChildClasses<R>::split) {
-        while (!(item0 >= plan->start[c] && item0 < plan->end[c])) ++c;  // scalar: every wave holds one check
-        fill = plan->fill[c];
-    } else {
 #pragma unroll
-        for (int k = 0; k < R::kChecks; ++k)
-            if (ChildClasses<R>::of(k) == K && item0 >= plan->start[k] && item0 < plan->end[k]) fill = plan->fill[k];
-    }
+    for (int k = 0; k < R::kChecks; ++k)
+        if (ChildClasses<R>::of(k) == K && item0 >= plan->start[k] && item0 < plan->end[k]) fill = plan->fill[k];
     if (item >= fill) return;  // segment padding (group-uniform)
     const uint32_t g = items[item];
     float v[R::D];
     src.load(g, lane, v);
-    bool hit;
-    if constexpr (ChildClasses<R>::split)
-        hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bx, by, bz) > 0;
-    else
-        hit = R::template children<Grp, EXT>(c, v, env, bx, by, bz);
+    const bool hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bx, by, bz) > 0;
     if (hit && lane == 0) valid[src.out(g)] = 0;  // every writer stores 0: the race is benign
 }
 
