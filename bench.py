@@ -69,15 +69,29 @@ def parse():
     ap.add_argument("--vertices", type=int, default=100_000,
                     help="prm_edges: roadmap vertices (RoadmapSettings::max_samples default, roadmap.hh:170)")
     ap.add_argument("--draws", type=int, default=4_000_000, help="fetch_prm: Halton draws per step (whole job)")
+    ap.add_argument("--edge-set", default="B", choices=["A", "B"],
+                    help="validate: SURVEY §8(d) config 2 set B (valid endpoints, length capped at 1.0: the headline) "
+                         "or set A (raw uniform pairs, long edges, n_e ~ 20-40)")
+    ap.add_argument("--base", default="000", choices=["000", "220"],
+                    help="validate: PandaBase<0,0,0> (the headline) or the fork's default Panda (2,2,0) "
+                         "(robots/panda_grid.hh:39)")
+    ap.add_argument("--scene", default="cage", choices=["cage", "table_pick"],
+                    help="validate: the 14-sphere cage (the headline) or MotionBenchMaker table_pick_panda scene0001 "
+                         "(tests/golden/panda_table_pick.npz)")
     return ap.parse_args()
 
 
-def make_edges(torch, vamp, env, robot, n_edges, seed, dev):
-    """Valid-endpoint edges, length capped at 1.0 (set B)."""
+def make_edges(torch, vamp, env, robot, n_edges, seed, dev, edge_set="B"):
+    """set B = valid-endpoint edges, length capped at 1.0; set A = raw
+    pairs of uniform configurations (no filter, no cap)."""
     g = torch.Generator(device=dev)
     g.manual_seed(seed)
     sm = torch.tensor(S_M, device=dev)
     sa = torch.tensor(S_A, device=dev)
+    if edge_set == "A":
+        u = torch.rand((2 * n_edges, 7), generator=g, device=dev, dtype=torch.float32)
+        q = torch.addcmul(sa, u, sm)
+        return q[0::2].contiguous(), q[1::2].contiguous()
     pool = []
     have = 0
     need = 2 * n_edges
@@ -132,16 +146,38 @@ def cpu_rake_baseline(vamp, env, robot, starts, goals, seconds):
             "cpu_model": cpu_model(), "ok_fraction": float(ok.mean())}, ok, nb, ne
 
 
-def oracle_sample(starts, goals, n):
-    """The independent checker (oracle/vamp_oracle.c, scalar restatement) on the first n edges."""
+def scene_envs(vamp, scene):
+    """(product Environment, oracle Env, description) of a validate scene: the 14-sphere cage, or
+    MotionBenchMaker table_pick_panda scene0001 as resolved obstacle rows (tests/golden/panda_table_pick.npz)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as op
 
     op.build()
-    env = op.Env()
-    for c in CAGE:
-        env.add_sphere(c, np.float32(0.2))
-    return op.validate_motions(env, starts[:n], goals[:n], (0, 0, 0), host_threads())
+    env, oenv = vamp.Environment(), op.Env()
+    if scene == "cage":
+        for c in CAGE:
+            env.add_sphere(vamp.Sphere(c, 0.2))
+            oenv.add_sphere(c, np.float32(0.2))
+        return env, oenv, "14-sphere cage"
+    fx = np.load(os.path.join(ROOT, "tests", "golden", "panda_table_pick.npz"), allow_pickle=False)
+    for k in ("spheres", "capsules", "zcapsules", "cuboids", "zcuboids"):
+        setattr(oenv, k, [list(r) for r in fx["env_" + k]])
+    for row in fx["env_spheres"]:
+        env.add_sphere(vamp.Sphere(row[0:3], float(row[3])))
+    for row in np.concatenate([fx["env_cuboids"], fx["env_zcuboids"]]):
+        env.add_cuboid(vamp.Cuboid.from_axes(row[0:3], row[3:6], row[6:9], row[9:12], row[12:15]))
+    for row in np.concatenate([fx["env_capsules"], fx["env_zcapsules"]]):
+        p1 = np.array(row[0:3], np.float32)
+        env.add_capsule(vamp.Cylinder(p1, (p1 + np.array(row[3:6], np.float32)).astype(np.float32), float(row[6])))
+    return env, oenv, "MBM table_pick_panda scene0001 (12 cuboids/capsules)"
+
+
+def oracle_sample(oenv, starts, goals, n, base):
+    """The independent checker (oracle/vamp_oracle.c, scalar restatement) on the first n edges."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as op
+
+    return op.validate_motions(oenv, starts[:n], goals[:n], base, host_threads())
 
 
 def cpu_model():
@@ -163,20 +199,16 @@ def parity_record(got_ok, got_n, ref_ok, ref_n, checker):
             "n_mismatches": int((g_n != np.asarray(ref_n)).sum()), "checker": checker}
 
 
-def algorithmic_flops(starts, goals, n=512):
+def algorithmic_flops(oenv, starts, goals, base, n=65536):
     """Executed float ops per edge under reference semantics (validate_motion with early
-    exit), counted by the instrumented restatement (oracle/vamp_oracle.c vo_stats.flops) on a
-    sample of the bench's own edges; split into the first rake block (head kernel) and the
-    back-steps (tail kernel).  Returns (head_per_edge, tail_per_edge)."""
+    exit), counted by the instrumented restatement (oracle/vamp_oracle.c vo_stats.flops) on the
+    first n = 65536 of the bench's own edges; split into the first rake block (head kernel) and the
+    back-steps (tail kernel).  Returns (head_per_edge, tail_per_edge, edges counted)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as op
 
-    op.build()
-    env = op.Env()
-    for c in CAGE:
-        env.add_sphere(c, np.float32(0.2))
-    h, t = op.validate_flops(env, starts[:n], goals[:n])
-    return float(h.mean()), float(t.mean())
+    h, t = op.validate_flops(oenv, starts[:n], goals[:n], base, host_threads())
+    return float(h.mean()), float(t.mean()), int(len(h))
 
 
 def traffic_record(path):
@@ -187,6 +219,14 @@ def traffic_record(path):
             return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+def c_ok_head_items(n_blocks, n_evaluated):
+    """The largest back-step index the tail enumerates per edge: n_e - 1 for an edge that survives its
+    first block (the CPU rake evaluated more than one block), 0 otherwise."""
+    nb = np.asarray(n_blocks, np.int64)
+    ne = np.asarray(n_evaluated, np.int64)
+    return np.where(ne > 1, nb - 1, 0)
 
 
 def strong_slice(n, rank, world):
@@ -783,21 +823,20 @@ def main():
         if world > 1:
             dist.destroy_process_group()
         return
-    env = vamp.Environment()
-    for c in CAGE:
-        env.add_sphere(vamp.Sphere(c, 0.2))
-    robot = vamp.panda_0_0
+    env, oenv, scene_desc = scene_envs(vamp, a.scene)
+    base = (0, 0, 0) if a.base == "000" else (200, 200, 0)
+    robot = vamp.PandaBase(*base)
 
     strong = a.scaling == "strong"
     if strong:  # one fixed batch (the same seed on every rank), this rank's contiguous range
-        s_full, g_full = make_edges(torch, vamp, env, robot, a.edges, seed=shard_seed(0), dev=dev)
+        s_full, g_full = make_edges(torch, vamp, env, robot, a.edges, seed=shard_seed(0), dev=dev, edge_set=a.edge_set)
         lo, E = strong_slice(a.edges, rank, world)
         starts, goals = s_full[lo:lo + E].contiguous(), g_full[lo:lo + E].contiguous()
         del s_full, g_full
         pinned = PinnedShard(torch, starts, goals, dev)
     else:
         E = a.edges
-        starts, goals = make_edges(torch, vamp, env, robot, E, seed=shard_seed(rank), dev=dev)
+        starts, goals = make_edges(torch, vamp, env, robot, E, seed=shard_seed(rank), dev=dev, edge_set=a.edge_set)
     ok = torch.empty(E, dtype=torch.uint8, device=dev)
     nb = torch.empty(E, dtype=torch.int32, device=dev)
 
@@ -907,24 +946,26 @@ def main():
     scan_ms = phases["scan_ms"] / calls
 
     if rank == 0:
-        s_np = starts[: 1 << 17].cpu().numpy()
-        g_np = goals[: 1 << 17].cpu().numpy()
-        f_head, f_tail = algorithmic_flops(s_np, g_np)
+        f_head, f_tail, f_edges = algorithmic_flops(oenv, s_all, g_all, base)
+        # O(n_e^2) back-step enumeration (vgpu_panda.hh rake_block: block k = k sequential subtractions):
+        # its float ops per edge on the tail's items (edges valid after block 0), against the tail's
+        # algorithmic work -- the cost a per-edge prefix kernel would remove
+        tail_items = c_ok_head_items(c_nb, c_ne)
+        backstep_ops = 56.0 * float((tail_items * (tail_items + 1) // 2).sum()) / max(1, len(c_nb))  # 7 rows x 8 lanes
         achieved = f_head * E / (head_ms * 1e-3) / 1e12
         achieved_step = (f_head + f_tail) * E / (kern_ms * 1e-3) / 1e12
-        tr = traffic_record(a.traffic_json)
+        tr = traffic_record(a.traffic_json) if (a.edge_set, a.base, a.scene) == ("B", "000", "cage") else None
         cpu = None
         parity = None
+        parity_failed = []
         if not a.no_cpu and world == 1:
             cpu = cpu_leg
             g_ok, g_nb = ok.cpu().numpy(), nb.cpu().numpy()
             parity = {"cpu_rake": parity_record(g_ok, g_nb, c_ok, c_nb, "mr-vamp_amd/csrc/cpu AVX2 rake, every edge"),
-                      "oracle": parity_record(g_ok, g_nb, *oracle_sample(s_all, g_all, a.oracle_edges),
+                      "oracle": parity_record(g_ok, g_nb, *oracle_sample(oenv, s_all, g_all, a.oracle_edges, base),
                                               "oracle/vamp_oracle.c validate_motion (scalar restatement), first "
                                               f"{a.oracle_edges} edges")}
-            bad = [k for k, v in parity.items() if v["mismatches"] or v["n_mismatches"]]
-            if bad:
-                print(f"PARITY FAILURE: {parity}", file=sys.stderr)
+            parity_failed = [k for k, v in parity.items() if v["mismatches"] or v["n_mismatches"]]
         ms_step = wall_max / a.steps * 1e3
         line = {
             "metric": "validated edge-interpolants/sec (Panda 7-DOF FK+CC)",
@@ -940,11 +981,15 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded uniform Panda configurations; collision-free endpoints, edges capped at 1.0)",
             "config": {
-                "workload": ("BASELINE configs[1]: Panda 7-DOF, 2^20 edges per GPU, 14-sphere cage, "
+                "workload": (f"BASELINE configs[1]: Panda 7-DOF, {E} edges per GPU (set {a.edge_set}), {scene_desc}, "
                              "validate_motion (rake 8, resolution 32, early exit)") if not strong else
                             (f"BASELINE configs[1] strong scaling: one batch of {a.edges} Panda edges split over "
                              f"{world} GPU(s); each step H2D from pinned host memory + validate + D2H of the results"),
-                "robot": "PandaBase<0,0,0>",
+                "robot": f"PandaBase<{base[0]},{base[1]},{base[2]}>",
+                "edge_set": a.edge_set + (" (valid endpoints, length capped at 1.0)" if a.edge_set == "B" else
+                                          " (raw uniform pairs)"),
+                "scene": a.scene,
+                "mean_n_e": float(c_nb.mean()),
                 "edges_per_gpu": E,
                 "interpolants_per_gpu": units_local,
                 "edge_valid_fraction": ok_frac,
@@ -963,12 +1008,17 @@ def main():
                 "unit": "TFLOP/s",
                 "frac": achieved_step / FP32_PEAK_TFLOPS,
                 "traffic": (tr or {}).get("step_bytes_per_call"),
+                "traffic_measured_in_run": False,
                 "algorithmic_flops_per_launch": (f_head + f_tail) * E,
                 "algorithmic_flops_per_edge": f_head + f_tail,
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": EDGE_BYTES * E,
                 "hbm_frac": EDGE_BYTES * E / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "traffic_source": (tr or {}).get("source"),
+                "traffic_source": ("committed PMC record of this workload, not measured in this run: " + a.traffic_json +
+                                   " (" + str((tr or {}).get("source")) + ")") if tr else None,
+                "algorithmic_flops_sample_edges": f_edges,
+                "backstep_subtract_flops_per_edge": backstep_ops,
+                "backstep_frac_of_tail": backstep_ops / max(f_tail, 1e-9),
                 "phase_ms": {"head": head_ms, "scan_and_count": scan_ms, "tail": tail_ms},
                 "phase_frac": {"head": achieved / FP32_PEAK_TFLOPS,
                                "tail": f_tail * E / (max(tail_ms, 1e-9) * 1e-3) / 1e12 / FP32_PEAK_TFLOPS},
@@ -978,7 +1028,10 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
+        if parity_failed:
+            print(f"PARITY FAILURE ({', '.join(parity_failed)}): {parity}", file=sys.stderr)
+            sys.exit(3)
     if world > 1:
         dist.destroy_process_group()
 

@@ -124,6 +124,10 @@ int vgpu_env_add_pointcloud(vgpu_env *env, const float *points, size_t n, float 
  * host-only one).  Synchronises the stream (array sizes are data-dependent). */
 int vgpu_env_add_pointcloud_device(vgpu_ctx *ctx, vgpu_env *env, const float *points, size_t n, float r_min,
                                    float r_max, float r_point, int64_t *build_ns);
+/* Appends a copy of point cloud `index` of src (its built CAPT arrays, host memory) to dst -- e.g.
+ * to realise an environment whose cloud was built once (host or device) on another context without
+ * rebuilding it or keeping the points alive. */
+int vgpu_env_copy_pointcloud(vgpu_env *dst, const vgpu_env *src, int index);
 /* counts[0] = heightfields, counts[1] = point clouds */
 int vgpu_env_ext_counts(const vgpu_env *env, int32_t counts[2]);
 /* the built CAPT of point cloud `index`: 2^nlog2 leaves, n_aff affordance vectors, top box */

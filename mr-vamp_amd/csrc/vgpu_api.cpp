@@ -39,6 +39,7 @@ hipError_t vgpu_launch_gather_rows(const float* q, const uint32_t* idx, const ui
                                    int dim, float* out, hipStream_t st);
 hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, size_t n_edges, uint32_t* item_edge,
                                      hipStream_t st);
+hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long* out, hipStream_t st);
 #define VGPU_STAGED_DECL(NAME)                                                                                       \
     int vgpu_##NAME##_staged_checks(void);                                                                           \
     uint64_t vgpu_##NAME##_staged_env_checks(void);                                                                  \
@@ -219,7 +220,7 @@ struct vgpu_ctx {
     size_t ws_bytes = 0;
     uint32_t* items = nullptr;
     size_t items_cap = 0;
-    uint32_t* total_host = nullptr;
+    uint32_t* total_host = nullptr;  // pinned, 4 words: [0] the 32-bit scan total, [2..3] its 64-bit sum
     // compaction workspace (selected indices' count word + hipcub temp)
     void* aux = nullptr;
     size_t aux_bytes = 0;
@@ -632,6 +633,19 @@ extern "C" int vgpu_env_add_pointcloud_device(vgpu_ctx* c, vgpu_env* e, const fl
     if (build_ns) *build_ns = t.build_ns;
     e->pointclouds.push_back(std::move(t));
     e->dirty = e->host_dirty = true;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_copy_pointcloud(vgpu_env* dst, const vgpu_env* src, int index)
+{
+    if (!dst || !src || index < 0 || (size_t)index >= src->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
+    if (dst == src) {
+        vgpu::CaptTree t = src->pointclouds[index];  // copy before the vector may reallocate
+        dst->pointclouds.push_back(std::move(t));
+    } else {
+        dst->pointclouds.push_back(src->pointclouds[index]);
+    }
+    dst->dirty = dst->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -1123,6 +1137,25 @@ extern "C" int vgpu_fkcc_attach(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, c
     return VGPU_OK;
 }
 
+// The back-step item count of a validate call (cnt[0 .. n_edges) scanned into off): read back once,
+// with its 64-bit sum -- the scan and the item indices are 32-bit, so a batch whose rake blocks do not
+// fit (very long edges) is rejected before any offset is used.
+static int item_total(vgpu_ctx* c, const uint32_t* cnt, const uint32_t* off, size_t n_edges, void* tmp,
+                      size_t tmp_bytes, size_t* n_items)
+{
+    auto* t64 = (unsigned long long*)(((uintptr_t)tmp + tmp_bytes + 7) & ~(uintptr_t)7);
+    HIPCHK(c, vgpu_launch_total64(cnt, n_edges, t64, c->cur));
+    HIPCHK(c, hipMemcpyAsync(c->total_host, off + n_edges, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipMemcpyAsync(c->total_host + 2, t64, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    unsigned long long total = 0;
+    std::memcpy(&total, c->total_host + 2, sizeof(total));
+    if (total != (unsigned long long)c->total_host[0] || total + n_edges >= (1ull << 32))
+        return fail(c, VGPU_ERR_INVALID_ARG, "edges too long: more than 2^32 rake blocks in one call (split the batch)");
+    *n_items = (size_t)total;
+    return VGPU_OK;
+}
+
 static int ensure_ws(vgpu_ctx* c, size_t n_edges, uint32_t** cnt, uint32_t** off, void** tmp, size_t* tmp_bytes)
 {
     const size_t idx_bytes = ((n_edges + 1) * sizeof(uint32_t) + 255) & ~(size_t)255;
@@ -1137,7 +1170,7 @@ static int ensure_ws(vgpu_ctx* c, size_t n_edges, uint32_t** cnt, uint32_t** off
         HIPCHK(c, hipMalloc(&c->ws, need));
         c->ws_bytes = need;
     }
-    if (!c->total_host) HIPCHK(c, hipHostMalloc((void**)&c->total_host, sizeof(uint32_t), hipHostMallocDefault));
+    if (!c->total_host) HIPCHK(c, hipHostMalloc((void**)&c->total_host, 4 * sizeof(uint32_t), hipHostMallocDefault));
     char* p = (char*)c->ws;
     *cnt = (uint32_t*)p;
     *off = (uint32_t*)(p + idx_bytes);
@@ -1204,10 +1237,9 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     }
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[1], c->cur));
     HIPCHK(c, vgpu_launch_scan(cnt, off, n_edges, tmp, tmp_bytes, c->cur));
-    // number of back-step work items: one D2H word (the item buffer is sized from it)
-    HIPCHK(c, hipMemcpyAsync(c->total_host, off + n_edges, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
-    HIPCHK(c, hipStreamSynchronize(c->cur));
-    const size_t n_items = *c->total_host;
+    // number of back-step work items: one read-back (the item buffer is sized from it)
+    size_t n_items = 0;
+    if ((rc = item_total(c, cnt, off, n_edges, tmp, tmp_bytes, &n_items))) return rc;
     if (n_items > c->items_cap) {
         if (c->items) HIPCHK(c, hipFree(c->items));
         c->items = nullptr;
@@ -1277,9 +1309,8 @@ extern "C" int vgpu_validate_motions_mask(vgpu_ctx* c, const vgpu_robot* r, vgpu
     if ((rc = staged_pass(c, kPandaStaged, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
     HIPCHK(c, vgpu_launch_tail_counts(starts, goals, n_edges, nullptr, n_blocks, cnt, c->cur));  // every back-step
     HIPCHK(c, vgpu_launch_scan(cnt, off, n_edges, tmp, tmp_bytes, c->cur));
-    HIPCHK(c, hipMemcpyAsync(c->total_host, off + n_edges, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
-    HIPCHK(c, hipStreamSynchronize(c->cur));
-    const size_t n_items = *c->total_host;
+    size_t n_items = 0;
+    if ((rc = item_total(c, cnt, off, n_edges, tmp, tmp_bytes, &n_items))) return rc;
     *n_total = n_items + n_edges;
     if (!block_ok || block_cap < *n_total)
         return fail(c, VGPU_ERR_INVALID_ARG, "block_ok capacity < total blocks (*n_total)");
@@ -1418,7 +1449,7 @@ extern "C" int vgpu_compact(vgpu_ctx* c, const float* rows, const uint8_t* valid
         HIPCHK(c, hipMalloc(&c->aux, need));
         c->aux_bytes = need;
     }
-    if (!c->total_host) HIPCHK(c, hipHostMalloc((void**)&c->total_host, sizeof(uint32_t), hipHostMallocDefault));
+    if (!c->total_host) HIPCHK(c, hipHostMalloc((void**)&c->total_host, 4 * sizeof(uint32_t), hipHostMallocDefault));
     uint32_t* cnt = (uint32_t*)c->aux;
     HIPCHK(c, vgpu_launch_compact(valid, n, index_out, cnt, (char*)c->aux + 256, tmp, c->cur));
     if (rows_out) HIPCHK(c, vgpu_launch_gather_rows(rows, index_out, cnt, n, dim, rows_out, c->cur));

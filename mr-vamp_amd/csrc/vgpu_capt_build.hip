@@ -342,7 +342,7 @@ hipError_t capt_build_device(const float* pts, size_t n, float r_min, float r_ma
     const float aff_l2 = l1 * l1, min_l2 = (r_min + r_point) * (r_min + r_point);
     float *P = nullptr, *tests = nullptr, *aabbs = nullptr, *aff = nullptr, *top = nullptr;
     uint32_t *ord = nullptr, *cur_off = nullptr, *cur_ids = nullptr, *cnt = nullptr, *nxt_off = nullptr,
-             *nxt_ids = nullptr, *aff_starts = nullptr;
+             *nxt_ids = nullptr, *aff_starts = nullptr, *ord2 = nullptr;  // ord2: the sorts' ping-pong twin of ord
     uint64_t *ka = nullptr, *kb = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0, cap_cur = 1, cap_nxt = 1;
@@ -368,7 +368,6 @@ hipError_t capt_build_device(const float* pts, size_t n, float r_min, float r_ma
         CB_CHK(hipMalloc(&tmp, tmp_bytes));
     }
     {
-        uint32_t* ord2 = nullptr;
         CB_CHK(hipMalloc(&ord2, m * sizeof(uint32_t)));
         hipLaunchKernelGGL(pad_kernel, dim3(blocks_of(m)), dim3(kBlock), 0, st, pts, n, m, P, ord);
         CB_CHK(hipGetLastError());
@@ -413,8 +412,6 @@ hipError_t capt_build_device(const float* pts, size_t n, float r_min, float r_ma
             std::swap(cur_ids, nxt_ids);
             std::swap(cap_cur, cap_nxt);
         }
-        CB_CHK(hipStreamSynchronize(st));
-        CB_CHK(hipFree(ord2));
     }
     {
         // leaves: cur_off / cur_ids hold every leaf's affordance list
@@ -452,7 +449,7 @@ done:
     (void)hipStreamSynchronize(st);
     for (void* p : {(void*)P, (void*)ord, (void*)ka, (void*)kb, (void*)tests, (void*)cnt, (void*)cur_off,
                     (void*)nxt_off, (void*)cur_ids, (void*)nxt_ids, (void*)aff_starts, (void*)aabbs, (void*)aff,
-                    (void*)top, tmp})
+                    (void*)top, (void*)ord2, tmp})
         if (p) (void)hipFree(p);
     return err;
 }

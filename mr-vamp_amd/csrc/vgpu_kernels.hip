@@ -137,6 +137,17 @@ __global__ __launch_bounds__(kBlock, VGPU_WAVES_PER_EU) void panda_validate_tail
     if (lane == 0 && !valid) ok[e] = 0;  // every writer stores 0: the race is benign
 }
 
+// 64-bit total of the per-edge back-step counts: the item scan is 32-bit, so a batch whose blocks
+// exceed 2^32 must be rejected before its offsets are trusted (one atomic per wave)
+__global__ __launch_bounds__(kBlock) void total64_kernel(const uint32_t* __restrict__ cnt, size_t n,
+                                                         unsigned long long* __restrict__ out)
+{
+    unsigned long long s = 0;
+    for (size_t i = (size_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kBlock) s += cnt[i];
+    for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off);
+    if (__lane_id() == 0 && s) atomicAdd(out, s);
+}
+
 }  // namespace vgpu
 
 static bool has_ext(const EnvView* env) { return env->n_hf > 0 || env->n_pc > 0; }
@@ -234,6 +245,16 @@ hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goa
     else
         hipLaunchKernelGGL(vgpu::panda_validate_head_kernel<false>, dim3(grid), dim3(vgpu::kBlock), 0, st, starts,
                            goals, n_edges, *env, bx, by, bz, ok, n_blocks, cnt);
+    return hipGetLastError();
+}
+
+hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long* out, hipStream_t st)
+{
+    hipError_t err = hipMemsetAsync(out, 0, sizeof(unsigned long long), st);
+    if (err != hipSuccess || n == 0) return err;
+    const size_t want = (n + vgpu::kBlock - 1) / vgpu::kBlock;
+    const unsigned grid = (unsigned)(want < 1024 ? want : 1024);
+    hipLaunchKernelGGL(vgpu::total64_kernel, dim3(grid), dim3(vgpu::kBlock), 0, st, cnt, n, out);
     return hipGetLastError();
 }
 

@@ -238,6 +238,7 @@ class Environment:
         self._ops: List[Tuple[str, object]] = []
         self._handles: Dict[int, C.c_void_p] = {}
         self._host: Optional[C.c_void_p] = None  # host-only twin holding the built CAPTs
+        self._n_clouds = 0  # point clouds in the twin (built once; realised by copying their arrays)
 
     def _changed(self):
         for dev, h in list(self._handles.items()):
@@ -275,19 +276,23 @@ class Environment:
     def attached(self) -> bool:
         return any(op[0] == "attach" for op in self._ops)
 
-    def add_pointcloud(self, points, r_min: float, r_max: float, r_point: float) -> int:
-        """Environment::add_pointcloud (bindings/environment.cc:148-158): builds a CAPT and
-        returns the build time in nanoseconds."""
-        pc = _PointCloud(points, r_min, r_max, r_point)
-        lib = load()
+    def _host_env(self):
         if self._host is None:
             h = C.c_void_p()
-            check(lib.vgpu_env_create(None, C.byref(h)))
+            check(load().vgpu_env_create(None, C.byref(h)))
             self._host = h
+        return self._host
+
+    def add_pointcloud(self, points, r_min: float, r_max: float, r_point: float) -> int:
+        """Environment::add_pointcloud (bindings/environment.cc:148-158): builds a CAPT once (host
+        twin) and returns the build time in nanoseconds; device environments copy its arrays."""
+        pc = _PointCloud(points, r_min, r_max, r_point)
+        host = self._host_env()
         ns = C.c_int64()
-        check(lib.vgpu_env_add_pointcloud(self._host, pc.points.ctypes.data_as(_lib.F32P), pc.points.shape[0],
-                                          pc.r_min, pc.r_max, pc.r_point, C.byref(ns)))
-        self._ops.append(("pointcloud", pc))
+        check(load().vgpu_env_add_pointcloud(host, pc.points.ctypes.data_as(_lib.F32P), pc.points.shape[0],
+                                             pc.r_min, pc.r_max, pc.r_point, C.byref(ns)))
+        self._ops.append(("pointcloud", self._n_clouds))
+        self._n_clouds += 1
         self._changed()
         return int(ns.value)
 
@@ -295,18 +300,15 @@ class Environment:
                               ctx: Optional[Context] = None) -> int:
         """Environment::add_pointcloud with the CAPT built on the GPU (vgpu_capt_build.hip) from
         DEVICE points (n x 3 float32, e.g. a filtered cloud already in HBM); the same arrays as
-        add_pointcloud.  The points must stay valid while this environment is used (device
-        environments of other contexts rebuild from them).  Returns the build time in ns."""
+        add_pointcloud.  The built arrays are kept in the host twin, so the points need not stay
+        alive and every context's environment copies them (no rebuild).  Returns the build time in ns."""
         ctx = ctx or context()
-        lib = load()
-        if self._host is None:
-            h = C.c_void_p()
-            check(lib.vgpu_env_create(None, C.byref(h)))
-            self._host = h
+        host = self._host_env()
         ns = C.c_int64()
         args = (C.c_void_p(int(points_ptr)), int(n), float(r_min), float(r_max), float(r_point))
-        check(lib.vgpu_env_add_pointcloud_device(ctx.h, self._host, *args, C.byref(ns)), ctx.h)
-        self._ops.append(("pointcloud_device", (ctx, args)))
+        check(load().vgpu_env_add_pointcloud_device(ctx.h, host, *args, C.byref(ns)), ctx.h)
+        self._ops.append(("pointcloud", self._n_clouds))
+        self._n_clouds += 1
         self._changed()
         return int(ns.value)
 
@@ -387,12 +389,8 @@ class Environment:
                 rows = np.ascontiguousarray(rows, np.float32)
                 rc = lib.vgpu_env_attach(h, tf.ctypes.data_as(_lib.F32P), rows.ctypes.data_as(_lib.F32P),
                                          rows.shape[0])
-            elif kind == "pointcloud":
-                rc = lib.vgpu_env_add_pointcloud(h, s.points.ctypes.data_as(_lib.F32P), s.points.shape[0], s.r_min,
-                                                 s.r_max, s.r_point, None)
-            elif kind == "pointcloud_device":
-                bctx, args = s
-                rc = lib.vgpu_env_add_pointcloud_device(bctx.h, h, *args, None)
+            elif kind == "pointcloud":  # s = index of the cloud in the host twin
+                rc = lib.vgpu_env_copy_pointcloud(h, self._host, int(s))
             else:
                 if s.center is None:
                     rc = lib.vgpu_env_add_capsule_endpoints(h, _f3(s.p1), _f3(s.p2), float(np.float32(s.r)))
@@ -609,12 +607,13 @@ class Robot:
 
     def validate(self, configuration, environment: Environment) -> bool:
         """vamp.<robot>.validate(q, env) (bindings/common.hh:172-190): bounds check in the
-        descaled unit box, then validate_motion(q, q) == fkcc of the broadcast block."""
-        q = np.asarray(configuration, np.float32)
+        descaled unit box, then validate_motion<Robot, rake, 1>(q, q, env) -- one broadcast block,
+        through fkcc_attach when the environment has an attachment (validate.hh:43)."""
+        q = np.asarray(configuration, np.float32).reshape(self.dimension())
         d = self.descale_configuration(q)
         if not ((d <= 1.0).all() and (d >= 0.0).all()):
             return False
-        return bool(self.cpu_fkcc_batch(q[None, :], environment, threads=1)[0])
+        return self.validate_motion(q, q, environment)
 
     def validate_motion(self, start, goal, environment: Environment) -> bool:
         """planning::validate_motion<Robot, 8, resolution> (planning/validate.hh:67-75)."""

@@ -68,6 +68,7 @@ SIGNATURES = {
                                           C.POINTER(C.c_int64)]),
     "vgpu_env_add_pointcloud_device": (C.c_int, [VP, VP, VP, C.c_size_t, C.c_float, C.c_float, C.c_float,
                                                  C.POINTER(C.c_int64)]),
+    "vgpu_env_copy_pointcloud": (C.c_int, [VP, VP, C.c_int]),
     "vgpu_env_ext_counts": (C.c_int, [VP, I32P]),
     "vgpu_env_pointcloud_info": (C.c_int, [VP, C.c_int, I32P, C.POINTER(C.c_size_t), F32P]),
     "vgpu_env_pointcloud_arrays": (C.c_int, [VP, C.c_int, F32P, F32P, U32P, F32P]),

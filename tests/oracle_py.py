@@ -354,21 +354,30 @@ def scale(q):
     return q
 
 
-def validate_flops(env: Env, starts, goals, base100=(0, 0, 0)):
+def validate_flops(env: Env, starts, goals, base100=(0, 0, 0), threads=8):
     """Executed float ops of validate_motion per edge (reference semantics, early exit),
-    split into the first rake block and the back-steps."""
+    split into the first rake block and the back-steps (edges in parallel chunks: ctypes calls
+    release the GIL)."""
+    from concurrent.futures import ThreadPoolExecutor
     ce = env.c()
     L = lib()
+    starts = np.ascontiguousarray(starts, np.float32).reshape(len(starts), -1)
+    goals = np.ascontiguousarray(goals, np.float32).reshape(len(goals), -1)
     head = np.zeros(len(starts))
     tail = np.zeros(len(starts))
-    for i in range(len(starts)):
-        h = VoStats(np.inf, np.inf, 0.0)
-        t = VoStats(np.inf, np.inf, 0.0)
-        n = C.c_int()
-        s = np.ascontiguousarray(starts[i], np.float32)
-        g = np.ascontiguousarray(goals[i], np.float32)
-        L.vo_panda_validate_motion_split(C.byref(ce), fp(s), fp(g), *base100, C.byref(n), C.byref(h), C.byref(t))
-        head[i], tail[i] = h.flops, t.flops
+
+    def run(lo, hi):
+        for i in range(lo, hi):
+            h = VoStats(np.inf, np.inf, 0.0)
+            t = VoStats(np.inf, np.inf, 0.0)
+            n = C.c_int()
+            L.vo_panda_validate_motion_split(C.byref(ce), fp(starts[i]), fp(goals[i]), *base100, C.byref(n),
+                                             C.byref(h), C.byref(t))
+            head[i], tail[i] = h.flops, t.flops
+
+    chunks = np.linspace(0, len(starts), max(1, threads) + 1).astype(int)
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        list(ex.map(lambda k: run(chunks[k], chunks[k + 1]), range(len(chunks) - 1)))
     return head, tail
 
 

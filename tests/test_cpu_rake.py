@@ -164,6 +164,15 @@ def test_attachment(vamp, oracle):
     ok, n, _ = vamp.panda_0_0.cpu_validate_batch(fx["starts"], fx["goals"], env)
     ook, on = oracle.robot_validate_motions_att("panda", oenv, o, fx["starts"], fx["goals"])
     assert np.array_equal(n, on) and np.array_equal(ok, ook)
+    # vamp.<robot>.validate(q, env) = validate_motion(q, q, env): the attachment is checked
+    # (validate.hh:43, bindings/common.hh:172-182) -- it disagrees with the plain fkcc where only the
+    # held object collides
+    q = fx["q_b000"][:400]
+    inside = ((vamp.panda_0_0.descale_configuration(q) >= 0) & (vamp.panda_0_0.descale_configuration(q) <= 1)).all(1)
+    want = vamp.panda_0_0.cpu_fkcc_batch(q, env, attach=True) & inside
+    got = np.array([vamp.panda_0_0.validate(x, env) for x in q])
+    assert np.array_equal(got, want)
+    assert (got != (vamp.panda_0_0.cpu_fkcc_batch(q, env) & inside)).any()
 
 
 def test_pair(vamp, oracle):

@@ -85,3 +85,28 @@ def test_mbm_cloud_device_build(torch):
     _, _, filt, _, _ = vpc.problem_dict_to_pointcloud("panda", problem, 2000, 0.01, True)
     r_min, r_max = vpc.ROBOT_RADII_RANGES["panda"]
     _device_vs_host(torch, np.asarray(filt, np.float32), r_min, r_max, vpc.POINT_RADIUS)
+
+
+def test_device_built_cloud_outlives_points_and_edits(torch):
+    """The device-built arrays live in the environment's host twin: after the points are freed and an
+    obstacle is added, realising the environment again (handle()) copies the arrays -- no rebuild, no
+    read of the freed buffer -- and fkcc equals an environment built on the host with the same edits."""
+    import vamp_amd as vamp
+    pts = cage_points(4000, 5)
+    d = torch.from_numpy(pts).to("cuda:0")
+    env_d = vamp.Environment()
+    env_d.add_pointcloud_device(d.data_ptr(), pts.shape[0], R_MIN, R_MAX, R_POINT)
+    q = vamp.panda_0_0.scale_configuration(np.random.default_rng(6).uniform(0, 1, (4096, 7)).astype(np.float32))
+    first = vamp.panda_0_0.fkcc_batch(q, env_d)
+    del d
+    torch.cuda.empty_cache()
+    env_d.add_sphere(vamp.Sphere([0.4, 0.0, 0.5], 0.1))  # invalidates the device copy: realised again
+    env_h = vamp.Environment()
+    env_h.add_pointcloud(pts, R_MIN, R_MAX, R_POINT)
+    env_h.add_sphere(vamp.Sphere([0.4, 0.0, 0.5], 0.1))
+    a = vamp.panda_0_0.fkcc_batch(q, env_d)
+    np.testing.assert_array_equal(a, vamp.panda_0_0.fkcc_batch(q, env_h))
+    assert (a <= first).all() and a.sum() < first.sum()
+    if torch.cuda.device_count() > 1:  # a second context realises it from the same arrays
+        ctx1 = vamp.context(1)
+        np.testing.assert_array_equal(vamp.panda_0_0.fkcc_batch(q, env_d, ctx1), a)

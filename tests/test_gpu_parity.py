@@ -202,3 +202,28 @@ def test_full_mask_mode(vamp, oracle):
     with pytest.raises(vamp.VgpuError):  # capacity below the block count
         vamp.panda_0_0.validate_mask_device(ds.data_ptr(), dg.data_ptr(), len(s), env, ok.data_ptr(), 0,
                                             blk.data_ptr(), 10, ctx)
+
+
+def test_too_many_blocks_rejected(vamp, oracle):
+    """The back-step scan and item indices are 32-bit: a batch of edges whose rake blocks exceed 2^32
+    (three edges of ~2^31 blocks each) is rejected with VGPU_ERR_INVALID_ARG before any offset is
+    used (vgpu_api.cpp item_total), in full-mask and early-exit mode alike."""
+    import torch
+    env = vamp.Environment()
+    s = np.zeros((3, 7), F)
+    s[:, 3] = -1.5
+    g = s.copy()
+    g[:, 0] += F(1e9)  # n = ceil(d / 8 * 32) saturates at 2147483520
+    dev = torch.device("cuda", 0)
+    ds, dg = torch.from_numpy(s).to(dev), torch.from_numpy(g).to(dev)
+    ok = torch.empty(3, dtype=torch.uint8, device=dev)
+    nb = torch.empty(3, dtype=torch.int32, device=dev)
+    blk = torch.empty(16, dtype=torch.uint8, device=dev)
+    ctx = vamp.context(0)
+    with pytest.raises(vamp.VgpuError, match="2\\^32"):
+        vamp.panda_0_0.validate_mask_device(ds.data_ptr(), dg.data_ptr(), 3, env, ok.data_ptr(), nb.data_ptr(),
+                                            blk.data_ptr(), blk.numel(), ctx)
+    ctx.sync()
+    # the context stays usable
+    q = oracle.scale(np.random.default_rng(3).random((256, 7), dtype=F))
+    assert np.array_equal(vamp.panda_0_0.fkcc_batch(q, env), oracle.fkcc_threads(oracle.Env(), q))

@@ -141,12 +141,13 @@ def test_knn_index_halton_ties_and_ranges(vamp, oracle):
         _same_lists(got, tuple(x[qf:qf + qc] for x in want))
 
 
-def test_knn_index_equals_brute_force_large(vamp, oracle):
-    """At 2e5 Fetch vertices (beyond the oracle's reach in a test) the indexed query equals the
-    GPU brute force, which equals the oracle at the smaller sizes above."""
+@pytest.mark.parametrize("n", [200000, 1300000], ids=["2e5", "1.3e6"])
+def test_knn_index_equals_brute_force_large(vamp, oracle, n):
+    """Beyond the oracle's reach in a test, the indexed query equals the GPU brute force (which equals
+    the oracle at the smaller sizes above) -- at 2e5 and at 1.3e6 Fetch vertices, the regime where
+    the auto mode picks the index (include/vamp_gpu.h vgpu_set_knn_mode: from 1e6)."""
     import time
-    n = 200000
-    V = oracle.robot_scale("fetch", oracle.halton(8, range(1, n + 1)).astype(F))
+    V = vamp.fetch.scale_configuration(vamp.halton(8, 1, n))
     sm = oracle.SPACE_MEASURE["fetch"]
     t = time.perf_counter()
     idx = knn_gpu(vamp, V, sm, mode=2)
@@ -154,5 +155,7 @@ def test_knn_index_equals_brute_force_large(vamp, oracle):
     t = time.perf_counter()
     bf = knn_gpu(vamp, V, sm, mode=1)
     t_bf = time.perf_counter() - t
-    print(f"knn 2e5 Fetch vertices: index {t_idx * 1e3:.1f} ms, brute force {t_bf * 1e3:.1f} ms (incl. transfers)")
+    print(f"knn {n} Fetch vertices: index {t_idx * 1e3:.1f} ms, brute force {t_bf * 1e3:.1f} ms (incl. transfers)")
     _same_lists(idx, bf)
+    auto = knn_gpu(vamp, V, sm, mode=0)
+    _same_lists(auto, bf)

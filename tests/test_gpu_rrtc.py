@@ -1,0 +1,86 @@
+"""BASELINE configs[0] and the Panda MotionBenchMaker scenes through the HIP path.
+
+configs[0] is "Panda 7-DOF RRT-Connect, one MotionBenchMaker problem, CPU AVX2 reference path": the
+planner is the CPU rake (mr-vamp_amd/csrc/cpu/vcpu_rrtc.cpp, planning/rrtc.hh:33-248), and every path it
+returns is then re-validated as a batch of edges on the GPU (vgpu_validate_motions): the 16 table_pick
+problems at both bases (0,0,0) and the fork's default (2,2,0) (robots/panda_grid.hh:39).  Each segment's
+GPU result must equal the oracle's validate_motion and the CPU rake's, bit for bit, and every segment of
+a solved path is valid.
+
+The table_pick scene fixture (reference-DAG masks and edges, tools/make_golden.py) and the 16 straight
+start -> goal edges go through the GPU too, with coverage and flips printed like the other fixture legs."""
+import numpy as np
+import pytest
+
+from conftest import host_fixture
+from test_gpu_parity import gpu_env_from_oracle
+from test_oracle import EDGE_MIN_COVERAGE, fixture_check, same_rsqrt_host, stable
+from test_rrtc import SETTINGS, problem
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+
+
+@pytest.fixture(scope="module")
+def vamp():
+    import vamp_amd
+    assert vamp_amd.context(0) is not None  # raises without a device / library: no fallback
+    return vamp_amd
+
+
+@pytest.mark.parametrize("base", [(0, 0, 0), (200, 200, 0)], ids=["b000", "b220"])
+def test_rrtc_paths_revalidated_on_gpu(vamp, oracle, base):
+    fx = host_fixture("panda_table_pick_problems.npz", oracle)
+    robot = vamp.PandaBase(*base)
+    n_seg = n_solved = 0
+    for k in range(1, int(fx["n_problems"]) + 1):
+        o, s, g = problem(oracle, fx, k)
+        env = gpu_env_from_oracle(vamp, o)
+        res = robot.rrtc(s, g, env, vamp.RRTCSettings(**SETTINGS), robot.halton())
+        assert res.solved, f"problem {k} unsolved"
+        n_solved += 1
+        a, b = res.path[:-1], res.path[1:]
+        ok_gpu, n_gpu = robot.validate_batch(a, b, env)
+        ok_cpu, n_cpu, _ = robot.cpu_validate_batch(a, b, env)
+        ok_ora, n_ora = oracle.validate_motions(o, a, b, base)
+        assert np.array_equal(n_gpu, n_ora) and np.array_equal(n_cpu, n_ora)
+        assert np.array_equal(ok_gpu, ok_ora.astype(bool)) and np.array_equal(ok_cpu, ok_gpu), f"problem {k}"
+        assert ok_gpu.all(), f"problem {k}: segments {np.nonzero(~ok_gpu)[0]} of a solved path invalid"
+        n_seg += len(a)
+    print(f"configs[0] base {base}: {n_solved}/16 solved, {n_seg} path segments re-validated on the GPU, "
+          f"0 mismatches vs oracle and CPU rake")
+
+
+def test_table_pick_scene_fixture_gpu(vamp, oracle):
+    """SURVEY §8(d) config 2's MBM run: table_pick scene0001 masks and edges on the GPU vs the
+    reference DAG (the CPU-rake leg is tests/test_rrtc.py)."""
+    from test_oracle_robots import scene_env
+    fx = host_fixture("panda_table_pick.npz", oracle)
+    oenv = scene_env(oracle, fx)
+    env = gpu_env_from_oracle(vamp, oenv)
+    same = same_rsqrt_host(oracle, fx)
+    got = vamp.panda_0_0.fkcc_batch(fx["q"], env)
+    assert np.array_equal(got, oracle.fkcc_threads(oenv, fx["q"], (0, 0, 0))), "GPU != oracle on the same host"
+    fixture_check("panda fkcc table_pick (GPU)", got, fx["valid"], stable(fx["test_margin"], fx["cull_margin"], same),
+                  same)
+    ok, n = vamp.panda_0_0.validate_batch(fx["starts"], fx["goals"], env)
+    rok, rn = oracle.validate_motions(oenv, fx["starts"], fx["goals"], (0, 0, 0))
+    assert np.array_equal(ok, rok) and np.array_equal(n, rn) and np.array_equal(n, fx["n"])
+    fixture_check("panda validate_motion table_pick (GPU)", ok, fx["ok"],
+                  stable(fx["edge_test_margin"], fx["edge_cull_margin"], same), same, EDGE_MIN_COVERAGE)
+
+
+def test_table_pick_straight_lines_gpu(vamp, oracle):
+    """The 16 problems' straight start -> goal validate_motion on the GPU vs the reference DAG."""
+    fx = host_fixture("panda_table_pick_problems.npz", oracle)
+    same = same_rsqrt_host(oracle, fx)
+    got, ref, keep = [], [], []
+    for k in range(1, int(fx["n_problems"]) + 1):
+        o, s, g = problem(oracle, fx, k)
+        ok, n = vamp.panda_0_0.validate_batch(s[None], g[None], gpu_env_from_oracle(vamp, o))
+        ook, on = oracle.validate_motions(o, s[None], g[None], (0, 0, 0))
+        assert ok[0] == ook[0] and n[0] == on[0] == fx[f"p{k}_n"][0]
+        got.append(ok[0])
+        ref.append(fx[f"p{k}_ok"][0])
+        keep.append(stable(fx[f"p{k}_test_margin"], fx[f"p{k}_cull_margin"], same)[0])
+    fixture_check("panda table_pick start->goal (GPU)", np.array(got), np.array(ref), np.array(keep), same, 0.5)

@@ -14,7 +14,7 @@ import pytest
 import rrtc_py
 from conftest import host_fixture
 from test_gpu_parity import gpu_env_from_oracle
-from test_oracle import EDGE_MIN_COVERAGE, fixture_check, same_rsqrt_host, stable
+from test_oracle import EDGE_MIN_COVERAGE, MARGIN_TEST, fixture_check, same_rsqrt_host, stable
 
 F = np.float32
 SETTINGS = dict(range=1.0, max_iterations=1000000, max_samples=1000000)
@@ -84,10 +84,21 @@ def test_rrtc_matches_restatement(vamp, oracle, k, base):
     # the ends are the start and goal, or the connect step's last increment onto them (rrtc.hh:213-221
     # walks the other tree from the nearest node's parent)
     assert np.abs(res.path[0] - s).max() <= 1e-5 and np.abs(res.path[-1] - g).max() <= 1e-5
-    # segments: collision-free under the planner's own checks; validate_motion (the caller's view,
-    # recomputing each segment's vector and length) agrees on all but near-boundary segments
-    ok, _ = oracle.validate_motions(o, res.path[:-1], res.path[1:], base)
-    assert ok.mean() >= 0.9, ok
+    # segments: collision-free under the planner's own checks (validate_vector with the planner's
+    # vector and distance); validate_motion recomputes both from the endpoints, which rakes slightly
+    # different interpolants -- so a disagreement is only admissible on a segment that grazes an
+    # obstacle.  Counted exactly: every failing segment must have an interpolant within the fixture
+    # margin band (MARGIN_TEST) of a contact; on the host the fixtures were made on: exactly 0.
+    ok, n = oracle.validate_motions(o, res.path[:-1], res.path[1:], base)
+    bad = np.nonzero(~ok.astype(bool))[0]
+    for i in bad:
+        a, b = res.path[i].astype(np.float64), res.path[i + 1].astype(np.float64)
+        t = np.arange(1, 8 * int(n[i]) + 1) / (8.0 * int(n[i]))
+        q = (a[None] + (b - a)[None] * t[:, None]).astype(F)
+        _, tm, _, _ = oracle.fkcc(o, q, base, stats=True)
+        assert np.abs(tm).min() <= MARGIN_TEST, f"segment {i} invalid far from any contact: {np.abs(tm).min()}"
+    if same_rsqrt_host(oracle, fx):
+        assert len(bad) == 0, f"{len(bad)} near-boundary segment disagreements: {bad}"
 
 
 def test_rrtc_rng_and_settings(vamp, oracle):
