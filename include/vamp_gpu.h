@@ -341,6 +341,17 @@ int vgpu_filter_pointcloud_host(vgpu_ctx *ctx, const float *pc, size_t n, float 
                                 const float origin[3], const float ws_min[3], const float ws_max[3], int cull,
                                 uint32_t *out_idx, size_t *count);
 
+/* vamp.<robot>.filter_from_pointcloud(pointcloud, configuration, environment, point_radius)
+ * (replaces binding::filter_robot_from_pointcloud<Robot>, bindings/common.hh:36-87, bound at :713):
+ * drops every point (radius point_radius) that overlaps one of the robot's spheres at `configuration`
+ * (Robot::sphere_fk<1>, host pointer, dim floats) or collides with the environment.  Device form:
+ * pc[n][3] -> keep[n] (1 = kept).  Host form: the kept points, in input order, -> out[*count][3]
+ * (capacity n).  Panda (with its base offset), Fetch, UR5, Baxter. */
+int vgpu_filter_robot_pointcloud(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, const float *configuration,
+                                 const float *pc, size_t n, float point_radius, uint8_t *keep);
+int vgpu_filter_robot_pointcloud_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env,
+                                      const float *configuration, const float *pc, size_t n, float point_radius,
+                                      float *out, size_t *count);
 int vgpu_pointcloud_collides_host(vgpu_ctx *ctx, vgpu_env *env, int index, const float *centers,
                                   const float *radii, size_t n, int simd, uint8_t *out);
 int vgpu_halton_host(vgpu_ctx *ctx, int dim, uint64_t first, size_t n, float *out);

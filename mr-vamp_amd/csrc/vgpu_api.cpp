@@ -23,6 +23,7 @@
 #include "vgpu_device.hh"
 #include "vgpu_host_env.hh"
 #include "vgpu_ops.hh"
+#include "gen/radii.inc"
 
 extern "C" {
 hipError_t vgpu_launch_panda_sample(uint64_t first, size_t n, float* q, hipStream_t st);
@@ -39,6 +40,8 @@ hipError_t vgpu_launch_gather_rows(const float* q, const uint32_t* idx, const ui
                                    int dim, float* out, hipStream_t st);
 hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, size_t n_edges, uint32_t* item_edge,
                                      hipStream_t st);
+hipError_t vgpu_launch_filter_robot(const float* pc, size_t n, float point_radius, const float* sph, int S,
+                                   const EnvView* env, uint8_t* keep, hipStream_t st);
 hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long* out, hipStream_t st);
 #define VGPU_STAGED_DECL(NAME)                                                                                       \
     int vgpu_##NAME##_staged_checks(void);                                                                           \
@@ -244,6 +247,8 @@ struct vgpu_ctx {
     int knn_mode = 0;
     uint32_t* knn_idx = nullptr;
     size_t knn_idx_cap = 0;
+    // filter_robot_from_pointcloud: the configuration, its sphere_fk<1> centres and the radii
+    float* small = nullptr;
     // optional phase timing
     bool prof = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -350,6 +355,7 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->st_host) (void)hipHostFree(c->st_host);
     if (c->knn_part) (void)hipFree(c->knn_part);
     if (c->knn_idx) (void)hipFree(c->knn_idx);
+    if (c->small) (void)hipFree(c->small);
     if (c->total_host) (void)hipHostFree(c->total_host);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -871,6 +877,7 @@ static EnvView make_view(const vgpu_env* e)
 // batch entry points
 // ---------------------------------------------------------------------------------------
 static const RobotOps* generic_ops(int32_t kind);
+static size_t dim_of(const vgpu_robot* r);
 
 extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t* ns)
 {
@@ -1359,6 +1366,49 @@ extern "C" int vgpu_filter_pointcloud(vgpu_ctx* c, const float* pc, size_t n, fl
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, vgpu_filter_pointcloud_run(pc, n, min_dist, max_range, origin, ws_min, ws_max, cull, out_idx, count,
                                          c->cur));
+    return VGPU_OK;
+}
+
+// filter_robot_from_pointcloud<Robot> (bindings/common.hh:36-87): sphere_fk<1> of the configuration
+// (the robot's own sphere_fk kernel on one row), then one lane per point (vgpu_query.hip)
+static const float* sphere_radii(int32_t kind, int* S)
+{
+    switch (kind) {
+    case VGPU_ROBOT_PANDA: *S = panda_n_spheres_table; return panda_sphere_radii;
+    case VGPU_ROBOT_FETCH: *S = fetch_n_spheres_table; return fetch_sphere_radii;
+    case VGPU_ROBOT_UR5: *S = ur5_n_spheres_table; return ur5_sphere_radii;
+    case VGPU_ROBOT_BAXTER: *S = baxter_n_spheres_table; return baxter_sphere_radii;
+    default: *S = 0; return nullptr;
+    }
+}
+
+extern "C" int vgpu_filter_robot_pointcloud(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* configuration,
+                                            const float* pc, size_t n, float point_radius, uint8_t* keep)
+{
+    if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
+    float b[3];
+    int rc = check_robot(c, r, b);
+    if (rc) return rc;
+    int S = 0;
+    const float* radii = sphere_radii(r->kind, &S);
+    if (!radii) return fail(c, VGPU_ERR_UNSUPPORTED, "filter_from_pointcloud: Panda, Fetch, UR5, Baxter");
+    if (!configuration) return fail(c, VGPU_ERR_INVALID_ARG, "null configuration");
+    if (n == 0) return VGPU_OK;
+    if (!pc || !keep) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if ((rc = vgpu_env_upload(e))) return rc;
+    const EnvView v = make_view(e);
+    HIPCHK(c, hipSetDevice(c->device));
+    constexpr int kSmallFloats = 16 + 4 * 128;
+    if (!c->small) HIPCHK(c, hipMalloc((void**)&c->small, kSmallFloats * sizeof(float)));
+    // [0, 16) configuration, [16, 16 + 3S) sphere_fk centres (ld = 1), then the radii
+    float host[kSmallFloats] = {};
+    const int dim = (int)dim_of(r);
+    std::memcpy(host, configuration, (size_t)dim * sizeof(float));
+    std::memcpy(host + 16 + 3 * S, radii, (size_t)S * sizeof(float));
+    HIPCHK(c, hipMemcpyAsync(c->small, host, kSmallFloats * sizeof(float), hipMemcpyHostToDevice, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));  // host is a stack buffer
+    if ((rc = vgpu_sphere_fk(c, r, c->small, 1, c->small + 16, 1))) return rc;
+    HIPCHK(c, vgpu_launch_filter_robot(pc, n, point_radius, c->small + 16, S, &v, keep, c->cur));
     return VGPU_OK;
 }
 
@@ -1879,5 +1929,31 @@ extern "C" int vgpu_build_roadmap_host(vgpu_ctx* c, const vgpu_robot* robot, vgp
         return fail(c, VGPU_ERR_INVALID_ARG, "adjacency capacity too small (*n_adj = required entries)");
     if ((rc = vgpu_roadmap_assemble(n, pairs.data(), pairs.size() / 2, offsets, adj, component)))
         return fail(c, rc, "roadmap assembly");
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_filter_robot_pointcloud_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e,
+                                                 const float* configuration, const float* pc, size_t n,
+                                                 float point_radius, float* out, size_t* count)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (!count) return fail(c, VGPU_ERR_INVALID_ARG, "null count");
+    *count = 0;
+    if (n == 0) return VGPU_OK;
+    if (!pc || !out) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
+    if (n > 0x7fffffffu) return fail(c, VGPU_ERR_INVALID_ARG, "point cloud size");
+    char* d;
+    const size_t pb = al(n * 12), kb = al(n), ib = al(n * 4);
+    int rc = stage(c, 2 * pb + kb + ib, &d);
+    if (rc) return rc;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipMemcpyAsync(d, pc, n * 12, hipMemcpyHostToDevice, c->cur));
+    uint8_t* keep = (uint8_t*)(d + pb);
+    if ((rc = vgpu_filter_robot_pointcloud(c, r, e, configuration, (const float*)d, n, point_radius, keep))) return rc;
+    // the kept points in input order (std::vector::emplace_back order, common.hh:80-83)
+    if ((rc = vgpu_compact(c, (const float*)d, keep, n, 3, (float*)(d + pb + kb), (uint32_t*)(d + 2 * pb + kb), count)))
+        return rc;
+    HIPCHK(c, hipMemcpyAsync(out, d + pb + kb, *count * 12, hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
 }

@@ -70,6 +70,34 @@ __global__ __launch_bounds__(256) void capt_query_kernel(const float* __restrict
                    : capt_scalar(h, env.base, x, y, z, r)) ? 1 : 0;
 }
 
+// filter_robot_from_pointcloud (bindings/common.hh:36-87): one lane per point.  sph = the robot's
+// sphere_fk<1> output at the configuration, x[S] y[S] z[S], then the radii r[S] (staged in LDS, every
+// lane reads the same sphere: broadcast).  A point is dropped when any robot sphere overlaps it -- the
+// reference's SCALAR float sphere_sphere_sql2 < 0, as its release build computes it:
+// fma(xs, xs, ys * ys) + fma(zs, zs, -(rs * rs)) (ref_probe "sql2s") -- or when it collides with the
+// environment (the broadcast FloatVector sphere_environment_in_collision = one G = 1 lane).
+constexpr int kFilterMaxSpheres = 128;
+template <bool EXT>
+__global__ __launch_bounds__(256) void filter_robot_kernel(const float* __restrict__ pc, size_t n, float pr,
+                                                           const float* __restrict__ sph, int S, EnvView env,
+                                                           uint8_t* __restrict__ keep)
+{
+    __shared__ float s[4 * kFilterMaxSpheres];
+    for (int k = threadIdx.x; k < 4 * S; k += 256) s[k] = sph[k];
+    if constexpr (EXT) capt_stage_lds(env);  // ends in a barrier (covers s[] as well)
+    else __syncthreads();
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    const float x = pc[3 * i], y = pc[3 * i + 1], z = pc[3 * i + 2];
+    bool hit = false;
+    for (int k = 0; k < S; ++k) {
+        const float xs = s[k] - x, ys = s[S + k] - y, zs = s[2 * S + k] - z, rs = s[3 * S + k] + pr;
+        hit |= (__builtin_fmaf(xs, xs, ys * ys) + __builtin_fmaf(zs, zs, -(rs * rs))) < 0.0f;
+    }
+    if (!hit) hit = env_lane<Grp1, EXT>(env, x, y, z, pr);
+    keep[i] = hit ? 0 : 1;
+}
+
 // rng::Halton<dim>::next draws first .. first + n - 1, one lane per draw (random/halton.hh:73-104)
 __global__ __launch_bounds__(256) void halton_kernel(int dim, uint64_t first, size_t n, float* __restrict__ out)
 {
@@ -96,5 +124,20 @@ extern "C" hipError_t vgpu_launch_capt_query(const float* centers, const float* 
     const unsigned grid = (unsigned)((n + 255) / 256);
     hipLaunchKernelGGL(vgpu::capt_query_kernel, dim3(grid), dim3(256), 0, st, centers, radii, n, *env, index, simd,
                        out);
+    return hipGetLastError();
+}
+
+extern "C" hipError_t vgpu_launch_filter_robot(const float* pc, size_t n, float point_radius, const float* sph, int S,
+                                               const EnvView* env, uint8_t* keep, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    if (S < 0 || S > vgpu::kFilterMaxSpheres) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)((n + 255) / 256);
+    if (env->n_hf > 0 || env->n_pc > 0)
+        hipLaunchKernelGGL(vgpu::filter_robot_kernel<true>, dim3(grid), dim3(256), 0, st, pc, n, point_radius, sph, S,
+                           *env, keep);
+    else
+        hipLaunchKernelGGL(vgpu::filter_robot_kernel<false>, dim3(grid), dim3(256), 0, st, pc, n, point_radius, sph, S,
+                           *env, keep);
     return hipGetLastError();
 }

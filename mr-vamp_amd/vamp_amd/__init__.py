@@ -499,6 +499,44 @@ class Halton:
         self.index += int(n)
 
 
+class PRMNeighborParams:
+    """vamp.PRMNeighborParams(dim, space_measure) = planning::PRMStarNeighborParams (roadmap.hh:42-77,
+    bindings/settings.cc:38-44): PRM* k(n) = ceil((e + e/dim) ln n), r(n) from the space measure,
+    gamma_scale 2.0."""
+
+    def __init__(self, dim: int, space_measure: float):
+        self.dim = int(dim)
+        self.space_measure = float(space_measure)
+        self.gamma_scale = 2.0
+
+    def _kr(self, num_states: int):
+        from .roadmap import prm_neighbor_params
+        k, r = prm_neighbor_params(self.dim, self.space_measure, int(num_states) + 1, self.gamma_scale)
+        return int(k[num_states]), float(r[num_states])
+
+    def max_neighbors(self, num_states: int) -> int:
+        return self._kr(num_states)[0]
+
+    def neighbor_radius(self, num_states: int) -> float:
+        return self._kr(num_states)[1]
+
+
+class PRMSettings:
+    """vamp.PRMSettings(neighbor_params) = RoadmapSettings<PRMStarNeighborParams> (roadmap.hh:150-171,
+    bindings/settings.cc:46-53): max_iterations = max_samples = 100000 by default."""
+
+    def __init__(self, neighbor_params: PRMNeighborParams):
+        self.neighbor_params = neighbor_params
+        self.max_iterations = 100000
+        self.max_samples = 100000
+
+    def max_neighbors(self, num_states: int) -> int:
+        return self.neighbor_params.max_neighbors(num_states)
+
+    def neighbor_radius(self, num_states: int) -> float:
+        return self.neighbor_params.neighbor_radius(num_states)
+
+
 class PlanningResult:
     """vamp::planning::PlanningResult (planning/plan.hh): path, cost, iterations, size, nanoseconds."""
 
@@ -615,6 +653,32 @@ class Robot:
             return False
         return self.validate_motion(q, q, environment)
 
+    def filter_from_pointcloud(self, pointcloud, configuration, environment: Environment, point_radius: float,
+                               ctx: Optional[Context] = None) -> np.ndarray:
+        """vamp.<robot>.filter_from_pointcloud(pointcloud, configuration, environment, point_radius)
+        (bindings/common.hh:36-87,713): the points that neither overlap the robot's spheres at
+        `configuration` nor collide with the environment, in input order, as float32 [m][3] -- on
+        the GPU (sphere_fk + one lane per point, vgpu_filter_robot_pointcloud_host)."""
+        ctx = ctx or context()
+        pc = np.ascontiguousarray(pointcloud, np.float32).reshape(-1, 3)
+        q = np.ascontiguousarray(configuration, np.float32).reshape(self.dimension())
+        out = np.empty((max(pc.shape[0], 1), 3), np.float32)
+        cnt = C.c_size_t(0)
+        check(load().vgpu_filter_robot_pointcloud_host(ctx.h, C.byref(self.c_robot), environment.handle(ctx),
+                                                       q.ctypes.data_as(_lib.F32P), pc.ctypes.data_as(_lib.F32P),
+                                                       pc.shape[0], float(point_radius), out.ctypes.data_as(_lib.F32P),
+                                                       C.byref(cnt)), ctx.h)
+        return out[:cnt.value].copy()
+
+    def filter_from_pointcloud_device(self, pc_ptr: int, n: int, configuration, environment: Environment,
+                                      point_radius: float, keep_ptr: int, ctx: Optional[Context] = None):
+        """Device form: pc[n][3] (device) -> keep[n] (device uint8, 1 = kept), stream-ordered."""
+        ctx = ctx or context()
+        q = np.ascontiguousarray(configuration, np.float32).reshape(self.dimension())
+        check(load().vgpu_filter_robot_pointcloud(ctx.h, C.byref(self.c_robot), environment.handle(ctx),
+                                                  q.ctypes.data_as(_lib.F32P), C.c_void_p(pc_ptr), int(n),
+                                                  float(point_radius), C.c_void_p(keep_ptr)), ctx.h)
+
     def validate_motion(self, start, goal, environment: Environment) -> bool:
         """planning::validate_motion<Robot, 8, resolution> (planning/validate.hh:67-75)."""
         s = np.ascontiguousarray(start, np.float32).reshape(self.dimension())
@@ -667,6 +731,41 @@ class Robot:
         rng.index = int(idx.value)
         return PlanningResult(path[:res.path_len].copy(), float(res.cost), int(res.iterations),
                               (int(res.size[0]), int(res.size[1])), int(res.nanoseconds), bool(res.solved))
+
+    def roadmap(self, start, goal, environment: Environment, settings: Optional[PRMSettings] = None,
+                rng: Optional[Halton] = None, ctx: Optional[Context] = None):
+        """vamp.<robot>.roadmap(start, goal, environment, settings, rng) (bindings/common.hh:312-321,667 ->
+        PRM::build_roadmap, planning/prm.hh:197-299) on the GPU: the sampler's draws rng.index ..
+        rng.index + max_iterations - 1 through the fused Halton -> scale -> fkcc kernel (sharded over
+        the ranks when torch.distributed is initialised), the vertex sequence start, goal, valid samples
+        in draw order cut at max_samples, then every vertex's PRM* neighbour query and validate_motion
+        of its candidates, adjacency in the reference's append order.  Returns a Roadmap with
+        vertices, edges, nanoseconds and iterations (= draws taken + 1, the reference loop's count);
+        rng advances by the draws taken."""
+        import time
+
+        from . import roadmap as _rm
+        settings = settings or PRMSettings(PRMNeighborParams(self.dimension(), self.space_measure()))
+        rng = rng or self.halton()
+        dim = self.dimension()
+        s = np.ascontiguousarray(start, np.float32).reshape(dim)
+        g = np.ascontiguousarray(goal, np.float32).reshape(dim)
+        t0 = time.perf_counter_ns()
+        max_it, max_s = int(settings.max_iterations), int(settings.max_samples)
+        rows, draws = _rm.roadmap_vertices(self, environment, max_it, rng.index, s, g, max(max_s, 2), ctx)
+        draws = draws.cpu().numpy()
+        taken = max_it
+        if max_s <= 2:  # the loop never draws (nodes.size() < max_samples fails at once)
+            taken = 0
+        elif len(draws) >= max_s:  # the last vertex's draw ends the loop
+            taken = int(draws[max_s - 1]) - rng.index + 1
+        rm = _rm.build_roadmap_edges(self, environment, rows.cpu().numpy(),
+                                     settings.neighbor_params.gamma_scale, settings.neighbor_params.space_measure,
+                                     ctx)
+        rng.skip(taken)
+        rm.nanoseconds = time.perf_counter_ns() - t0
+        rm.iterations = taken + 1
+        return rm
 
     def cpu_validate_vector(self, start, vector, distance: float, environment: Environment) -> bool:
         """planning::validate_vector<Robot, 8, resolution>(start, vector, distance, env)."""
@@ -881,4 +980,4 @@ __all__ += ["PandaPair", "panda_pair"]
 # robots/ur5.hh (6 dof) and robots/baxter.hh (14-dof dual arm): no base offset
 ur5 = Robot("ur5", 0, 0, 0, kind=_lib.VGPU_ROBOT_UR5)
 baxter = Robot("baxter", 0, 0, 0, kind=_lib.VGPU_ROBOT_BAXTER)
-__all__ += ["ur5", "baxter", "RRTCSettings", "Halton", "PlanningResult"]
+__all__ += ["ur5", "baxter", "RRTCSettings", "Halton", "PlanningResult", "PRMNeighborParams", "PRMSettings"]

@@ -78,6 +78,9 @@ SIGNATURES = {
                                          C.POINTER(C.c_size_t)]),
     "vgpu_filter_pointcloud_host": (C.c_int, [VP, F32P, C.c_size_t, C.c_float, C.c_float, F32P, F32P, F32P,
                                               C.c_int, U32P, C.POINTER(C.c_size_t)]),
+    "vgpu_filter_robot_pointcloud": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, VP, C.c_size_t, C.c_float, VP]),
+    "vgpu_filter_robot_pointcloud_host": (C.c_int, [VP, C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, C.c_float,
+                                                    F32P, C.POINTER(C.c_size_t)]),
     "vgpu_env_upload": (C.c_int, [VP]),
     "vgpu_env_attach": (C.c_int, [VP, F32P, F32P, C.c_size_t]),
     "vgpu_env_detach": (C.c_int, [VP]),

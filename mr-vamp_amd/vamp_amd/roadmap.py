@@ -133,6 +133,18 @@ class Roadmap:
         self.offsets = offsets
         self.adj = adj
         self.component = component
+        self.nanoseconds = 0  # Roadmap::nanoseconds / iterations (plan.hh:182-188), set by Robot.roadmap
+        self.iterations = 0
+
+    # the Python face of the reference's Roadmap (bindings/common.hh:550-574)
+    def __len__(self) -> int:
+        return len(self.vertices)
+
+    def __getitem__(self, i):
+        return self.vertices[i]
+
+    def __iter__(self):
+        return iter(self.vertices)
 
     @property
     def edges(self) -> List[List[int]]:

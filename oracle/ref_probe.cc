@@ -19,7 +19,8 @@
 //     are restated below with the reference's own FloatVector types because
 //     validate.hh itself includes environment.hh -> Eigen)
 //   * rng::Halton<dim>::next                                (random/halton.hh:73-104)
-//   * collision::sql2_3 on FloatVector (collision/math.hh:29-42), the CAPT affordance test
+//   * collision::sql2_3 on FloatVector (collision/math.hh:29-42), the CAPT affordance test, and the
+//     scalar sphere_sphere_sql2 of filter_robot_from_pointcloud (bindings/common.hh:71-72)
 //   * expression probes for code whose header cannot be compiled here (capt.hh needs
 //     <pdqsort.h>, sphere_heightfield.hh needs shapes.hh -> Eigen): the CAPT leaf-box test
 //     (capt.hh:505-521), Volume::distsq_to / contained_by_internal_ball (capt.hh:70-89) and
@@ -150,6 +151,16 @@ __attribute__((noinline)) static void probe_hf(const float *x, const float *y, c
     auto zh = FloatVector<8>::gather(data, indices);
     auto zhs = hzs * zh + hz;
     (Z - R - zhs).to_array(out);
+}
+
+// filter_robot_from_pointcloud's sphere test (bindings/common.hh:71-72): scalar float
+// collision::sphere_sphere_sql2 = sql2_3<float>(a, b) - (ar + br)^2 (sphere_sphere.hh:20-22; that
+// header includes shapes.hh -> Eigen, so its two lines are restated over the reference's own sql2_3)
+__attribute__((noinline)) static float probe_sql2_scalar(const float *a, const float *b)
+{
+    auto sum = collision::sql2_3(a[0], a[1], a[2], b[0], b[1], b[2]);
+    auto rs = a[3] + b[3];
+    return sum - rs * rs;
 }
 
 // Robot::scale_configuration shape (robots/panda/fk.hh:34-37): q * s_m + s_a on FloatVector<7>
@@ -339,6 +350,15 @@ int main(int argc, char **argv)
             probe_sql2(launder(ax), ay, az, in[6 * i + 3], in[6 * i + 4], in[6 * i + 5], o);
             std::memcpy(&out[i], o, 32);
         }
+        write_f32(argv[3], out);
+    }
+    else if (mode == "sql2s")
+    {
+        // in: N x 8 (ax ay az ar bx by bz br).  out: N scalar sphere_sphere_sql2 values
+        auto in = read_f32(argv[2]);
+        const size_t n = in.size() / 8;
+        std::vector<float> out(n);
+        for (size_t i = 0; i < n; ++i) out[i] = probe_sql2_scalar(launder(&in[8 * i]), &in[8 * i + 4]);
         write_f32(argv[3], out);
     }
     else if (mode == "capt_box")

@@ -109,6 +109,9 @@ void vo_capt_collides_batch(const vo_capt *t, const float *centers, const float 
  * the collides_simd leaf-box distance (FloatVector clamp), Volume::distsq_to and the
  * contained_by_internal_ball sum (scalar) */
 float vo_sql2_3(float ax, float ay, float az, float bx, float by, float bz);
+/* scalar float sphere_sphere_sql2 (sphere_sphere.hh:20-22) as the release build contracts it (ref_probe
+ * "sql2s"): fma(xs, xs, ys*ys) + fma(zs, zs, -(rs*rs)) */
+float vo_sql2_scalar(float ax, float ay, float az, float ar, float bx, float by, float bz, float br);
 float vo_capt_box_vec(const float c[3], const float lo[3], const float up[3]);
 float vo_capt_vol_distsq(const float p[3], const float lo[3], const float up[3]);
 float vo_capt_vol_ball(const float p[3], const float lo[3], const float up[3]);
@@ -125,6 +128,10 @@ int vo_robot_nspheres(int robot);
 float vo_l2_norm(const float *v, int dim);                                   /* dim <= 16 */
 void vo_robot_scale(int robot, float *q);                                    /* scale_configuration */
 void vo_robot_sphere_fk(int robot, const float *q, int bx100, int by100, int bz100, float out_xyz[][3]);
+/* filter_robot_from_pointcloud (bindings/common.hh:36-87): keep[i] = 1 when point i (radius
+ * point_radius) overlaps no robot sphere at q and is clear of the environment */
+void vo_robot_filter_pointcloud(int robot, const vo_env *env, const float *q, int bx100, int by100, int bz100,
+                                const float *pc, size_t n, float point_radius, uint8_t *keep);
 /* q is [G][dim]; returns 1 = valid */
 int vo_robot_fkcc_block(int robot, const vo_env *env, const float *q, int G, int bx100, int by100, int bz100,
                         vo_stats *stats);

@@ -403,6 +403,21 @@ def robot_sphere_fk(robot, q, base100=(0, 0, 0)):
     return out
 
 
+def robot_filter_pointcloud(robot, env: Env, q, pc, point_radius, base100=(0, 0, 0)):
+    """filter_robot_from_pointcloud (bindings/common.hh:36-87): keep mask [n] (oracle/vamp_oracle.c)"""
+    rid, dim, _ = ROBOTS[robot]
+    q = np.ascontiguousarray(q, np.float32).reshape(dim)
+    pc = np.ascontiguousarray(pc, np.float32).reshape(-1, 3)
+    keep = np.zeros(pc.shape[0], np.uint8)
+    ce = env.c()
+    L = lib()
+    L.vo_robot_filter_pointcloud.argtypes = [C.c_int, C.c_void_p, F32P, C.c_int, C.c_int, C.c_int, F32P, C.c_size_t,
+                                             C.c_float, U8P]
+    L.vo_robot_filter_pointcloud(rid, C.byref(ce), fp(q), *base100, fp(pc), pc.shape[0], float(point_radius),
+                                 keep.ctypes.data_as(U8P))
+    return keep.astype(bool)
+
+
 def robot_fkcc(robot, env: Env, q, base100=(0, 0, 0), G=1, stats=False):
     rid, dim, _ = ROBOTS[robot]
     q = np.ascontiguousarray(q, np.float32).reshape(-1, dim)

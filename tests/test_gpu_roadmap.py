@@ -159,3 +159,31 @@ def test_knn_index_equals_brute_force_large(vamp, oracle, n):
     _same_lists(idx, bf)
     auto = knn_gpu(vamp, V, sm, mode=0)
     _same_lists(auto, bf)
+
+
+@pytest.mark.parametrize("max_iterations,max_samples", [(3000, 800), (2000, 100000)], ids=["samples", "iterations"])
+def test_robot_roadmap_binding(vamp, oracle, max_iterations, max_samples):
+    """vamp.<robot>.roadmap(start, goal, environment, settings, rng) (bindings/common.hh:312-321,667):
+    the vertex sequence, the adjacency lists, iterations (= draws + 1, prm.hh:235,292) and the rng's
+    advance equal the reference loop restated over the oracle, whichever limit ends it."""
+    rng = np.random.default_rng(31)
+    oenv = random_scene(oracle, rng, 3, 3, 2)
+    env = gpu_env_from_oracle(vamp, oenv)
+    robot = vamp.panda_0_0
+    pool = oracle.scale(rng.random((64, 7), dtype=F))
+    pv = oracle.fkcc_threads(oenv, pool)
+    s, g = pool[pv][0], pool[pv][1]
+    settings = vamp.PRMSettings(vamp.PRMNeighborParams(7, robot.space_measure()))
+    settings.max_iterations, settings.max_samples = max_iterations, max_samples
+    h = robot.halton()
+    h.skip(10)  # draws 11 ..
+    rm = robot.roadmap(s, g, env, settings, h)
+    q = oracle.scale(oracle.halton(7, range(11, 11 + max_iterations)))
+    ok = oracle.fkcc_threads(oenv, q)
+    want = np.concatenate([s[None], g[None], q[ok]])[:max_samples]
+    assert np.array_equal(rm.vertices, want) and len(rm) == len(want)
+    taken = int(np.nonzero(ok)[0][max_samples - 3]) + 1 if ok.sum() >= max_samples - 2 else max_iterations
+    assert h.index == 11 + taken and rm.iterations == taken + 1
+    edges, _ = oracle.build_roadmap_edges("panda", oenv, want)
+    assert rm.edges == edges
+    assert rm.nanoseconds > 0 and np.array_equal(rm[5], want[5])

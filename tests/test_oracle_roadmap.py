@@ -87,3 +87,15 @@ def test_build_roadmap_edges_structure(oracle):
         for j in edges[i]:
             assert comp[i] == comp[j]
     assert ok.sum() > 0 and (~ok).sum() > 0
+
+
+def test_prm_settings_mirror(oracle):
+    """vamp.PRMNeighborParams / PRMSettings (bindings/settings.cc:38-53): defaults and k/r equal the
+    oracle's PRMStarNeighborParams (roadmap.hh:42-77)."""
+    import vamp_amd as vamp
+    p = vamp.PRMNeighborParams(7, vamp.panda.space_measure())
+    st = vamp.PRMSettings(p)
+    assert st.max_iterations == 100000 and st.max_samples == 100000 and p.gamma_scale == 2.0
+    for n in (2, 3, 10, 1000, 123457):
+        assert st.max_neighbors(n) == oracle.prm_max_neighbors(7, n)
+        assert np.float32(st.neighbor_radius(n)) == np.float32(oracle.prm_neighbor_radius(7, p.space_measure, 2.0, n))

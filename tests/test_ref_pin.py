@@ -157,3 +157,17 @@ def test_scale_configuration_bit_exact(oracle, ext):
     per joint; the Halton -> configuration step of the sampling path."""
     got = oracle.scale(ext["scale_u"])
     assert np.array_equal(got.view(np.uint32), ext["scale_q"].view(np.uint32))
+
+
+def test_sql2_scalar_bit_exact(oracle):
+    """filter_robot_from_pointcloud's robot-sphere test (bindings/common.hh:71-72): the scalar float
+    sphere_sphere_sql2 as the reference's release build contracts it -- fma(xs, xs, ys*ys) +
+    fma(zs, zs, -(rs*rs)) -- on 65536 inputs, half of them within 1e-6 of contact
+    (tests/golden/ref_pins_sql2s.npz, tools/make_golden.py --sql2s)."""
+    z = golden("ref_pins_sql2s.npz")
+    L = oracle.lib()
+    L.vo_sql2_scalar.restype = C.c_float
+    L.vo_sql2_scalar.argtypes = [C.c_float] * 8
+    got = np.array([L.vo_sql2_scalar(*map(float, row)) for row in z["sql2s_in"]], F)
+    assert (got.view(np.uint32) == z["sql2s"].view(np.uint32)).all()
+    assert 0.2 < np.signbit(z["sql2s"]).mean() < 0.8

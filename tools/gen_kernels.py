@@ -656,8 +656,26 @@ class RobotGen:
         return "\n".join(out)
 
 
+def gen_radii(paths) -> str:
+    """Host-and-device table of every robot's collision-sphere radii (reference order, the
+    Spheres<rake>::r of Robot::sphere_fk): used where a kernel needs the radii next to
+    sphere_fk's centres (filter_robot_from_pointcloud, bindings/common.hh:36-87)."""
+    out = ["// GENERATED by tools/gen_kernels.py --radii from model/*.json -- do not edit.", "#pragma once", ""]
+    for path in paths:
+        m = json.load(open(path))
+        vals = ", ".join(flit(sp["radius"]) for sp in m["spheres"])
+        out.append(f"constexpr int {m['robot']}_n_spheres_table = {len(m['spheres'])};")
+        out.append(f"constexpr float {m['robot']}_sphere_radii[{len(m['spheres'])}] = {{{vals}}};")
+    return "\n".join(out) + "\n"
+
+
 def main():
     global REMAT, TY
+    if "--radii" in sys.argv:  # tools/gen_kernels.py --radii OUT model/a.json model/b.json ...
+        args = [a for a in sys.argv[1:] if a != "--radii"]
+        open(args[0], "w").write(gen_radii(args[1:]))
+        print(f"wrote {args[0]}")
+        return
     if "--no-remat" in sys.argv:
         REMAT = False
         sys.argv.remove("--no-remat")

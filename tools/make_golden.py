@@ -102,6 +102,20 @@ def make_ref_pins(rng):
                         halton8=h8, halton8_k=k8)
 
 
+def make_sql2s_pins(rng):
+    """ref_probe "sql2s": the scalar float sphere_sphere_sql2 of filter_robot_from_pointcloud
+    (bindings/common.hh:71-72), half the inputs within 1e-6 (relative) of contact."""
+    n = 65536
+    a = rng.uniform(-1, 1, (n, 8)).astype(F)
+    a[:, 3] = rng.uniform(0.01, 0.3, n)
+    a[:, 7] = rng.choice(np.array([0.0025, 0.01, 0.05], F), n)
+    d = rng.normal(size=(n // 2, 3))
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    h = n // 2
+    a[:h, 4:7] = (a[:h, 0:3] + d * (a[:h, 3:4] + a[:h, 7:8]) * (1 + rng.uniform(-1e-6, 1e-6, (h, 1)))).astype(F)
+    np.savez_compressed(os.path.join(GOLD, "ref_pins_sql2s.npz"), sql2s_in=a, sql2s=probe("sql2s", a))
+
+
 def make_ext_pins(rng):
     """Expression pins for the point-cloud and heightfield paths (ref_probe modes sql2,
     capt_box, hf): collision::sql2_3 compiled from the reference's math.hh, and restated
@@ -496,6 +510,10 @@ def main():
         return
     if "--attach-fetch" in sys.argv:
         make_attach_robot(np.random.default_rng(20261022), "fetch", "table_pick_fetch/scene0001.yaml")
+        return
+    if "--sql2s" in sys.argv:
+        make_sql2s_pins(np.random.default_rng(20261101))
+        print("ref_pins_sql2s.npz")
         return
     if "--attach-ur5" in sys.argv:
         make_attach_robot(np.random.default_rng(20261023), "ur5", "table_pick_ur5/scene0001.yaml")
