@@ -319,6 +319,14 @@ int vgpu_cpu_rrtc(const vgpu_robot *robot, vgpu_env *env, const float *start, co
                   const vgpu_rrtc_settings *settings, uint64_t *rng_index, float *path, size_t path_cap,
                   vgpu_plan_result *result);
 
+/* build_roadmap's neighbour queries on the host CPU (the reference's nigh KD-tree role, planning/nn.hh:89-95;
+ * mr-vamp_amd/csrc/cpu/vcpu_roadmap.cpp): an exact static k-d tree over V[n][dim] with per-subtree minimum
+ * vertex indices, answering the causal query of each listed vertex q = queries[j] (the k[q] nearest of
+ * vertices 0 .. q-1 within r[q], Space::distance in the AVX lane order) -- the same lists as
+ * vgpu_roadmap_knn.  Rows j of nbr/dist [m][kmax] and cnt[m].  threads <= 0: every hardware thread. */
+int vgpu_cpu_roadmap_knn(int dim, const float *V, size_t n, const uint32_t *queries, size_t m, const uint32_t *k,
+                         const float *r, uint32_t kmax, uint32_t *nbr, float *dist, uint32_t *cnt, int threads);
+
 /* FloatVector<dim>::l2_norm (vector/interface.hh:402-410): squares summed in the AVX hsum lane order
  * (avx.hh:441-452; above 8 lanes the two registers first as fma(lo, lo, hi * hi), pinned by ref_probe
  * "l2norm"), then std::sqrt.  dim <= 16.  The distance of every planner and NN (nn.hh:53-57). */
@@ -358,6 +366,46 @@ int vgpu_halton_host(vgpu_ctx *ctx, int dim, uint64_t first, size_t n, float *ou
 int vgpu_sample_fkcc_host(vgpu_ctx *ctx, const vgpu_robot *robot, vgpu_env *env, uint64_t first, size_t n, float *q,
                           uint8_t *valid);
 int vgpu_robot_info(int32_t kind, int32_t *dimension, int32_t *resolution, int32_t *n_spheres);
+
+/* ---- multi-GPU at the C level (mr-vamp_amd/csrc/vgpu_multi.cpp) ----------------------- */
+/* Contiguous shard [*first, *first + *count) of n units owned by `rank` of `world` (balanced: sizes differ
+ * by at most one).  The split of edges, configurations and Halton draws over devices or ranks. */
+int vgpu_shard_range(size_t n, int rank, int world, size_t *first, size_t *count);
+/* One process, several devices: one context per device (devices[n]), one host thread per device per call.
+ * vgpu_multi_env_create realises a (host-only or any) environment on every device: envs[vgpu_multi_size]
+ * (destroy each with vgpu_env_destroy before vgpu_multi_destroy). */
+typedef struct vgpu_multi vgpu_multi;
+int vgpu_multi_create(const int *devices, int n, vgpu_multi **out);
+void vgpu_multi_destroy(vgpu_multi *m);
+int vgpu_multi_size(const vgpu_multi *m);
+vgpu_ctx *vgpu_multi_context(vgpu_multi *m, int i);
+const char *vgpu_multi_last_error(const vgpu_multi *m);
+int vgpu_multi_env_create(vgpu_multi *m, const vgpu_env *src, vgpu_env **envs);
+/* validate_motion of n edges (host arrays), contiguous ranges per device, results in place */
+int vgpu_multi_validate_motions_host(vgpu_multi *m, const vgpu_robot *robot, vgpu_env *const *envs,
+                                     const float *starts, const float *goals, size_t n, uint8_t *ok,
+                                     int32_t *n_blocks);
+/* the PRM vertex stage (prm.hh:235-254) over the devices: the valid draws of first .. first + n_draws - 1
+ * in draw order, rows_out[*count][dim] and their 1-based draw indices (capacity n_draws each) */
+int vgpu_multi_sample_fkcc_host(vgpu_multi *m, const vgpu_robot *robot, vgpu_env *const *envs, uint64_t first,
+                                size_t n_draws, float *rows_out, uint64_t *draws_out, size_t *count);
+/* One process per GPU: RCCL communicators (librccl.so.1 loaded at run time; VGPU_ERR_UNSUPPORTED without
+ * it).  Rank 0 makes the 128-byte id, the caller ships it to the other ranks (any side channel), every
+ * rank calls vgpu_comm_init with its own context current. */
+typedef struct vgpu_comm vgpu_comm;
+int vgpu_comm_unique_id(uint8_t id[128]);
+int vgpu_comm_init(vgpu_ctx *ctx, int rank, int world, const uint8_t id[128], vgpu_comm **out);
+void vgpu_comm_destroy(vgpu_comm *comm);
+/* The PRM vertex stage of BASELINE configs[3] sharded over the ranks with ONE exchange: this rank's
+ * contiguous share of draws first .. first + n_draws_total - 1 through the fused sampler + fkcc +
+ * compaction, then an all-gather of the counts and of the count-padded rows and draw indices.  rows[cap][dim]
+ * and draws[cap] (device) receive every rank's valid vertices in rank order = draw order, the vertex
+ * sequence of build_roadmap after its start and goal; *count alike on every rank. */
+int vgpu_prm_vertices_allgather(vgpu_ctx *ctx, vgpu_comm *comm, const vgpu_robot *robot, vgpu_env *env,
+                                uint64_t first, size_t n_draws_total, float *rows, uint64_t *draws, size_t cap,
+                                size_t *count);
+/* a deep copy of an environment bound to ctx (NULL: host-only) */
+int vgpu_env_clone(const vgpu_env *src, vgpu_ctx *ctx, vgpu_env **out);
 
 #ifdef __cplusplus
 }

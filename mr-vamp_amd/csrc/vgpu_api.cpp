@@ -51,8 +51,8 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
     size_t vgpu_##NAME##_staged_plan_bytes(void);                                                                    \
     uint32_t vgpu_##NAME##_staged_blocks(int kind, uint32_t n_groups);                                               \
     hipError_t vgpu_##NAME##_staged_bound(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
-                                          uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by, \
-                                          float bz, void* mask, uint8_t* valid, hipStream_t st);                     \
+                                          uint64_t first, uint32_t n_groups, const EnvView* env, const float* bases, \
+                                          int chain, void* mask, uint8_t* valid, hipStream_t st);                    \
     hipError_t vgpu_##NAME##_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \
                                           uint32_t* counts, hipStream_t st);                                         \
@@ -64,11 +64,24 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
                                           hipStream_t st);                                                           \
     hipError_t vgpu_##NAME##_staged_children(int kind, const void* s0, const void* s1, const void* s2,               \
                                              const void* s3, uint64_t first, const void* plan, const uint32_t* ub,   \
-                                             const uint32_t* items, const EnvView* env, float bx, float by,          \
-                                             float bz, uint8_t* valid, hipStream_t st);
+                                             const uint32_t* items, const EnvView* env, const float* bases,          \
+                                             uint8_t* valid, hipStream_t st);
 VGPU_STAGED_DECL(panda)
 VGPU_STAGED_DECL(fetch)
 VGPU_STAGED_DECL(ur5)
+VGPU_STAGED_DECL(pair_a)
+VGPU_STAGED_DECL(pair_b)
+VGPU_STAGED_DECL(pair_i0)
+VGPU_STAGED_DECL(pair_i1)
+VGPU_STAGED_DECL(baxter_c0)
+VGPU_STAGED_DECL(baxter_c1)
+VGPU_STAGED_DECL(baxter_c2)
+VGPU_STAGED_DECL(baxter_c3)
+VGPU_STAGED_DECL(baxter_c4)
+VGPU_STAGED_DECL(baxter_c5)
+VGPU_STAGED_DECL(baxter_c6)
+hipError_t vgpu_launch_pair_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
+                                        int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
 const RobotOps* vgpu_ur5_ops(void);
 const RobotOps* vgpu_baxter_ops(void);
 hipError_t vgpu_launch_fetch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
@@ -642,6 +655,29 @@ extern "C" int vgpu_env_add_pointcloud_device(vgpu_ctx* c, vgpu_env* e, const fl
     return VGPU_OK;
 }
 
+// A deep copy of src's obstacles, point clouds and attachment bound to context c (or host-only for NULL):
+// the per-device environments of a multi-device batch (vgpu_multi.cpp)
+extern "C" int vgpu_env_clone(const vgpu_env* src, vgpu_ctx* c, vgpu_env** out)
+{
+    if (!src || !out) return VGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    auto* e = new (std::nothrow) vgpu_env();
+    if (!e) return fail(c, VGPU_ERR_OOM, "out of host memory");
+    e->ctx = c;
+    e->spheres = src->spheres;
+    e->capsules = src->capsules;
+    e->zcapsules = src->zcapsules;
+    e->cuboids = src->cuboids;
+    e->zcuboids = src->zcuboids;
+    e->heightfields = src->heightfields;
+    e->pointclouds = src->pointclouds;
+    e->attached = src->attached;
+    e->att_tf = src->att_tf;
+    e->att_spheres = src->att_spheres;
+    *out = e;
+    return VGPU_OK;
+}
+
 extern "C" int vgpu_env_copy_pointcloud(vgpu_env* dst, const vgpu_env* src, int index)
 {
     if (!dst || !src || index < 0 || (size_t)index >= src->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
@@ -870,6 +906,10 @@ static EnvView make_view(const vgpu_env* e)
     v.n_pc = (int)e->pointclouds.size();
     v.att = (const VGPU_CONST float*)(e->dev + e->att_off);
     v.n_att = e->attached ? (int)e->att_spheres.size() : 0;
+    // the five obstacle sections are contiguous in the blob (records + sentinels, 16-float aligned)
+    v.obs_floats = (int)(e->off[OBS_ZCUBOID] + (size_t)(e->cnt[OBS_ZCUBOID] + kObsPad) * kObsStride[OBS_ZCUBOID] -
+                         e->off[OBS_SPHERE]);
+    v.obs_lds = 0;
     return v;
 }
 
@@ -982,14 +1022,14 @@ struct StagedOps {
     size_t (*plan_bytes)(void);
     uint32_t (*blocks)(int, uint32_t);
     hipError_t (*bound)(int, const void*, const void*, const void*, const void*, uint64_t, uint32_t, const EnvView*,
-                        float, float, float, void*, uint8_t*, hipStream_t);
+                        const float*, int, void*, uint8_t*, hipStream_t);
     hipError_t (*count)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
                         const uint8_t*, uint32_t*, hipStream_t);
     hipError_t (*plan)(const uint32_t*, uint32_t, uint32_t, uint64_t, void*, hipStream_t);
     hipError_t (*queue)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
                         const void*, const uint8_t*, const uint32_t*, uint32_t*, hipStream_t);
     hipError_t (*children)(int, const void*, const void*, const void*, const void*, uint64_t, const void*,
-                           const uint32_t*, const uint32_t*, const EnvView*, float, float, float, uint8_t*, hipStream_t);
+                           const uint32_t*, const uint32_t*, const EnvView*, const float*, uint8_t*, hipStream_t);
 };
 #define VGPU_STAGED_OPS(NAME)                                                                                        \
     StagedOps                                                                                                        \
@@ -1002,6 +1042,9 @@ struct StagedOps {
 static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda);
 static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch);
 static const StagedOps kUr5Staged = VGPU_STAGED_OPS(ur5);
+// the two-Panda composite: four chained passes (vgpu_pair_staged.hip) -- arm A, arm B, inter-arm chunks
+static const StagedOps kPairStaged[4] = {VGPU_STAGED_OPS(pair_a), VGPU_STAGED_OPS(pair_b), VGPU_STAGED_OPS(pair_i0),
+                                         VGPU_STAGED_OPS(pair_i1)};
 
 // robots built from vgpu_robot.hh (one TU each): their launch table, or NULL
 static const RobotOps* generic_ops(int32_t kind)
@@ -1012,7 +1055,23 @@ static const RobotOps* generic_ops(int32_t kind)
     default: return nullptr;
     }
 }
-static const StagedOps* generic_staged(int32_t kind) { return kind == VGPU_ROBOT_UR5 ? &kUr5Staged : nullptr; }
+// the Baxter: its 388 checks in 7 chained chunks of <= 64 (vgpu_baxter_staged.hip)
+static const StagedOps kBaxterStaged[7] = {VGPU_STAGED_OPS(baxter_c0), VGPU_STAGED_OPS(baxter_c1),
+                                           VGPU_STAGED_OPS(baxter_c2), VGPU_STAGED_OPS(baxter_c3),
+                                           VGPU_STAGED_OPS(baxter_c4), VGPU_STAGED_OPS(baxter_c5),
+                                           VGPU_STAGED_OPS(baxter_c6)};
+// A robot's staged pipeline: one pass, or several chained passes over the same groups (check lists
+// beyond one 64-bit mask, the composite's arms and inter-arm checks)
+struct StagedChain {
+    const StagedOps* ops;
+    int n;
+};
+static StagedChain generic_chain(int32_t kind)
+{
+    if (kind == VGPU_ROBOT_UR5) return {&kUr5Staged, 1};
+    if (kind == VGPU_ROBOT_BAXTER) return {kBaxterStaged, 7};
+    return {nullptr, 0};
+}
 
 // One staged pass (vgpu_staged.hh) over n groups:
 //   bound -> count(all checks) -> scan -> [read back the per-check counts: the pass's ONE sync]
@@ -1020,9 +1079,13 @@ static const StagedOps* generic_staged(int32_t kind) { return kind == VGPU_ROBOT
 // The first round's per-check counts bound every later round's (groups only ever become invalid),
 // so they size all item buffers and children grids; the exact per-round layout is computed on the
 // device (plan_kernel) and read there by queue and children.
+// b: the robot base (b[0..2]) -- and the composite's second arm (b[3..5]); chain != 0: a later pass
+// over the same groups (the flags are ANDed into, groups already invalid skip every stage)
 static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* s0, const void* s1, const void* s2,
-                       const void* s3, uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid)
+                       const void* s3, uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid,
+                       int chain = 0, const float* b2 = nullptr)
 {
+    const float bases[6] = {b[0], b[1], b[2], b2 ? b2[0] : 0.0f, b2 ? b2[1] : 0.0f, b2 ? b2[2] : 0.0f};
     if (n == 0) return VGPU_OK;
     if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many groups in one call (< 2^31)");
     const int checks = ops.checks();
@@ -1041,7 +1104,7 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
     void* plan = c->st_cnt + 2 * cells_al;
     void* tmp = c->st_cnt + 2 * cells_al + plan_words;
     HIPCHK(c, hipMemsetAsync(counts + cells, 0, sizeof(uint32_t), c->cur));
-    HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, b[0], b[1], b[2], c->st_mask, valid, c->cur));
+    HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, chain, c->st_mask, valid, c->cur));
     const uint64_t all = checks >= 64 ? ~0ull : ((1ull << checks) - 1ull);
     const uint64_t env_bits = ops.env_checks();
     // every check's fired groups (all groups valid here): segment boundaries offs[k * nb], k = 0..checks
@@ -1084,9 +1147,27 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
         first_round = false;
         HIPCHK(c, ops.plan(offs, (uint32_t)nb, W, set, plan, c->cur));
         HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, plan, valid, offs, c->st_items, c->cur));
-        HIPCHK(c, ops.children(kind, s0, s1, s2, s3, first, plan, ub, c->st_items, v, b[0], b[1], b[2], valid, c->cur));
+        HIPCHK(c, ops.children(kind, s0, s1, s2, s3, first, plan, ub, c->st_items, v, bases, valid, c->cur));
     }
     return VGPU_OK;
+}
+
+// Chained staged passes over the same groups: the first initialises the flags, the later ones only
+// clear them (a group already invalid skips every stage) -- the reference's result is an OR over checks.
+static int chain_pass(vgpu_ctx* c, const StagedChain& ch, int kind, const void* s0, const void* s1, const void* s2,
+                      const void* s3, uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid,
+                      const float* b2 = nullptr)
+{
+    for (int p = 0; p < ch.n; ++p)
+        if (int rc = staged_pass(c, ch.ops[p], kind, s0, s1, s2, s3, first, n, v, b, valid, p, b2)) return rc;
+    return VGPU_OK;
+}
+
+// The composite's validity fkcc_A && fkcc_B && !inter (vgpu_pair_staged.hip): arm A, arm B, inter-arm chunks
+static int pair_staged(vgpu_ctx* c, int kind, const void* s0, const void* s1, const void* s2, const void* s3, size_t n,
+                       const EnvView* v, const float pb[6], uint8_t* valid)
+{
+    return chain_pass(c, StagedChain{kPairStaged, 4}, kind, s0, s1, s2, s3, 0, n, v, pb, valid, pb + 3);
 }
 
 extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n, uint8_t* valid)
@@ -1101,7 +1182,7 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     HIPCHK(c, hipSetDevice(c->device));
     if (const RobotOps* g = generic_ops(r->kind)) {
         if (c->staged && g->staged)
-            return staged_pass(c, *generic_staged(r->kind), 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
+            return chain_pass(c, generic_chain(r->kind), 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
         HIPCHK(c, g->fkcc(q, n, &v, valid, c->cur));
         return VGPU_OK;
     }
@@ -1113,6 +1194,7 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     if (r->kind == VGPU_ROBOT_PANDA_PAIR) {
         float pb[6];
         pair_bases(r, pb);
+        if (c->staged) return pair_staged(c, 0, q, nullptr, nullptr, nullptr, n, &v, pb, valid);
         HIPCHK(c, vgpu_launch_pair_fkcc(q, n, &v, pb, valid, c->cur));
         return VGPU_OK;
     }
@@ -1207,12 +1289,13 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     void* tmp;
     size_t tmp_bytes;
     if ((rc = ensure_ws(c, n_edges, &cnt, &off, &tmp, &tmp_bytes))) return rc;
-    const bool pair = r->kind == VGPU_ROBOT_PANDA_PAIR;  // monolithic head/tail kernels
+    const bool pair_staged_path = r->kind == VGPU_ROBOT_PANDA_PAIR && c->staged;  // chained staged passes
+    const bool pair = r->kind == VGPU_ROBOT_PANDA_PAIR && !c->staged;             // monolithic head/tail kernels
     const bool fetch = r->kind == VGPU_ROBOT_FETCH && !c->staged;
     const RobotOps* g = generic_ops(r->kind);
     const bool g_mono = g && !(c->staged && g->staged);
-    const StagedOps& ops = g ? (g->staged ? *generic_staged(r->kind) : kPandaStaged)
-                             : (r->kind == VGPU_ROBOT_FETCH ? kFetchStaged : kPandaStaged);
+    const StagedChain chain = g ? (g->staged ? generic_chain(r->kind) : StagedChain{&kPandaStaged, 1})
+                                : StagedChain{r->kind == VGPU_ROBOT_FETCH ? &kFetchStaged : &kPandaStaged, 1};
     float pb[6];
     pair_bases(r, pb);
     if (c->prof) HIPCHK(c, hipEventRecord(c->ev[0], c->cur));
@@ -1226,12 +1309,15 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
                                                           cnt, c->cur));
     } else if (g_mono) {
         HIPCHK(c, g->validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
+    } else if (pair_staged_path) {
+        if ((rc = pair_staged(c, 2, starts, goals, nullptr, nullptr, n_edges, &v, pb, ok))) return rc;
+        HIPCHK(c, vgpu_launch_pair_tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
     } else if (pair) {
         HIPCHK(c, vgpu_launch_pair_validate_head(starts, goals, n_edges, &v, pb, ok, n_blocks, cnt, c->cur));
     } else if (fetch) {
         HIPCHK(c, vgpu_launch_fetch_validate_head(starts, goals, n_edges, &v, ok, n_blocks, cnt, c->cur));
     } else if (c->staged) {
-        if ((rc = staged_pass(c, ops, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
+        if ((rc = chain_pass(c, chain, 2, starts, goals, nullptr, nullptr, 0, n_edges, &v, b, ok))) return rc;
         if (g)
             HIPCHK(c, g->tail_counts(starts, goals, n_edges, ok, n_blocks, cnt, c->cur));
         else if (r->kind == VGPU_ROBOT_FETCH)
@@ -1265,10 +1351,15 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
             else
                 HIPCHK(c, vgpu_launch_fetch_validate_tail(starts, goals, n_items, &v, ok, off, c->items, c->cur));
         }
+    } else if (pair_staged_path) {
+        if (n_items) {
+            HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
+            if ((rc = pair_staged(c, 3, starts, goals, c->items, off, n_items, &v, pb, ok))) return rc;
+        }
     } else if (c->staged) {
         if (n_items) {
             HIPCHK(c, vgpu_launch_scatter_items(cnt, off, n_edges, c->items, c->cur));
-            if ((rc = staged_pass(c, ops, 3, starts, goals, c->items, off, 0, n_items, &v, b, ok))) return rc;
+            if ((rc = chain_pass(c, chain, 3, starts, goals, c->items, off, 0, n_items, &v, b, ok))) return rc;
         }
     } else {
         HIPCHK(c, vgpu_launch_panda_validate_tail(starts, goals, n_edges, n_items, &v, b[0], b[1], b[2], ok, cnt,
@@ -1465,7 +1556,7 @@ extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, u
     }
     if (const RobotOps* g = generic_ops(r->kind)) {
         if (c->staged && g->staged)
-            return staged_pass(c, *generic_staged(r->kind), 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
+            return chain_pass(c, generic_chain(r->kind), 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
         HIPCHK(c, g->sample_fkcc(first, n, &v, q, valid, c->cur));
         return VGPU_OK;
     }

@@ -1,6 +1,7 @@
 // vgpu_baxter.hip -- Baxter (robots/baxter.hh: 14-dof dual arm, 75 spheres, 33 link checks incl.
 // 8 leaves + 355 self link pairs of baxter/fk.hh, resolution 64) through the generic robot kernels
-// (vgpu_robot.hh).  388 checks exceed the staged pipeline's 64-bit masks: monolithic kernels only.
+// (vgpu_robot.hh) -- the monolithic kernels (VAMP_AMD_STAGED=0); the staged pipeline runs the 388 checks
+// in 7 chained chunks (vgpu_baxter_staged.hip).
 // Its validate_motion distance is the two-register FloatVector<14>::l2_norm (ref_probe "l2norm").
 #include <utility>
 
@@ -41,4 +42,4 @@ struct BaxterR {
 
 }  // namespace vgpu
 
-VGPU_ROBOT_EXPORTS(vgpu::BaxterR, baxter, false)
+VGPU_ROBOT_EXPORTS(vgpu::BaxterR, baxter, true)  // staged: vgpu_baxter_staged.hip

@@ -40,6 +40,7 @@ __device__ __forceinline__ uint32_t umax(uint32_t a, uint32_t b) { return a > b 
 
 struct Grp1 {
     static constexpr int G = 1;
+    __device__ static __forceinline__ uint32_t or_bits(uint32_t b) { return b; }
     __device__ static __forceinline__ bool any(bool p) { return p; }
     __device__ static __forceinline__ bool any_bits(uint32_t b) { return (b >> 31) != 0u; }
     __device__ static __forceinline__ float max(float v) { return v; }
@@ -47,6 +48,15 @@ struct Grp1 {
 
 struct Grp8 {
     static constexpr int G = 8;
+    // OR of a small bit mask over the group's 8 lanes
+    __device__ static __forceinline__ uint32_t or_bits(uint32_t b)
+    {
+        int x = (int)b;
+        x |= dpp_i<0xB1>(x);
+        x |= dpp_i<0x4E>(x);
+        x |= dpp_i<0x141>(x);
+        return (uint32_t)x;
+    }
     // any lane of the group with its sign bit set (bits OR-reduced over the DPP half-row)
     __device__ static __forceinline__ bool any_bits(uint32_t b)
     {
@@ -176,6 +186,10 @@ struct EnvView {
     // levels of the first point cloud's split tree staged in this workgroup's LDS by
     // capt_stage_lds (0: none -- the host-built view, and kernels that do not stage)
     int pc_lds_levels;
+    // floats of the five obstacle sections (obs[0] .. end of obs[4], contiguous in the blob): what
+    // the VGPU_ENV_LDS variant copies into LDS per workgroup (env_stage_lds); 0 = not staged
+    int obs_floats;
+    int obs_lds;
 };
 constexpr int kAttHdr = 8;
 constexpr int kExtHdr = 16;
@@ -184,6 +198,12 @@ enum : int { HF_X = 0, HF_Y, HF_Z, HF_XS, HF_YS, HF_ZS, HF_XD, HF_YD, HF_XD2, HF
 // point-cloud (CAPT) header: top lower xyz, top upper xyz, r_point | nlog2, tests_off, aabbs_off,
 // starts_off, aff_off (uint32 bits).  aff = [n_aff][3][8] floats (x8 y8 z8), 16-B aligned.
 enum : int { PC_TOP = 0, PC_RPOINT = 6, PC_NLOG2 = 7, PC_TESTS, PC_AABBS, PC_STARTS, PC_AFF };
+
+// Robot base offsets of a staged pass (robots/panda/fk.hh:109-111, added to world-frame centres):
+// x y z of the robot -- and of the second arm, for the two-Panda composite's inter-arm checks
+struct Bases {
+    float x, y, z, x2, y2, z2;
+};
 
 __device__ __forceinline__ bool signbit_f(float v) { return (__float_as_uint(v) >> 31) != 0u; }
 
@@ -246,8 +266,22 @@ template <int S>
 struct ObsRec {
     float v[S];
 };
-template <int TYPE, class TestFn>
-__device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float emax, uint32_t acc, TestFn test)
+// obstacle records are read through the scalar cache (address space 4, s_load) -- or, in the
+// VGPU_ENV_LDS A/B variant, from a per-workgroup LDS copy (address space 3, ds_read broadcast)
+#define VGPU_LDS_AS __attribute__((address_space(3)))
+template <int AS, class T>
+struct ObsPtr;
+template <class T>
+struct ObsPtr<4, T> {
+    using type = const VGPU_CONST T*;
+};
+template <class T>
+struct ObsPtr<3, T> {
+    using type = const VGPU_LDS_AS T*;
+};
+template <int TYPE, int AS = 4, class TestFn>
+__device__ __forceinline__ uint32_t scan_type(typename ObsPtr<AS, float>::type o, float emax, uint32_t acc,
+                                              TestFn test)
 {
     // The lane state is kept as VALU bit masks (acc: sign bit = hit) instead of per-lane bools:
     // combining divergent bools costs a 64-bit SALU op each, and the scalar unit -- shared by
@@ -255,7 +289,7 @@ __device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float e
     constexpr int S = kObsStride[TYPE];
     constexpr int U = VGPU_SCAN_UNROLL;
     using Rec = ObsRec<S>;  // one record: a single s_load per field group
-    const VGPU_CONST Rec* p = (const VGPU_CONST Rec*)o;
+    typename ObsPtr<AS, Rec>::type p = (typename ObsPtr<AS, Rec>::type)o;
     float md[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) md[u] = p[u].v[0];
@@ -398,6 +432,45 @@ __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float
     return false;
 }
 
+#ifndef VGPU_ENV_LDS_FLOATS
+#define VGPU_ENV_LDS_FLOATS 4096
+#endif
+#ifdef VGPU_ENV_LDS
+__device__ __forceinline__ float* env_lds()
+{
+    __shared__ float e[VGPU_ENV_LDS_FLOATS];  // one per workgroup of every kernel that stages
+    return e;
+}
+#endif
+// VGPU_ENV_LDS variant: every thread of the workgroup copies the obstacle sections into LDS (ends in
+// a barrier; call before any return).  Environments larger than the LDS copy keep the scalar path.
+__device__ __forceinline__ void env_stage_lds(EnvView& env)
+{
+#ifdef VGPU_ENV_LDS
+    env.obs_lds = env.obs_floats > 0 && env.obs_floats <= VGPU_ENV_LDS_FLOATS;
+    if (env.obs_lds) {
+        float* e = env_lds();
+        const VGPU_CONST float* src = env.obs[0];
+        for (int i = threadIdx.x; i < env.obs_floats; i += blockDim.x) e[i] = src[i];
+    }
+    __syncthreads();
+#else
+    (void)env;
+#endif
+}
+
+template <int TYPE, class TestFn>
+__device__ __forceinline__ uint32_t scan_env_type(const EnvView& env, float emax, uint32_t acc, TestFn test)
+{
+#ifdef VGPU_ENV_LDS
+    if (env.obs_lds) {
+        const VGPU_LDS_AS float* base = (const VGPU_LDS_AS float*)env_lds();
+        return scan_type<TYPE, 3>(base + (env.obs[TYPE] - env.obs[0]), emax, acc, test);
+    }
+#endif
+    return scan_type<TYPE>(env.obs[TYPE], emax, acc, test);
+}
+
 // Returns acc with this lane's hits OR-ed into the sign bit.  A lane entering with its sign
 // bit already set (an earlier child hit) does not keep any obstacle loop alive.
 template <class Grp, bool EXT = false>
@@ -411,11 +484,11 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
     const float rsq = r * r;
 
     if (env.n[OBS_SPHERE])  // sphere_sphere.hh:10-22
-        acc = scan_type<OBS_SPHERE>(env.obs[OBS_SPHERE], emax, acc, [&](const auto* o) {
+        acc = scan_env_type<OBS_SPHERE>(env, emax, acc, [&](const auto* o) {
             return sphere_sphere(o[1], o[2], o[3], o[4], x, y, z, r);
         });
     if (env.n[OBS_CAPSULE])  // sphere_capsule.hh:9-22
-        acc = scan_type<OBS_CAPSULE>(env.obs[OBS_CAPSULE], emax, acc, [&](const auto* o) {
+        acc = scan_env_type<OBS_CAPSULE>(env, emax, acc, [&](const auto* o) {
             const float dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
             const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
             const float px = __builtin_fmaf(o[4], cdf, o[1]);
@@ -426,7 +499,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
         });
     if (env.n[OBS_ZCAPSULE])  // sphere_capsule.hh:30-43
-        acc = scan_type<OBS_ZCAPSULE>(env.obs[OBS_ZCAPSULE], emax, acc, [&](const auto* o) {
+        acc = scan_env_type<OBS_ZCAPSULE>(env, emax, acc, [&](const auto* o) {
             const float dot = (z - o[3]) * o[6];
             const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
             const float pz = __builtin_fmaf(o[6], cdf, o[3]);
@@ -435,7 +508,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
         });
     if (env.n[OBS_CUBOID])  // sphere_cuboid.hh:9-27
-        acc = scan_type<OBS_CUBOID>(env.obs[OBS_CUBOID], emax, acc, [&](const auto* o) {
+        acc = scan_env_type<OBS_CUBOID>(env, emax, acc, [&](const auto* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
             const float a1 = max0(__builtin_fabsf(dot3(o[4], o[5], o[6], xs, ys, zs)) - o[13]);
             const float a2 = max0(__builtin_fabsf(dot3(o[7], o[8], o[9], xs, ys, zs)) - o[14]);
@@ -443,7 +516,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
         });
     if (env.n[OBS_ZCUBOID])  // sphere_cuboid.hh:35-52
-        acc = scan_type<OBS_ZCUBOID>(env.obs[OBS_ZCUBOID], emax, acc, [&](const auto* o) {
+        acc = scan_env_type<OBS_ZCUBOID>(env, emax, acc, [&](const auto* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
             const float a1 = max0(__builtin_fabsf(dot2(o[4], o[5], xs, ys)) - o[13]);
             const float a2 = max0(__builtin_fabsf(dot2(o[7], o[8], xs, ys)) - o[14]);

@@ -50,12 +50,12 @@ struct FetchR {
         rake_block_d<8>(s, rk, lane, k, v);
     }
     template <class Grp, bool EXT>
-    __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, float, float, float)
+    __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, const Bases&)
     {
         return fetch_bound_mask<Grp, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], env, 0.0f, 0.0f, 0.0f);
     }
     template <class Grp, bool EXT>
-    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, float, float, float)
+    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, const Bases&)
     {
         return fetch_children<Grp, EXT>(c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], env, 0.0f, 0.0f, 0.0f);
     }

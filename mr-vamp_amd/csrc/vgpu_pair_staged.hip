@@ -1,0 +1,152 @@
+// vgpu_pair_staged.hip -- the two-Panda composite of BASELINE configs[4] through the staged pipeline
+// (vgpu_staged.hh).  Validity = fkcc_A && fkcc_B && !inter(A, B) (oracle/vamp_oracle.c
+// vo_pair_fkcc_block), an AND of three ORs over checks, so it runs as CHAINED staged passes over the
+// same groups, each with its own bound -> count -> queue -> children stages and <= 64 checks:
+//   pair_a    arm A's 32 Panda checks (panda/fk.hh:1335-6276) on joints 0..6 at base A
+//   pair_b    arm B's 32 checks on joints 7..13 at base B (groups invalid after pair_a skip)
+//   pair_i0   inter-arm link-bounding pairs 0..63 (gen/panda_pair_staged.inc, link-major order)
+//   pair_i1   inter-arm pairs 64..120
+// Every pass recomputes the frames it needs (lazily: a pass only evaluates its own links).  The
+// 14-dof rake (two AVX registers, pinned l2_norm) feeds the head and tail sources.
+#include "vgpu_rake.hh"
+#include "vgpu_staged.hh"
+
+#include "gen/panda_fk.inc"
+#include "gen/panda_pair_staged.inc"
+
+#ifndef VGPU_PAIR_BOUND_WAVES
+#define VGPU_PAIR_BOUND_WAVES 5
+#endif
+#ifndef VGPU_PAIR_INTER_WAVES
+#define VGPU_PAIR_INTER_WAVES 6
+#endif
+
+namespace vgpu {
+
+constexpr int kPairDimS = 14;
+constexpr int kPairResS = 32;  // robots/panda_base.hh:21
+
+struct PairRakeR {  // the composite's rake blocks (validate.hh:23-56 over 14 dof)
+    static constexpr int D = kPairDimS;
+    static constexpr unsigned kSourceKinds = 1u | 4u | 8u;  // configurations, validate head, validate tail
+    __device__ static __forceinline__ void sample(uint64_t, float v[D])
+    {
+#pragma unroll
+        for (int j = 0; j < D; ++j) v[j] = 0.0f;  // never instantiated (kSourceKinds)
+    }
+    __device__ static __forceinline__ void head(const float* s, const float* g, int lane, float v[D])
+    {
+        const RakeD<D> rk = rake_setup_d<D, kPairResS>(s, g);
+        rake_block_d<D>(s, rk, lane, 0, v);
+    }
+    __device__ static __forceinline__ void tail(const float* s, const float* g, int lane, int k, float v[D])
+    {
+        const RakeD<D> rk = rake_setup_d<D, kPairResS>(s, g);
+        rake_block_d<D>(s, rk, lane, k, v);
+    }
+};
+
+// one arm's Panda hierarchy; ARM 0 = joints 0..6 at (x, y, z), ARM 1 = joints 7..13 at (x2, y2, z2)
+template <int ARM>
+struct PairArmR : PairRakeR {
+    static constexpr int kChecks = panda_n_checks;
+    static constexpr int kWavesPerEU = VGPU_PAIR_BOUND_WAVES;
+    static constexpr int kChildWavesPerEU = 7;
+    using Mask = panda_mask_t;
+    static constexpr Mask kEnvChecks = panda_env_check_bits;
+    // the Panda's children register classes (vgpu_staged.hip PandaR)
+    static constexpr int kClasses = 3;
+    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 0, 0, 2,
+                                              0, 0, 0, 1, 1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    static constexpr int kClassWaves[kClasses] = {8, 7, 6};
+    template <class Grp, bool EXT>
+    __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, const Bases& b)
+    {
+        constexpr int o = 7 * ARM;
+        return ARM == 0 ? panda_bound_mask<Grp, EXT>(v[o], v[o + 1], v[o + 2], v[o + 3], v[o + 4], v[o + 5], v[o + 6],
+                                                      env, b.x, b.y, b.z)
+                        : panda_bound_mask<Grp, EXT>(v[o], v[o + 1], v[o + 2], v[o + 3], v[o + 4], v[o + 5], v[o + 6],
+                                                      env, b.x2, b.y2, b.z2);
+    }
+    template <class Grp, bool EXT>
+    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, const Bases& b)
+    {
+        constexpr int o = 7 * ARM;
+        return ARM == 0 ? panda_children<Grp, EXT>(c, v[o], v[o + 1], v[o + 2], v[o + 3], v[o + 4], v[o + 5],
+                                                   v[o + 6], env, b.x, b.y, b.z)
+                        : panda_children<Grp, EXT>(c, v[o], v[o + 1], v[o + 2], v[o + 3], v[o + 4], v[o + 5],
+                                                   v[o + 6], env, b.x2, b.y2, b.z2);
+    }
+};
+
+#define PAIR_Q(v) v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], v[8], v[9], v[10], v[11], v[12], v[13]
+
+// the inter-arm checks of one chunk K (checks 64K .. 64K + kChecks - 1); no environment checks
+template <int K>
+struct PairInterR : PairRakeR {
+    static constexpr int kFirst = K * panda_pair_chunk;
+    static constexpr int kChecks = (panda_pair_n_checks - kFirst) < panda_pair_chunk ? (panda_pair_n_checks - kFirst)
+                                                                                      : panda_pair_chunk;
+    static constexpr int kWavesPerEU = VGPU_PAIR_BOUND_WAVES;
+    static constexpr int kChildWavesPerEU = VGPU_PAIR_INTER_WAVES;
+    using Mask = uint64_t;
+    static constexpr Mask kEnvChecks = 0u;
+    template <class Grp, bool EXT>
+    __device__ static __forceinline__ Mask bound(const float* v, const EnvView&, const Bases& b)
+    {
+        if constexpr (K == 0)
+            return panda_pair_bound_mask_0<Grp>(PAIR_Q(v), b.x, b.y, b.z, b.x2, b.y2, b.z2);
+        else
+            return panda_pair_bound_mask_1<Grp>(PAIR_Q(v), b.x, b.y, b.z, b.x2, b.y2, b.z2);
+    }
+    template <class Grp, bool EXT>
+    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView&, const Bases& b)
+    {
+        return panda_pair_children<Grp>(kFirst + c, PAIR_Q(v), b.x, b.y, b.z, b.x2, b.y2, b.z2);
+    }
+};
+static_assert(panda_pair_n_checks <= 2 * panda_pair_chunk, "two inter-arm chunks");
+
+}  // namespace vgpu
+
+// one pass per object file (the Makefile compiles this TU once per VGPU_PAIR_PASS = 0..3, in parallel)
+#ifndef VGPU_PAIR_PASS
+#error "compile with -DVGPU_PAIR_PASS=<0..3>"
+#endif
+#if VGPU_PAIR_PASS == 0
+VGPU_STAGED_EXPORTS(vgpu::PairArmR<0>, pair_a)
+
+namespace vgpu {
+// validate head -> tail back-step counts of the 14-dof rake
+__global__ __launch_bounds__(kStagedBlock) void pair_tail_counts_kernel(const float* __restrict__ starts,
+                                                                        const float* __restrict__ goals,
+                                                                        size_t n_edges, const uint8_t* __restrict__ ok,
+                                                                        int32_t* __restrict__ n_blocks,
+                                                                        uint32_t* __restrict__ cnt)
+{
+    const size_t e = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
+    if (e >= n_edges) return;
+    const RakeD<kPairDimS> rk = rake_setup_d<kPairDimS, kPairResS>(starts + kPairDimS * e, goals + kPairDimS * e);
+    if (n_blocks) n_blocks[e] = rk.n;
+    cnt[e] = ((!ok || ok[e]) && rk.n > 1) ? (uint32_t)(rk.n - 1) : 0u;
+}
+
+}  // namespace vgpu
+
+extern "C" hipError_t vgpu_launch_pair_tail_counts(const float* starts, const float* goals, size_t n_edges,
+                                                   const uint8_t* ok, int32_t* n_blocks, uint32_t* cnt, hipStream_t st)
+{
+    hipError_t err = hipMemsetAsync(cnt + n_edges, 0, sizeof(uint32_t), st);
+    if (err != hipSuccess || n_edges == 0) return err;
+    const unsigned grid = (unsigned)((n_edges + vgpu::kStagedBlock - 1) / vgpu::kStagedBlock);
+    hipLaunchKernelGGL(vgpu::pair_tail_counts_kernel, dim3(grid), dim3(vgpu::kStagedBlock), 0, st, starts, goals,
+                       n_edges, ok, n_blocks, cnt);
+    return hipGetLastError();
+}
+#elif VGPU_PAIR_PASS == 1
+VGPU_STAGED_EXPORTS(vgpu::PairArmR<1>, pair_b)
+#elif VGPU_PAIR_PASS == 2
+VGPU_STAGED_EXPORTS(vgpu::PairInterR<0>, pair_i0)
+#else
+VGPU_STAGED_EXPORTS(vgpu::PairInterR<1>, pair_i1)
+#endif

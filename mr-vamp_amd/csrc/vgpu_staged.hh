@@ -23,7 +23,7 @@
 //
 // A robot R provides: D (dof), kChecks, Mask (uint32_t / uint64_t), kEnvChecks (mask of the
 // environment checks), sample(k, v), head(s, g, lane, v) and tail(s, g, lane, k, v) (the rake
-// blocks), bound<Grp, EXT>(v, env, bx, by, bz) -> Mask and children<Grp, EXT>(c, v, env, ...).
+// blocks), bound<Grp, EXT>(v, env, bases) -> Mask and children<Grp, EXT>(c, v, env, bases).
 // VGPU_STAGED_EXPORTS(R, name) emits the extern "C" launchers vgpu_<name>_staged_*.
 #pragma once
 
@@ -65,6 +65,18 @@ struct ChildClasses<R, std::void_t<decltype(R::kClassOf)>> {
     static constexpr int n = R::kClasses;
     __host__ __device__ static constexpr int of(int c) { return R::kClassOf[c]; }
     __host__ __device__ static constexpr int waves(int k) { return R::kClassWaves[k]; }
+};
+
+// Source kinds a robot's staged exports instantiate (bit k = kind k of StagedHost::with_source): all
+// by default; a robot may restrict them with R::kSourceKinds (the composite has no sampler and no
+// full-mask mode), which also cuts its compile time
+template <class R, class = void>
+struct SourceKinds {
+    static constexpr unsigned v = 0x1Fu;
+};
+template <class R>
+struct SourceKinds<R, std::void_t<decltype(R::kSourceKinds)>> {
+    static constexpr unsigned v = R::kSourceKinds;
 };
 
 // ---- group sources ----------------------------------------------------------------------------
@@ -208,16 +220,25 @@ __device__ __forceinline__ void block_counts(typename R::Mask m, uint32_t* __res
 // ---- stage 1: bounding masks ---------------------------------------------------------------
 template <class R, class Src, bool EXT>
 __global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
-                                                                             float bx, float by, float bz,
+                                                                             Bases bs, int chain,
                                                                              typename R::Mask* __restrict__ mask,
                                                                              uint8_t* __restrict__ valid)
 {
     using Grp = typename GrpOf<Src::G>::T;
     if constexpr (EXT) capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
+#ifdef VGPU_ENV_LDS
+    env_stage_lds(env);
+#endif
     const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
     const uint32_t g = (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);
     if (g >= n_groups) return;  // group-uniform
+    // a chained pass (a later pass over the same groups, e.g. the composite's arm B after arm A): a
+    // group already invalid is done -- its mask stays 0 -- and the flag is not re-initialised
+    if (chain && !valid[src.out(g)]) {
+        if (lane == 0) mask[g] = 0;
+        return;
+    }
     float v[R::D];
     src.load(g, lane, v);
     if constexpr (std::is_same<Src, SrcSamplesT<R>>::value) {
@@ -226,10 +247,12 @@ __global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void bound_kernel(Src
             for (int j = 0; j < R::D; ++j) src.q_out[R::D * (size_t)g + j] = v[j];
         }
     }
-    const typename R::Mask m = R::template bound<Grp, EXT>(v, env, bx, by, bz);
+    const typename R::Mask m = R::template bound<Grp, EXT>(v, env, bs);
     if (lane == 0) {
         mask[g] = m;
-        if constexpr (Src::kInit) valid[src.out(g)] = 1;
+        if constexpr (Src::kInit) {
+            if (!chain) valid[src.out(g)] = 1;
+        }
     }
 }
 
@@ -330,26 +353,29 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
 // plan); the generated switch folds to that one case, so the kernel's registers cover only its class.
 template <class R, int K, class Grp, bool EXT, int C = 0>
 __device__ __forceinline__ int children_of_class(uint32_t item0, const StagedPlan* __restrict__ plan, const float* v,
-                                                 const EnvView& env, float bx, float by, float bz)
+                                                 const EnvView& env, const Bases& bs)
 {
     if constexpr (C == R::kChecks) {
         return -1;
     } else {
         if constexpr (ChildClasses<R>::of(C) == K) {
             if (item0 >= plan->start[C] && item0 < plan->end[C])
-                return R::template children<Grp, EXT>(C, v, env, bx, by, bz) ? 1 : 0;
+                return R::template children<Grp, EXT>(C, v, env, bs) ? 1 : 0;
         }
-        return children_of_class<R, K, Grp, EXT, C + 1>(item0, plan, v, env, bx, by, bz);
+        return children_of_class<R, K, Grp, EXT, C + 1>(item0, plan, v, env, bs);
     }
 }
 
 template <class R, class Src, bool EXT, int K>
 __global__ __launch_bounds__(kStagedBlock, ChildClasses<R>::waves(K)) void children_kernel(
-    Src src, const StagedPlan* __restrict__ plan, const uint32_t* __restrict__ items, EnvView env, float bx, float by,
-    float bz, uint8_t* __restrict__ valid)
+    Src src, const StagedPlan* __restrict__ plan, const uint32_t* __restrict__ items, EnvView env, Bases bs,
+    uint8_t* __restrict__ valid)
 {
     using Grp = typename GrpOf<Src::G>::T;
     if constexpr (EXT) capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
+#ifdef VGPU_ENV_LDS
+    env_stage_lds(env);
+#endif
     const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
     const uint32_t item = plan->lo[K] + (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);
@@ -365,7 +391,7 @@ __global__ __launch_bounds__(kStagedBlock, ChildClasses<R>::waves(K)) void child
     const uint32_t g = items[item];
     float v[R::D];
     src.load(g, lane, v);
-    const bool hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bx, by, bz) > 0;
+    const bool hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bs) > 0;
     if (hit && lane == 0) valid[src.out(g)] = 0;  // every writer stores 0: the race is benign
 }
 
@@ -383,17 +409,17 @@ struct StagedHost {
     static unsigned group_blocks(uint32_t n_groups) { return (n_groups + kStagedBlock - 1) / kStagedBlock; }
 
     template <class Src>
-    static hipError_t bound(const Src& src, uint32_t n_groups, const EnvView* env, float bx, float by, float bz,
+    static hipError_t bound(const Src& src, uint32_t n_groups, const EnvView* env, const Bases& bs, int chain,
                             M* mask, uint8_t* valid, hipStream_t st)
     {
         if (n_groups == 0) return hipSuccess;
         const unsigned grid = grid_of<Src>(n_groups);
         if (env->n_hf > 0 || env->n_pc > 0)
             hipLaunchKernelGGL((bound_kernel<R, Src, true>), dim3(grid), dim3(kStagedBlock), 0, st, src, n_groups,
-                               *env, bx, by, bz, mask, valid);
+                               *env, bs, chain, mask, valid);
         else
             hipLaunchKernelGGL((bound_kernel<R, Src, false>), dim3(grid), dim3(kStagedBlock), 0, st, src, n_groups,
-                               *env, bx, by, bz, mask, valid);
+                               *env, bs, chain, mask, valid);
         return hipGetLastError();
     }
 
@@ -418,7 +444,7 @@ struct StagedHost {
     // one launch per class with items; ub[k] = upper bound of class k's item count this round
     template <class Src, bool EXT, int K = 0>
     static hipError_t children_classes(const Src& src, const StagedPlan* plan, const uint32_t* ub,
-                                       const uint32_t* items, const EnvView* env, float bx, float by, float bz,
+                                       const uint32_t* items, const EnvView* env, const Bases& bs,
                                        uint8_t* valid, hipStream_t st)
     {
         if constexpr (K == ChildClasses<R>::n) {
@@ -428,21 +454,21 @@ struct StagedHost {
             if (threads > 0) {
                 const unsigned grid = (unsigned)((threads + kStagedBlock - 1) / kStagedBlock);
                 hipLaunchKernelGGL((children_kernel<R, Src, EXT, K>), dim3(grid), dim3(kStagedBlock), 0, st, src,
-                                   plan, items, *env, bx, by, bz, valid);
+                                   plan, items, *env, bs, valid);
                 const hipError_t err = hipGetLastError();
                 if (err != hipSuccess) return err;
             }
-            return children_classes<Src, EXT, K + 1>(src, plan, ub, items, env, bx, by, bz, valid, st);
+            return children_classes<Src, EXT, K + 1>(src, plan, ub, items, env, bs, valid, st);
         }
     }
 
     template <class Src>
     static hipError_t children(const Src& src, const StagedPlan* plan, const uint32_t* ub, const uint32_t* items,
-                               const EnvView* env, float bx, float by, float bz, uint8_t* valid, hipStream_t st)
+                               const EnvView* env, const Bases& bs, uint8_t* valid, hipStream_t st)
     {
         if (env->n_hf > 0 || env->n_pc > 0)
-            return children_classes<Src, true>(src, plan, ub, items, env, bx, by, bz, valid, st);
-        return children_classes<Src, false>(src, plan, ub, items, env, bx, by, bz, valid, st);
+            return children_classes<Src, true>(src, plan, ub, items, env, bs, valid, st);
+        return children_classes<Src, false>(src, plan, ub, items, env, bs, valid, st);
     }
 
     static hipError_t plan(const uint32_t* offs, uint32_t nb, uint32_t W, M set, StagedPlan* plan, hipStream_t st)
@@ -458,17 +484,26 @@ struct StagedHost {
     static hipError_t with_source(int kind, const void* s0, const void* s1, const void* s2, const void* s3,
                                   uint64_t first, Fn fn)
     {
+        constexpr unsigned K = SourceKinds<R>::v;
         switch (kind) {
         case 0:
-            return fn(SrcConfigsT<R>{(const float*)s0});
+            if constexpr ((K & 1u) != 0) return fn(SrcConfigsT<R>{(const float*)s0});
+            break;
         case 1:
-            return fn(SrcSamplesT<R>{first, (float*)s0, nullptr});
+            if constexpr ((K & 2u) != 0) return fn(SrcSamplesT<R>{first, (float*)s0, nullptr});
+            break;
         case 2:
-            return fn(SrcHeadT<R>{(const float*)s0, (const float*)s1});
+            if constexpr ((K & 4u) != 0) return fn(SrcHeadT<R>{(const float*)s0, (const float*)s1});
+            break;
         case 3:
-            return fn(SrcTailT<R>{(const float*)s0, (const float*)s1, (const uint32_t*)s2, (const uint32_t*)s3});
+            if constexpr ((K & 8u) != 0)
+                return fn(SrcTailT<R>{(const float*)s0, (const float*)s1, (const uint32_t*)s2, (const uint32_t*)s3});
+            break;
         case 4:
-            return fn(SrcTailMaskT<R>{(const float*)s0, (const float*)s1, (const uint32_t*)s2, (const uint32_t*)s3});
+            if constexpr ((K & 16u) != 0)
+                return fn(SrcTailMaskT<R>{(const float*)s0, (const float*)s1, (const uint32_t*)s2,
+                                          (const uint32_t*)s3});
+            break;
         }
         return hipErrorInvalidValue;
     }
@@ -489,12 +524,13 @@ struct StagedHost {
         return vgpu::StagedHost<R>::group_blocks(n_groups); /* count / queue grid: one thread per group */          \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_bound(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
-                                          uint64_t first, uint32_t n_groups, const EnvView* env, float bx, float by, \
-                                          float bz, void* mask, uint8_t* valid, hipStream_t st)                      \
+                                          uint64_t first, uint32_t n_groups, const EnvView* env,                     \
+                                          const float* bases, int chain, void* mask, uint8_t* valid, hipStream_t st) \
     {                                                                                                                \
         using H = vgpu::StagedHost<R>;                                                                               \
+        const Bases bs{bases[0], bases[1], bases[2], bases[3], bases[4], bases[5]};                            \
         return H::with_source(kind, s0, s1, s2, s3, first, [&](auto src) {                                          \
-            return H::bound(src, n_groups, env, bx, by, bz, (typename R::Mask*)mask, valid, st);                     \
+            return H::bound(src, n_groups, env, bs, chain, (typename R::Mask*)mask, valid, st);                      \
         });                                                                                                          \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
@@ -526,16 +562,17 @@ struct StagedHost {
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_children(int kind, const void* s0, const void* s1, const void* s2,               \
                                              const void* s3, uint64_t first, const void* plan, const uint32_t* ub,   \
-                                             const uint32_t* items, const EnvView* env, float bx, float by,          \
-                                             float bz, uint8_t* valid, hipStream_t st)                               \
+                                             const uint32_t* items, const EnvView* env, const float* bases,          \
+                                             uint8_t* valid, hipStream_t st)                                         \
     {                                                                                                                \
         using H = vgpu::StagedHost<R>;                                                                               \
+        const Bases bs{bases[0], bases[1], bases[2], bases[3], bases[4], bases[5]};                            \
         return H::with_source(kind, s0, s1, s2, s3, first, [&](auto src) {                                          \
             if constexpr (std::is_same<decltype(src), vgpu::SrcSamplesT<R>>::value) {                                \
                 src.q_in = src.q_out; /* the samples the bound stage wrote */                                         \
                 src.q_out = nullptr;                                                                                 \
             }                                                                                                        \
-            return H::children(src, (const vgpu::StagedPlan*)plan, ub, items, env, bx, by, bz, valid, st);           \
+            return H::children(src, (const vgpu::StagedPlan*)plan, ub, items, env, bs, valid, st);                   \
         });                                                                                                          \
     }                                                                                                                \
     }

@@ -11,7 +11,8 @@
 #define VGPU_BOUND_WAVES_PER_EU 5
 #endif
 // children classes (A/B on MI355X, 2^20 cage edges): class 0 at 8 waves/EU 1.5-3 % faster than 7;
-// class 2 at 4 (112 VGPRs, no spill) as fast as 7 (spilling)
+// class 2 (checks 15, 21) at 6: 79 VGPRs since their children hold the link5 centres and stream the other
+// link's (tools/gen_kernels.py HOLD; 105 VGPRs at 4 waves/EU before, A/B 3.50 -> 3.44 ms)
 #ifndef VGPU_PANDA_CLASS0_WAVES
 #define VGPU_PANDA_CLASS0_WAVES 8
 #endif
@@ -19,7 +20,7 @@
 #define VGPU_PANDA_CLASS1_WAVES 7
 #endif
 #ifndef VGPU_PANDA_CLASS2_WAVES
-#define VGPU_PANDA_CLASS2_WAVES 4
+#define VGPU_PANDA_CLASS2_WAVES 6
 #endif
 
 namespace vgpu {
@@ -54,15 +55,14 @@ struct PandaR {
         rake_block(s, rk, lane, k, v);
     }
     template <class Grp, bool EXT>
-    __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, float bx, float by, float bz)
+    __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, const Bases& b)
     {
-        return panda_bound_mask<Grp, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, bx, by, bz);
+        return panda_bound_mask<Grp, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, b.x, b.y, b.z);
     }
     template <class Grp, bool EXT>
-    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, float bx, float by,
-                                                    float bz)
+    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, const Bases& b)
     {
-        return panda_children<Grp, EXT>(c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, bx, by, bz);
+        return panda_children<Grp, EXT>(c, v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, b.x, b.y, b.z);
     }
 };
 

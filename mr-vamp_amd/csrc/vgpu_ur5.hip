@@ -59,7 +59,7 @@ struct Ur5R {
         return ur5_bound_mask<Grp, EXT>(v[I]..., env, 0.0f, 0.0f, 0.0f);
     }
     template <class Grp, bool EXT>
-    __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, float, float, float)
+    __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, const Bases&)
     {
         return bound_<Grp, EXT>(v, env, std::make_index_sequence<D>{});
     }
@@ -70,7 +70,7 @@ struct Ur5R {
         return ur5_children<Grp, EXT>(c, v[I]..., env, 0.0f, 0.0f, 0.0f);
     }
     template <class Grp, bool EXT>
-    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, float, float, float)
+    __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, const Bases&)
     {
         return children_<Grp, EXT>(c, v, env, std::make_index_sequence<D>{});
     }

@@ -350,14 +350,16 @@ class Environment:
                                               out_ptr), ctx.h)
 
     def handle(self, ctx: Context) -> C.c_void_p:
-        if ctx.device in self._handles:
-            return self._handles[ctx.device]
+        """This environment realised on ctx (one device copy per context, rebuilt after a change)."""
+        key = ctx.h.value  # per context: two contexts may share a device
+        if key in self._handles:
+            return self._handles[key]
         lib = load()
         h = C.c_void_p()
         check(lib.vgpu_env_create(ctx.h, C.byref(h)), ctx.h)
         self._realise(lib, h, ctx.h)
         check(lib.vgpu_env_upload(h), ctx.h)
-        self._handles[ctx.device] = h
+        self._handles[key] = h
         return h
 
     def host_handle(self) -> C.c_void_p:

@@ -120,6 +120,25 @@ SIGNATURES = {
     "vgpu_cpu_validate_motions": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_size_t, U8P, I32P, I32P,
                                             C.c_int]),
     "vgpu_l2_norm": (C.c_float, [F32P, C.c_int]),
+    "vgpu_shard_range": (C.c_int, [C.c_size_t, C.c_int, C.c_int, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "vgpu_multi_create": (C.c_int, [C.POINTER(C.c_int), C.c_int, C.POINTER(VP)]),
+    "vgpu_multi_destroy": (None, [VP]),
+    "vgpu_multi_size": (C.c_int, [VP]),
+    "vgpu_multi_context": (VP, [VP, C.c_int]),
+    "vgpu_multi_last_error": (C.c_char_p, [VP]),
+    "vgpu_multi_env_create": (C.c_int, [VP, VP, C.POINTER(VP)]),
+    "vgpu_multi_validate_motions_host": (C.c_int, [VP, C.POINTER(VgpuRobot), C.POINTER(VP), F32P, F32P, C.c_size_t,
+                                                   U8P, I32P]),
+    "vgpu_multi_sample_fkcc_host": (C.c_int, [VP, C.POINTER(VgpuRobot), C.POINTER(VP), C.c_uint64, C.c_size_t, F32P,
+                                              C.POINTER(C.c_uint64), C.POINTER(C.c_size_t)]),
+    "vgpu_comm_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+    "vgpu_comm_init": (C.c_int, [VP, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(VP)]),
+    "vgpu_comm_destroy": (None, [VP]),
+    "vgpu_prm_vertices_allgather": (C.c_int, [VP, VP, C.POINTER(VgpuRobot), VP, C.c_uint64, C.c_size_t, VP, VP,
+                                              C.c_size_t, C.POINTER(C.c_size_t)]),
+    "vgpu_env_clone": (C.c_int, [VP, VP, C.POINTER(VP)]),
+    "vgpu_cpu_roadmap_knn": (C.c_int, [C.c_int, F32P, C.c_size_t, U32P, C.c_size_t, U32P, F32P, C.c_uint32, U32P, F32P,
+                                       U32P, C.c_int]),
     "vgpu_robot_scale_params": (C.c_int, [C.POINTER(VgpuRobot), F32P, F32P, F32P]),
     "vgpu_cpu_eefk": (C.c_int, [C.POINTER(VgpuRobot), F32P, C.c_size_t, F32P]),
     "vgpu_cpu_validate_vector": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, F32P, C.c_float, C.POINTER(C.c_int)]),

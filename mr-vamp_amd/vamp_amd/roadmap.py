@@ -124,6 +124,26 @@ def prm_neighbor_params(dim: int, space_measure: float, n: int, gamma_scale: flo
     return k, r
 
 
+def cpu_knn(V, queries, space_measure: float, gamma_scale: float = 2.0, kmax=None, threads: int = 0):
+    """build_roadmap's causal neighbour queries of the listed vertices on the host CPU (exact k-d tree,
+    vgpu_cpu_roadmap_knn): (nbr [m, kmax], dist [m, kmax], cnt [m]) -- the lists vgpu_roadmap_knn gives."""
+    from . import _lib
+    from ._lib import check, load
+    V = np.ascontiguousarray(V, np.float32)
+    n, dim = V.shape
+    q = np.ascontiguousarray(queries, np.uint32).ravel()
+    k, r = prm_neighbor_params(dim, space_measure, n, gamma_scale)
+    kmax = int(kmax or max(1, int(k.max()) if n else 1))
+    nbr = np.zeros((max(len(q), 1), kmax), np.uint32)
+    dist = np.zeros((max(len(q), 1), kmax), np.float32)
+    cnt = np.zeros(max(len(q), 1), np.uint32)
+    check(load().vgpu_cpu_roadmap_knn(dim, V.ctypes.data_as(_lib.F32P), n, q.ctypes.data_as(_lib.U32P), len(q),
+                                      k.ctypes.data_as(_lib.U32P), r.ctypes.data_as(_lib.F32P), kmax,
+                                      nbr.ctypes.data_as(_lib.U32P), dist.ctypes.data_as(_lib.F32P),
+                                      cnt.ctypes.data_as(_lib.U32P), int(threads)))
+    return nbr[:len(q)], dist[:len(q)], cnt[:len(q)]
+
+
 class Roadmap:
     """Roadmap<dim> (prm.hh:285-299): vertices [n, dim] and, per vertex, the indices of its
     neighbours in the order build_roadmap appended them; plus the connected components."""

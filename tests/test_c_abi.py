@@ -17,7 +17,7 @@ CAGE = [(0.55, 0, 0.25), (0.35, 0.35, 0.25), (0, 0.55, 0.25), (-0.55, 0, 0.25), 
 
 def declared():
     txt = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:int|void|float|const char \*)\s*\**(vgpu_\w+)\s*\(", txt, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|void|float|const char \*|vgpu_ctx \*)\s*\**(vgpu_\w+)\s*\(", txt, re.M)))
 
 
 @pytest.fixture(scope="module")

@@ -99,3 +99,20 @@ def test_prm_settings_mirror(oracle):
     for n in (2, 3, 10, 1000, 123457):
         assert st.max_neighbors(n) == oracle.prm_max_neighbors(7, n)
         assert np.float32(st.neighbor_radius(n)) == np.float32(oracle.prm_neighbor_radius(7, p.space_measure, 2.0, n))
+
+
+@pytest.mark.parametrize("robot,dim,n", [("fetch", 8, 3000), ("panda", 7, 2500), ("baxter", 14, 800)])
+def test_cpu_kdtree_knn_equals_oracle(oracle, robot, dim, n):
+    """vgpu_cpu_roadmap_knn (exact k-d tree, the CPU baseline's neighbour query) == the oracle's brute
+    force, on uniform vertices with a duplicate, and on Halton vertices; any query order."""
+    from vamp_amd import roadmap
+    rng = np.random.default_rng(3)
+    V = oracle.robot_scale(robot, rng.random((n, dim), dtype=np.float32))
+    V[n // 2] = V[n // 3]
+    sm = oracle.SPACE_MEASURE[robot]
+    onb, od, oc = oracle.roadmap_knn(V, sm)
+    qs = rng.permutation(n).astype(np.uint32)
+    nb, d, c = roadmap.cpu_knn(V, qs, sm, kmax=onb.shape[1], threads=4)
+    assert np.array_equal(c, oc[qs])
+    mask = np.arange(onb.shape[1])[None, :] < c[:, None]
+    assert np.array_equal(nb[mask], onb[qs][mask]) and np.array_equal(d[mask], od[qs][mask])

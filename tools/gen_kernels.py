@@ -25,6 +25,8 @@ import numpy as np
 
 F = np.float32
 REMAT = False  # rebuild rotation matrices per check (A/B on MI355X: 5.80 -> 6.81 ms, off)
+HOLD = True    # GPU self-pair children: hold the smaller side's centres, stream the other (--no-hold: chunks)
+GATE = True    # GPU staged bound stage: the wrist checks' (q5, q6) gate table when the model has one (--no-gate)
 
 # Emitted types.  The HIP kernels compute one configuration per lane in `float` with the
 # per-lane check bits in `uint32_t`; the CPU restatement (--cpu, mr-vamp_amd/csrc/cpu/) emits
@@ -379,6 +381,8 @@ class RobotGen:
         E.raw("}")
 
     def emit_self_pairs(self, E, fr, pairs, on_hit):
+        if not TY["cpu"] and HOLD:
+            return self.emit_self_pairs_held(E, fr, pairs, on_hit)
         spheres = self.m["spheres"]
         E.raw("{")
         E.indent += 1
@@ -406,6 +410,43 @@ class RobotGen:
             E.indent -= 1
             E.raw("}")
             if ci + 1 < nchunks:
+                E.raw(f"if (Grp::any_bits(h)) {on_hit}  // early exit (work only)")
+        E.raw(f"if (Grp::any_bits(h)) {on_hit}")
+        E.indent -= 1
+        E.raw("}")
+
+    def emit_self_pairs_held(self, E, fr, pairs, on_hit):
+        """GPU form: the centres of the side with fewer distinct spheres are computed once and held;
+        the other side's spheres are streamed one at a time (each centre lives only for its own tests),
+        so the live set is |held| x 3 + one frame + a centre -- not both sides.  Same expressions,
+        same bits; the OR is order-independent.  Early exit every CH streamed spheres."""
+        spheres = self.m["spheres"]
+        CH = 6
+        sa = sorted(set(p[0] for p in pairs))
+        sb = sorted(set(p[1] for p in pairs))
+        hold_a = len(sa) <= len(sb)
+        held, stream = (sa, sb) if hold_a else (sb, sa)
+        pset = set((p[0], p[1]) for p in pairs)
+        E.raw("{")
+        E.indent += 1
+        E.raw(bdecl("h", "OR of the children's test-value bits: sign bit = any child fired"))
+        hc = {x: fr.center(spheres[x]["frame"], spheres[x]["offset"]) for x in held}
+        for ci in range(0, len(stream), CH):
+            E.raw("{")
+            E.indent += 1
+            for y in stream[ci:ci + CH]:
+                c = fr.center(spheres[y]["frame"], spheres[y]["offset"])
+                for x in held:
+                    a, b = (x, y) if hold_a else (y, x)
+                    if (a, b) not in pset:
+                        continue
+                    ca, cb = (hc[x], c) if hold_a else (c, hc[x])
+                    E.raw(f"h |= self_bits({ca[0].expr()}, {ca[1].expr()}, {ca[2].expr()}, "
+                          f"{flit(spheres[a]['radius'])}, {cb[0].expr()}, {cb[1].expr()}, {cb[2].expr()}, "
+                          f"{flit(spheres[b]['radius'])});")
+            E.indent -= 1
+            E.raw("}")
+            if ci + CH < len(stream):
                 E.raw(f"if (Grp::any_bits(h)) {on_hit}  // early exit (work only)")
         E.raw(f"if (Grp::any_bits(h)) {on_hit}")
         E.indent -= 1
@@ -495,6 +536,116 @@ class RobotGen:
                "    float ax, float ay, float az, float bx, float by, float bz)",
                "{"]
         return "\n".join(hdr + E.lines + ["}", ""])
+
+    def load_gate(self):
+        """model/<robot>_pair_gate.json (tools/make_pair_gate.py), used by the GPU staged bound stage;
+        None without one (or for the CPU restatement, which evaluates every check)."""
+        import os
+        path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "model", f"{self.name}_pair_gate.json")
+        if TY["cpu"] or not GATE or not os.path.exists(path):
+            return None
+        return json.load(open(path))
+
+    def gate_function(self, gate):
+        n0, n1 = gate["n"]
+        lo0, lo1 = gate["lo"]
+        h0, h1 = gate["h"]
+        allmask = (1 << len(gate["checks"])) - 1
+        vals = ", ".join(str(v) for v in gate["gate"])
+        return [f"// (q_{gate['dofs'][0]}, q_{gate['dofs'][1]}) gate of checks {gate['checks']}: bit k set when check",
+                f"// checks[k] can fire somewhere in the cell (tools/make_pair_gate.py, margin {gate['margin']} m);",
+                "// outside the table (or NaN) every check is allowed",
+                f"static __device__ const uint8_t {self.name}_gate_table[{n0 * n1}] = {{{vals}}};",
+                f"__device__ __forceinline__ uint32_t {self.name}_gate(float a, float b)",
+                "{",
+                f"    const float fa = (a - {flit(lo0)}) * {flit(1.0 / h0)};",
+                f"    const float fb = (b - {flit(lo1)}) * {flit(1.0 / h1)};",
+                f"    if (!(fa >= 0.0f && fa < {flit(n0)} && fb >= 0.0f && fb < {flit(n1)})) return {allmask}u;",
+                f"    return {self.name}_gate_table[(int)fa * {n1} + (int)fb];",
+                "}", ""]
+
+    def gen_pair_staged(self, chunk=64) -> str:
+        """Staged form of the composite's inter-arm check (vgpu_staged.hh; BASELINE configs[4]): check
+        c = link-bounding pair (la, lb) in the same link-major order as gen_pair_inter, split into
+        chunks of <= 64 checks, one bound function per chunk (u64 mask of the chunk's bounding tests
+        that fire for the group) and one children function over all checks (check c's sphere pairs,
+        both links' frames recomputed, the arm with the fewer spheres held).  valid == no check whose
+        bounding test and one of its children fire: the monolithic gen_pair_inter's OR, staged."""
+        m = self.m
+        dim = m["dimension"]
+        nb = len(m["bounding"])
+        spheres = m["spheres"]
+        links = [b["link"] for b in m["bounding"]]
+        checks = [(la, lb) for la in range(nb) for lb in range(nb)]
+        args = ", ".join(f"{TY['f']} q{i}" for i in range(2 * dim))
+        base_args = "float ax, float ay, float az, float bx, float by, float bz"
+
+        def wc(E, c, pre):
+            return [E.add(c[i], SV("var", name=f"{pre}{'xyz'[i]}")) for i in range(3)]
+
+        out = [f"// GENERATED by tools/gen_kernels.py --pair-staged from model/{self.name}.json -- do not edit.",
+               f"constexpr int {self.name}_pair_n_checks = {len(checks)};",
+               f"constexpr int {self.name}_pair_chunk = {chunk};"]
+        for k in range(0, len(checks), chunk):
+            E = Emitter()
+            fa, fb = self.Frames(self, E, 0), self.Frames(self, E, dim)
+            bca, bcb = {}, {}
+            E.raw("uint64_t mask = 0u;")
+            for c in range(k, min(k + chunk, len(checks))):
+                la, lb = checks[c]
+                if la not in bca:
+                    bca[la] = wc(E, fa.bound_center(la), "a")
+                if lb not in bcb:
+                    bcb[lb] = wc(E, fb.bound_center(lb), "b")
+                A_, B_ = bca[la], bcb[lb]
+                ra, rb = m["bounding"][la]["radius"], m["bounding"][lb]["radius"]
+                E.raw(f"if (Grp::any(self_lane({A_[0].expr()}, {A_[1].expr()}, {A_[2].expr()}, {flit(ra)}, "
+                      f"{B_[0].expr()}, {B_[1].expr()}, {B_[2].expr()}, {flit(rb)}))) mask |= 1ull << {c - k};"
+                      f"  // {links[la]} (A) vs {links[lb]} (B)")
+            E.raw("return mask;")
+            out += ["template <class Grp>",
+                    f"{TY['qual']} uint64_t {self.name}_pair_bound_mask_{k // chunk}(",
+                    f"    {args},", f"    {base_args})", "{"] + E.lines + ["}", ""]
+        body = []
+        for c, (la, lb) in enumerate(checks):
+            E = Emitter()
+            E.indent = 2
+            ga, gb = self.Frames(self, E, 0), self.Frames(self, E, dim)
+            sa_ = [i for i, sp in enumerate(spheres) if sp["link"] == links[la]]
+            sb_ = [j for j, sp in enumerate(spheres) if sp["link"] == links[lb]]
+            for i in sa_:
+                ga.rot(spheres[i]["frame"])
+            for j in sb_:
+                gb.rot(spheres[j]["frame"])
+            hold_a = len(sa_) <= len(sb_)
+            held, stream = (sa_, sb_) if hold_a else (sb_, sa_)
+            gh, gs = (ga, gb) if hold_a else (gb, ga)
+            ph, ps = ("a", "b") if hold_a else ("b", "a")
+            E.raw(bdecl("h"))
+            hc = {x: wc(E, gh.center(spheres[x]["frame"], spheres[x]["offset"]), ph) for x in held}
+            CH = 6
+            for ci in range(0, len(stream), CH):
+                E.raw("{")
+                E.indent += 1
+                for y in stream[ci:ci + CH]:
+                    cy = wc(E, gs.center(spheres[y]["frame"], spheres[y]["offset"]), ps)
+                    for x in held:
+                        (i, ci_), (j, cj_) = ((x, hc[x]), (y, cy)) if hold_a else ((y, cy), (x, hc[x]))
+                        E.raw(f"h |= self_bits({ci_[0].expr()}, {ci_[1].expr()}, {ci_[2].expr()}, "
+                              f"{flit(spheres[i]['radius'])}, {cj_[0].expr()}, {cj_[1].expr()}, {cj_[2].expr()}, "
+                              f"{flit(spheres[j]['radius'])});")
+                E.indent -= 1
+                E.raw("}")
+                if ci + CH < len(stream):
+                    E.raw("if (Grp::any_bits(h)) return true;  // early exit (work only)")
+            E.raw("return Grp::any_bits(h);")
+            body += [f"    case {c}: {{  // {links[la]} (A) vs {links[lb]} (B): {len(sa_)} x {len(sb_)} sphere pairs"]
+            body += E.lines + ["    }"]
+        out += ["template <class Grp>",
+                f"{TY['qual']} bool {self.name}_pair_children(int check,",
+                f"    {args},", f"    {base_args})", "{", "    switch (check) {"] + body + \
+               ["    default:", "        return false;", "    }", "}", ""]
+        return "\n".join(out)
 
     def signature(self, ret, fname, extra=""):
         dim = self.m["dimension"]
@@ -610,16 +761,25 @@ class RobotGen:
         evaluated check by check instead of in one divergent pass."""
         m = self.m
         order = m["check_order"]
-        assert len(order) <= 64
+        if len(order) > 64:
+            return self.gen_staged_chunked()
         wide = len(order) > 32
         mt, one = ("uint64_t", "1ull") if wide else ("uint32_t", "1u")
         E = Emitter()
         fr = self.Frames(self, E)
         E.raw(f"{mt} mask = 0u;")
+        gate = self.load_gate()
+        gated = {}
+        if gate is not None:  # the wrist self checks' (q_a, q_b) gate table (tools/make_pair_gate.py)
+            d0, d1 = gate["dofs"]
+            E.raw(f"const uint32_t gate = Grp::or_bits({self.name}_gate(q{d0}, q{d1}));  // per group: checks that can fire")
+            gated = {c: b for b, c in enumerate(gate["checks"])}
         for c, o in enumerate(order):
             kind, test, ck = self.bound_test(fr, o)
             if kind == "env":
                 E.raw(f"if (Grp::any_bits({test})) mask |= {one} << {c};")
+            elif c in gated:
+                E.raw(f"if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c};")
             else:
                 E.raw(f"if (Grp::any({test})) mask |= {one} << {c};")
         E.raw("return mask;")
@@ -628,7 +788,15 @@ class RobotGen:
                f"constexpr int {self.name}_n_checks = {len(order)};",
                f"using {self.name}_mask_t = {mt};",
                f"constexpr {mt} {self.name}_env_check_bits = {env_bits:#x}{'ull' if wide else 'u'};  // environment checks"]
+        if gate is not None:
+            out += self.gate_function(gate)
         out += self.signature(mt, "bound_mask") + E.lines + ["}", ""]
+        out += self.staged_children(order)
+        return "\n".join(out)
+
+    def staged_children(self, order):
+        """<robot>_children(check, q..., env, base): check c's children, frames recomputed"""
+        m = self.m
         body = []
         for c, o in enumerate(order):
             E = Emitter()
@@ -651,26 +819,45 @@ class RobotGen:
             self.emit_children(E, fr, kind, ck, "return true;")
             body += [f"    case {c}: {{  // {kind}: {label} ({len(ck['children'])} children)"] + E.lines + \
                     ["        return false;", "    }"]
-        out += self.signature("bool", "children", "int check, ")
+        out = self.signature("bool", "children", "int check, ")
         out += ["    switch (check) {"] + body + ["    default:", "        return false;", "    }", "}", ""]
+        return out
+
+    def gen_staged_chunked(self, chunk=64) -> str:
+        """Staged form of a robot with more than 64 checks (the Baxter: 388): the check list in chunks
+        of <= 64, one bound function per chunk (only the frames its checks need, a u64 mask of the
+        chunk's bounding tests) -- each chunk a chained staged pass over the same groups
+        (vgpu_baxter_staged.hip) -- and one children function over all checks."""
+        m = self.m
+        order = m["check_order"]
+        name = self.name
+        out = [f"// GENERATED by tools/gen_kernels.py from model/{name}.json -- do not edit.",
+               f"constexpr int {name}_n_checks = {len(order)};",
+               f"constexpr int {name}_chunk = {chunk};",
+               f"constexpr int {name}_n_chunks = {(len(order) + chunk - 1) // chunk};"]
+        envs = []
+        for k in range(0, len(order), chunk):
+            E = Emitter()
+            fr = self.Frames(self, E)
+            E.raw("uint64_t mask = 0u;")
+            for c in range(k, min(k + chunk, len(order))):
+                kind, test, ck = self.bound_test(fr, order[c])
+                if kind == "env":
+                    E.raw(f"if (Grp::any_bits({test})) mask |= 1ull << {c - k};")
+                else:
+                    E.raw(f"if (Grp::any({test})) mask |= 1ull << {c - k};")
+            E.raw("return mask;")
+            out += self.signature("uint64_t", f"bound_mask_{k // chunk}") + E.lines + ["}", ""]
+            envs.append(sum(1 << (c - k) for c in range(k, min(k + chunk, len(order)))
+                            if order[c]["kind"] == "env"))
+        out.append(f"constexpr uint64_t {name}_env_check_bits_chunk[{len(envs)}] = {{" +
+                   ", ".join(f"{e:#x}ull" for e in envs) + "};")
+        out += self.staged_children(order)
         return "\n".join(out)
 
 
-def gen_radii(paths) -> str:
-    """Host-and-device table of every robot's collision-sphere radii (reference order, the
-    Spheres<rake>::r of Robot::sphere_fk): used where a kernel needs the radii next to
-    sphere_fk's centres (filter_robot_from_pointcloud, bindings/common.hh:36-87)."""
-    out = ["// GENERATED by tools/gen_kernels.py --radii from model/*.json -- do not edit.", "#pragma once", ""]
-    for path in paths:
-        m = json.load(open(path))
-        vals = ", ".join(flit(sp["radius"]) for sp in m["spheres"])
-        out.append(f"constexpr int {m['robot']}_n_spheres_table = {len(m['spheres'])};")
-        out.append(f"constexpr float {m['robot']}_sphere_radii[{len(m['spheres'])}] = {{{vals}}};")
-    return "\n".join(out) + "\n"
-
-
 def main():
-    global REMAT, TY
+    global REMAT, TY, HOLD, GATE
     if "--radii" in sys.argv:  # tools/gen_kernels.py --radii OUT model/a.json model/b.json ...
         args = [a for a in sys.argv[1:] if a != "--radii"]
         open(args[0], "w").write(gen_radii(args[1:]))
@@ -681,6 +868,12 @@ def main():
         sys.argv.remove("--no-remat")
     if "--cpu" in sys.argv:
         TY = TY_CPU
+    if "--no-hold" in sys.argv:
+        HOLD = False
+        sys.argv.remove("--no-hold")
+    if "--no-gate" in sys.argv:
+        GATE = False
+        sys.argv.remove("--no-gate")
     argv = [a for a in sys.argv if not a.startswith("--")]
     sys.argv[1:3] = argv[1:3]
     model = json.load(open(sys.argv[1]))
@@ -699,10 +892,12 @@ def main():
             out = g.gen_fkcc()
     elif "att_checks" in model:  # the attachment variant: its fkcc only (first rake block)
         out = g.gen_fkcc()
-    elif len(model["check_order"]) <= 64:  # check masks: 32-bit up to 32 checks, 64-bit up to 64
+    else:  # check masks: 32-bit up to 32 checks, 64-bit up to 64, chunks of 64 beyond
         out += "\n" + g.gen_staged()
     if "--pair" in sys.argv:  # the composite's inter-robot check, as its own include
         out = g.gen_pair_inter()
+    if "--pair-staged" in sys.argv:  # its staged form (vgpu_pair_staged.hip)
+        out = g.gen_pair_staged()
     open(sys.argv[2], "w").write(out)
     print(f"wrote {sys.argv[2]} ({len(out.splitlines())} lines)")
 

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--edges", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--tag", default=os.path.basename(os.environ.get("VAMP_AMD_LIB", "default")))
+    ap.add_argument("--only-setb", action="store_true", help="validate set B only (PMC passes)")
     a = ap.parse_args()
     import torch
 
@@ -57,6 +58,8 @@ def main():
         units = 8 * nb.long().sum().item()
         print(json.dumps({"tag": a.tag, "kernel": "validate_setB", "ms": ms, "interp_per_s": units / ms * 1e3,
                           "ok": ok.float().mean().item()}))
+        if a.only_setb:
+            return
         # raw pairs (set A): mostly invalid, long edges
         gen = torch.Generator(device=dev)
         gen.manual_seed(5)
