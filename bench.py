@@ -427,52 +427,66 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
 
     wall = timed_steps(a, torch, dist, dev, world, step)
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(n) / world, dev, world)
-    # the kNN kernel alone (this rank's queries), HIP events on the launch stream
+    # the kNN kernel alone (this rank's queries), HIP events on the launch stream, in both methods
+    # of vgpu_set_knn_mode: brute force (the roofline: its flops are the ones executed) and the
+    # spatial index (auto's choice from 1e6 vertices; same lists, compared below)
     nbr = torch.empty((max(qc, 1), kmax), dtype=torch.int32, device=dev)
     dd = torch.empty((max(qc, 1), kmax), dtype=torch.float32, device=dev)
     cc = torch.empty(max(qc, 1), dtype=torch.int32, device=dev)
     from vamp_amd._lib import check, load
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(stream)
-    for _ in range(a.steps):
-        check(load().vgpu_roadmap_knn_range(ctx.h, dim, V.data_ptr(), n, qf, qc, k.data_ptr(), r.data_ptr(), kmax,
-                                            nbr.data_ptr(), dd.data_ptr(), cc.data_ptr()), ctx.h)
-    e1.record(stream)
-    torch.cuda.synchronize(dev)
-    knn_ms = e0.elapsed_time(e1) / a.steps
+    knn = {}
+    lists = {}
+    for mode, name in ((1, "brute"), (2, "index")):
+        check(load().vgpu_set_knn_mode(ctx.h, mode), ctx.h)
+        reps = 1 if n >= 1_000_000 else a.steps
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            check(load().vgpu_roadmap_knn_range(ctx.h, dim, V.data_ptr(), n, qf, qc, k.data_ptr(), r.data_ptr(), kmax,
+                                                nbr.data_ptr(), dd.data_ptr(), cc.data_ptr()), ctx.h)
+        e1.record(stream)
+        torch.cuda.synchronize(dev)
+        knn[name] = e0.elapsed_time(e1) / reps
+        lists[name] = (nbr[:qc].clone(), cc[:qc].clone())
+    check(load().vgpu_set_knn_mode(ctx.h, 0), ctx.h)
+    knn_ms = knn["brute"]
+    (nb_b, cc_b), (nb_i, cc_i) = lists["brute"], lists["index"]
+    width = torch.arange(kmax, device=dev)[None, :] < cc_b[:, None].long()
+    index_equals_brute = bool(torch.equal(cc_b, cc_i)) and bool(torch.equal(nb_b[width], nb_i[width]))
+    del lists, nb_b, nb_i, cc_b, cc_i
     candidates = int(cc[:qc].long().sum())
     if rank != 0:
         return
-    # algorithmic work of the query kernel: one Space<8>::distance per (vertex, earlier vertex)
-    # pair = 8 sub + 8 mul + 7 add + 1 sqrt (nn.hh:53-57)
+    # algorithmic work of the brute-force query kernel: one Space<8>::distance per (vertex, earlier
+    # vertex) pair = 8 sub + 8 mul + 7 add + 1 sqrt (nn.hh:53-57)
     pairs_scanned = sum(range(qf, qf + qc))
     flops = 24.0 * pairs_scanned
     achieved = flops / (knn_ms * 1e-3) / 1e12
     cpu = None
     if not a.no_cpu and world == 1:
-        sys.path.insert(0, os.path.join(ROOT, "tests"))
-        import oracle_py as op
-        from test_oracle_fetch import fetch_env
-
-        oenv = fetch_env(op, fx)
+        # the reference's host path for the stage: an exact k-d tree neighbour query (nigh's role,
+        # planning/nn.hh:89-95; csrc/cpu/vcpu_roadmap.cpp) and validate_motion on the AVX2 rake
+        # (csrc/cpu), over a prefix of the same vertex sequence, all host threads of this rank
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
         Vh = V.cpu().numpy()
         m = 4000
-        while True:  # grow the prefix until the restated stage takes ~cpu_seconds
+        while True:  # grow the prefix until the stage takes ~cpu_seconds / 3
             t = time.perf_counter()
-            nb_, _, cn_ = op.roadmap_knn(Vh[:m], op.SPACE_MEASURE["fetch"], threads=threads)
+            nb_, _, cn_ = roadmap.cpu_knn(Vh[:m], np.arange(m), robot.space_measure(), threads=threads)
             qi = np.repeat(np.arange(m), cn_.astype(np.int64))
             qm = np.concatenate([np.arange(c) for c in cn_]).astype(np.int64)
             qj = nb_[qi, qm].astype(np.int64)
-            op.robot_validate_motions("fetch", oenv, Vh[qj], Vh[qi], threads=threads)
+            t_nn = time.perf_counter() - t
+            robot.cpu_validate_batch(Vh[qj], Vh[qi], env, threads=threads)
             dt = time.perf_counter() - t
             if dt >= a.cpu_seconds / 3 or m >= n:
                 break
             m = min(n, int(m * min(4.0, max(1.3, (a.cpu_seconds / max(dt, 1e-3)) ** 0.5))))
         cpu = {"value": m / dt, "unit": "vertices/s", "cores": threads, "kind": "port",
-               "sample": f"the first {m} vertices of the same sequence: oracle/vamp_oracle.c brute-force neighbour "
-                         f"queries + validate_motion of the {len(qi)} candidates, {threads} threads, {dt:.1f} s "
-                         f"(the stage is superlinear in the vertex count: the rate at {n} is lower)",
+               "sample": f"the first {m} vertices of the same sequence: exact k-d tree neighbour queries "
+                         f"(vgpu_cpu_roadmap_knn, {t_nn:.2f} s) + validate_motion of the {len(qi)} candidates on the "
+                         f"AVX2 rake (mr-vamp_amd/csrc/cpu), {threads} threads, {dt:.1f} s in all; the host graph "
+                         f"assembly is not included (the stage is superlinear in the vertex count: the rate at {n} is lower)",
                "cpu_model": cpu_model()}
     line = {
         "metric": "PRM edge-stage roadmap vertices/sec (Fetch 8-DOF build_roadmap: neighbour queries + edge validation)",
@@ -495,7 +509,11 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         "roofline": {"kernel": "knn_kernel<8, K> (causal neighbour queries)", "bound": "valu", "achieved": achieved,
                      "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
                      "traffic": None, "kernel_ms": knn_ms, "algorithmic_flops_per_vertex_pair": 24,
-                     "vertex_pairs_rank0": pairs_scanned},
+                     "vertex_pairs_rank0": pairs_scanned,
+                     "knn_ms": knn, "knn_mode_in_step": "index" if n >= 1_000_000 else "brute",
+                     "index_equals_brute": index_equals_brute,
+                     "note": "roofline of the brute-force kernel (every pair evaluated); the index kernel's time is "
+                             "beside it, not priced in flops (it skips pairs)"},
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
@@ -734,10 +752,39 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
 
     wall = timed_steps(a, torch, dist, dev, world, step)
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(N), dev, world)
+    # configs[2]'s "1M collision queries" as raw CAPT::collides_simd sphere queries (scenes.raw_queries:
+    # x, y ~ U[-1, 1], z ~ U[0, 1.2], r ~ U[r_min, r_max]), outside the contract's timed region
+    rq_c, rq_r = scenes.raw_queries(1 << 20)
+    cd, rd = torch.from_numpy(rq_c).to(dev), torch.from_numpy(rq_r).to(dev)
+    rq_out = torch.empty(1 << 20, dtype=torch.uint8, device=dev)
+    hp = env.handle(ctx)
+
+    def raw():
+        env.pointcloud_collides_device(cd.data_ptr(), rd.data_ptr(), 1 << 20, rq_out.data_ptr(), simd=True, ctx=ctx)
+
+    for _ in range(3):
+        raw()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(20):
+        raw()
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    raw_ms = e0.elapsed_time(e1) / 20
+    # the cell grid's build (vgpu_capt_grid.hip) is part of each device upload: time one re-upload
+    t = time.perf_counter()
+    env._changed()
+    env.handle(ctx)
+    torch.cuda.synchronize(dev)
+    upload_ms = (time.perf_counter() - t) * 1e3
+    del hp
     if rank != 0:
         return
     import oracle_py as op
     oenv = op.Env().add_pointcloud(pts, scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    raw_want = op.Capt(pts, scenes.R_MIN, scenes.R_MAX, scenes.R_POINT).collides(rq_c[:1 << 17], rq_r[:1 << 17],
+                                                                                 simd=True)
+    raw_got = rq_out[:1 << 17].cpu().numpy().astype(bool)
     qs = q[:2048].cpu().numpy()
     _, _, _, fl = op.fkcc(oenv, qs, (0, 0, 0), stats=True)
     f_cfg = float(fl.mean())
@@ -792,6 +839,14 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                  "workgroup; CAPT arrays (~4.7 MB) L2/MALL resident"},
         cpu)
     line["parity"] = parity
+    line["raw_queries"] = {
+        "queries": 1 << 20, "ms": raw_ms, "queries_per_s": (1 << 20) / raw_ms * 1e3,
+        "hit_fraction": float(rq_out.float().mean().item()),
+        "oracle_mismatches": int((raw_got != raw_want).sum()), "oracle_compared": 1 << 17,
+        "note": "one lane per sphere, CAPT::collides_simd semantics (capt.hh:457-541) through the cell grid; HIP events"}
+    line["environment_upload_ms"] = {"ms": upload_ms, "note": "one re-realisation of the environment on the device: "
+                                                              "handle create, CAPT arrays from the host twin, blob upload, "
+                                                              "cell-grid build (host wall clock)"}
     print(json.dumps(line))
 
 

@@ -98,7 +98,7 @@ VCPU_INLINE V sphere_sphere(V ax, V ay, V az, V ar, V bx, V by, V bz, V br)
 enum : int { OBS_SPHERE = 0, OBS_CAPSULE = 1, OBS_ZCAPSULE = 2, OBS_CUBOID = 3, OBS_ZCUBOID = 4, OBS_TYPES = 5 };
 constexpr int kObsStride[OBS_TYPES] = {8, 16, 16, 16, 16};
 constexpr int kAttHdr = 8;
-constexpr int kExtHdr = 16;
+constexpr int kExtHdr = 32;  // = vgpu_device.hh (the host view leaves the device-only cell grid fields 0)
 enum : int { HF_X = 0, HF_Y, HF_Z, HF_XS, HF_YS, HF_ZS, HF_XD, HF_YD, HF_XD2, HF_YD2, HF_OFF, HF_CELLS };
 enum : int { PC_TOP = 0, PC_RPOINT = 6, PC_NLOG2 = 7, PC_TESTS, PC_AABBS, PC_STARTS, PC_AFF };
 

@@ -89,6 +89,7 @@ hipError_t vgpu_launch_fetch_tail_counts(const float* starts, const float* goals
 hipError_t vgpu_launch_mask_finish(size_t n_edges, const uint32_t* off, uint8_t* ok, uint8_t* block_ok, hipStream_t st);
 hipError_t vgpu_launch_tail_counts(const float* starts, const float* goals, size_t n_edges, const uint8_t* ok,
                                    int32_t* n_blocks, uint32_t* cnt, hipStream_t st);
+hipError_t vgpu_launch_capt_grid(float* base, const vgpu::CaptGridArgs* g, hipStream_t st);
 hipError_t vgpu_launch_capt_query(const float* centers, const float* radii, size_t n, const EnvView* env, int index,
                                   int simd, uint8_t* out, hipStream_t st);
 hipError_t vgpu_launch_panda_sphere_fk(const float* q, size_t n, float bx, float by, float bz, float* out,
@@ -279,6 +280,7 @@ struct vgpu_env {
     std::array<float, 7> att_tf{};
     std::vector<std::array<float, 4>> att_spheres;
     size_t hf_off = 0, pc_off = 0, att_off = 0;
+    std::vector<vgpu::CaptGridArgs> pc_grid;  // device copy: each cloud's cell grid (cells_off 0 = none)
     bool dirty = true;       // device copy stale
     bool host_dirty = true;  // host copy (the CPU rake's view, csrc/cpu/) stale
     std::vector<float> host_blob;
@@ -757,7 +759,16 @@ extern "C" int vgpu_env_detach(vgpu_env* e)
 // (environment.hh:40-66) followed by kObsPad sentinels (md = +inf), then heightfield / point-cloud
 // headers and arrays, then the attachment.  The same layout serves the device (vgpu_env_upload)
 // and the CPU rake (vgpu_env_host_view); offsets are recorded in the environment.
-static int build_blob(vgpu_env* e, std::vector<float>& blob)
+// Cells of the device point clouds' grids: VGPU_CAPT_GRID_CELLS unset = capt_grid_plan's default,
+// 0 = no grid (the plain traversal, for A/B runs), N = about N cells.
+static bool grid_cells(size_t& cells)
+{
+    const char* v = std::getenv("VGPU_CAPT_GRID_CELLS");
+    cells = v ? (size_t)std::strtoull(v, nullptr, 10) : 0;
+    return !(v && cells == 0);
+}
+
+static int build_blob(vgpu_env* e, std::vector<float>& blob, bool device = false)
 {
     sort_md(e->spheres);
     sort_md(e->capsules);
@@ -765,6 +776,7 @@ static int build_blob(vgpu_env* e, std::vector<float>& blob)
     sort_md(e->cuboids);
     sort_md(e->zcuboids);
     blob.clear();
+    if (device) e->pc_grid.clear();
     auto put = [&](auto& v, int type, int np) {
         const int S = kObsStride[type];
         e->off[type] = blob.size();
@@ -828,6 +840,29 @@ static int build_blob(vgpu_env* e, std::vector<float>& blob)
         hd[PC_AABBS] = hdr_u((uint32_t)o_aabbs);
         hd[PC_STARTS] = hdr_u((uint32_t)o_starts);
         hd[PC_AFF] = hdr_u((uint32_t)o_aff);
+        // device copies: room for the cell grid, filled by vgpu_launch_capt_grid after the upload
+        vgpu::CaptGridArgs g{};
+        size_t cells = 0;
+        if (device && grid_cells(cells) && vgpu::capt_grid_plan(t, cells, g)) {
+            align16();
+            g.tests_off = (uint32_t)o_tests;
+            g.starts_off = (uint32_t)o_starts;
+            g.aff_off = (uint32_t)o_aff;
+            g.cells_off = (uint32_t)blob.size();
+            blob.resize(blob.size() + 2 * (size_t)g.nx * g.ny * g.nz, 0.0f);
+            hd = &blob[e->pc_off + kExtHdr * i];
+            const float gv[] = {g.x0, g.y0, g.z0, g.inv_h};
+            std::copy(gv, gv + 4, hd + PC_GX);
+            hd[PC_GNX] = hdr_u(g.nx);
+            hd[PC_GNY] = hdr_u(g.ny);
+            hd[PC_GNZ] = hdr_u(g.nz);
+            hd[PC_GNXF] = (float)g.nx;
+            hd[PC_GNYF] = (float)g.ny;
+            hd[PC_GNZF] = (float)g.nz;
+            hd[PC_GUNIT] = g.unit;
+            hd[PC_GCELLS] = hdr_u(g.cells_off);
+        }
+        if (device) e->pc_grid.push_back(g);
     }
     // the attachment: frame (7 floats + pad), then its spheres (16-B aligned)
     align16();
@@ -847,7 +882,7 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     if (!e->dirty && e->dev) return VGPU_OK;
     std::lock_guard<std::mutex> lock(e->host_mu);  // build_blob re-sorts the host rows
     std::vector<float> blob;
-    if (int rc = build_blob(e, blob)) return rc;
+    if (int rc = build_blob(e, blob, true)) return rc;
     HIPCHK(c, hipSetDevice(c->device));
     if (blob.size() > e->dev_floats) {
         if (e->dev) {
@@ -859,6 +894,8 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
         e->dev_floats = blob.size();
     }
     HIPCHK(c, hipMemcpyAsync(e->dev, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice, c->cur));
+    for (const auto& g : e->pc_grid)
+        if (g.cells_off) HIPCHK(c, vgpu_launch_capt_grid(e->dev, &g, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));  // blob is a host temporary
     e->dirty = false;
     return VGPU_OK;

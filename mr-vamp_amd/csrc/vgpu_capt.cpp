@@ -162,4 +162,41 @@ void capt_build(const float* points, size_t n, float r_min, float r_max, float r
         std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
 }
 
+bool capt_grid_plan(const CaptTree& t, size_t cells, CaptGridArgs& g)
+{
+    g = CaptGridArgs{};
+    if (t.aff_starts.empty() || t.aff.empty()) return false;
+    const double m = (double)t.r_max + (double)t.r_point;
+    double lo[3], ext[3], vol = 1.0;
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = (double)t.top[k] - m;
+        ext[k] = (double)t.top[3 + k] + m - lo[k];
+        if (!std::isfinite(lo[k]) || !std::isfinite(ext[k]) || !(ext[k] > 0.0)) return false;
+        vol *= ext[k];
+    }
+    if (cells == 0) cells = std::min<size_t>(std::max<size_t>((size_t)128 << t.nlog2, 1u << 12), 1u << 22);
+    double h = std::cbrt(vol / (double)cells);
+    uint32_t n[3];
+    for (;;) {  // at most 1024 cells per axis (the device's cell index error bound), ~cells in all
+        bool ok = true;
+        for (int k = 0; k < 3; ++k) {
+            const double c = std::ceil(ext[k] / h);
+            if (c > 1024.0) ok = false;
+            n[k] = (uint32_t)std::max(1.0, c);
+        }
+        if (ok) break;
+        h *= 1.25;
+    }
+    g.x0 = (float)lo[0];
+    g.y0 = (float)lo[1];
+    g.z0 = (float)lo[2];
+    g.inv_h = (float)(1.0 / h);
+    g.nx = n[0];
+    g.ny = n[1];
+    g.nz = n[2];
+    g.unit = (float)(1.0 / (double)g.inv_h / 256.0);
+    g.nlog2 = t.nlog2;
+    return g.unit > 0.0f && std::isfinite(g.unit);
+}
+
 }  // namespace vgpu

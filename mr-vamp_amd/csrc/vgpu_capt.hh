@@ -27,6 +27,20 @@ struct CaptTree {
 // are ordered by point index (the reference's pdqsort leaves that order unspecified).
 void capt_build(const float* points, size_t n, float r_min, float r_max, float r_point, CaptTree& out);
 
+// Cell grid of a device copy (vgpu_capt_grid.hip); offsets in floats into the environment blob.
+struct CaptGridArgs {
+    uint32_t tests_off, starts_off, aff_off;
+    int nlog2;
+    float x0, y0, z0, inv_h;
+    uint32_t nx, ny, nz;
+    float unit;
+    uint32_t cells_off;
+};
+
+// Sizes the grid of tree t: the top box grown by r_max + r_point, cubic cells, about `cells`
+// of them (0 = default: 128 per leaf, within [2^12, 2^22]; 8 B each).  false: no grid (empty cloud).
+bool capt_grid_plan(const CaptTree& t, size_t cells, CaptGridArgs& g);
+
 struct Heightfield {
     float x, y, z, xs, ys, zs;  // offset and reciprocal scales (factory::heightfield::flat)
     size_t xd, yd;

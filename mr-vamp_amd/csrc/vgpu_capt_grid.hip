@@ -1,0 +1,129 @@
+// vgpu_capt_grid.hip -- the cell grid of a device point cloud: an acceleration structure over the
+// CAPT (collision/capt.hh:91-398) that decides most queries with one 8-byte load and starts the
+// rest below the root.  It changes no answer: every bound is taken over exactly the affordances
+// the reference's traversal can reach from the cell, and query_lane (vgpu_device.hh capt_lane)
+// falls back to that traversal whenever a bound does not decide.
+//
+// Grid: a box of nx * ny * nz cubic cells of side h = 1 / inv_h from (x0, y0, z0) (the CAPT's top
+// box grown by r_max + r_point on every side).  A centre x lands in cell floor((x - x0) * inv_h)
+// evaluated in float; that is within 3e-5 cells of the exact quotient for up to ~1000 cells per
+// axis, so the EXPANDED cell [i - kSlack, i + 1 + kSlack] * h (kSlack = 1e-3) contains every
+// centre the device puts in cell i.  Per cell, one thread, in double:
+//   node  the deepest split node whose region contains the whole expanded cell: every split above
+//         it sends the whole cell one way (a >= t for all a when lo >= t; a < t for all when
+//         hi < t or t is NaN -- the device's `a >= t` is false on NaN), so a descent from it
+//         reaches the same leaf as one from the root;
+//   lo    min over the leaves the cell can reach (both sides of each split it straddles) of the
+//         least distance from the cell to an affordance of the leaf (point-to-box distance);
+//   hi    max over those leaves of min over the leaf's affordances of the FARTHEST-corner
+//         distance: some affordance of whichever leaf is reached lies within hi of any centre.
+// lo is rounded down and hi up to multiples of unit = h / 256 (16 bits each; 0xFFFF = no bound:
+// a cell with an empty leaf or more than kMaxLeaves reachable leaves).  The device tests
+// (r + r_point)^2 < (lo)^2 * 0.9999 -> miss and > (hi)^2 * 1.0001 -> hit: the reference's
+// fma sum-of-squares differs from the exact squared distance by < 1e-6 relative (all terms
+// non-negative), and the float products of the bound by < 1e-6.
+#include "vgpu_capt.hh"
+#include "vgpu_device.hh"
+
+namespace vgpu {
+
+constexpr double kSlack = 1e-3;
+constexpr int kMaxLeaves = 64;
+
+__global__ __launch_bounds__(256) void capt_grid_kernel(float* __restrict__ base, CaptGridArgs g)
+{
+    const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t n_cells = g.nx * g.ny * g.nz;
+    if (cell >= n_cells) return;
+    const uint32_t ix = cell % g.nx, iy = (cell / g.nx) % g.ny, iz = cell / (g.nx * g.ny);
+    const double h = 1.0 / (double)g.inv_h;
+    const double o[3] = {(double)g.x0, (double)g.y0, (double)g.z0};
+    const uint32_t ic[3] = {ix, iy, iz};
+    double L[3], U[3];
+    for (int k = 0; k < 3; ++k) {
+        L[k] = o[k] + ((double)ic[k] - kSlack) * h;
+        U[k] = o[k] + ((double)ic[k] + 1.0 + kSlack) * h;
+    }
+    const float* __restrict__ tests = base + g.tests_off;
+    const uint32_t* __restrict__ starts = (const uint32_t*)(base + g.starts_off);
+    const float* __restrict__ aff = base + g.aff_off;
+    const int nlog2 = g.nlog2;
+
+    // the deepest node containing the whole expanded cell
+    uint32_t node = 0;
+    for (int lv = 0; lv < nlog2; ++lv) {
+        const float t = tests[node];
+        const int ax = lv % 3;
+        if (L[ax] >= (double)t) node = 2u * node + 2u;                 // every a >= t
+        else if (U[ax] < (double)t || t != t) node = 2u * node + 1u;  // no a >= t
+        else break;
+    }
+    // the leaves reachable from it, depth first
+    double lo2 = __builtin_inf(), hi2 = 0.0;
+    int leaves = 0;
+    bool bounded = true;
+    uint32_t stack[64];
+    int sp = 0;
+    stack[sp++] = node;
+    const uint32_t first_leaf = (1u << nlog2) - 1u;
+    while (sp > 0 && bounded) {
+        const uint32_t n = stack[--sp];
+        if (n >= first_leaf) {
+            if (++leaves > kMaxLeaves) {
+                bounded = false;
+                break;
+            }
+            const uint32_t leaf = n - first_leaf;
+            double lmin = __builtin_inf(), hmin = __builtin_inf();
+            for (uint32_t j = starts[leaf], e = starts[leaf + 1]; j < e; ++j) {
+                const float* v = aff + 24u * j;
+                for (int l = 0; l < 8; ++l) {
+                    const double p[3] = {(double)v[l], (double)v[8 + l], (double)v[16 + l]};
+                    if (!(__builtin_isfinite(p[0]) && __builtin_isfinite(p[1]) && __builtin_isfinite(p[2]))) continue;
+                    double dn = 0.0, df = 0.0;
+                    for (int k = 0; k < 3; ++k) {
+                        const double a = L[k] - p[k], b = p[k] - U[k];
+                        const double near = a > 0.0 ? a : (b > 0.0 ? b : 0.0);
+                        const double far = fmax(fabs(p[k] - L[k]), fabs(p[k] - U[k]));
+                        dn += near * near;
+                        df += far * far;
+                    }
+                    lmin = fmin(lmin, dn);
+                    hmin = fmin(hmin, df);
+                }
+            }
+            lo2 = fmin(lo2, lmin);
+            hi2 = fmax(hi2, hmin);  // an empty leaf: +inf, no hit bound
+            continue;
+        }
+        const int lv = 31 - __builtin_clz(n + 1u);
+        const float t = tests[n];
+        const int ax = lv % 3;
+        if (sp + 2 > 64) {
+            bounded = false;
+            break;
+        }
+        if (U[ax] >= (double)t) stack[sp++] = 2u * n + 2u;             // some a >= t
+        if (L[ax] < (double)t || t != t) stack[sp++] = 2u * n + 1u;    // some a < t (or NaN t)
+    }
+    uint32_t lq = 0u, hq = 0xFFFFu;
+    if (bounded) {
+        const double u = (double)g.unit;
+        const double lo = sqrt(lo2) / u, hi = sqrt(hi2) / u;
+        // round lo down and hi up by one extra unit: the double sqrt / divide may be an ulp off
+        lq = lo >= 65535.0 ? 65535u : (uint32_t)fmax(floor(lo) - 1.0, 0.0);
+        hq = hi + 1.0 < 65535.0 ? (uint32_t)ceil(hi) + 1u : 0xFFFFu;
+    }
+    ((uint2*)(base + g.cells_off))[cell] = make_uint2(lq | (hq << 16), node);
+}
+
+}  // namespace vgpu
+
+extern "C" hipError_t vgpu_launch_capt_grid(float* base, const vgpu::CaptGridArgs* g, hipStream_t st)
+{
+    const uint64_t n = (uint64_t)g->nx * g->ny * g->nz;
+    if (n == 0) return hipSuccess;
+    if (n >= ((uint64_t)1 << 31)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(vgpu::capt_grid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, *g);
+    return hipGetLastError();
+}

@@ -192,12 +192,20 @@ struct EnvView {
     int obs_lds;
 };
 constexpr int kAttHdr = 8;
-constexpr int kExtHdr = 16;
+constexpr int kExtHdr = 32;
 // heightfield header: x y z xs ys zs xd yd xd2 yd2 (floats) | data_off cells (uint32 bits)
 enum : int { HF_X = 0, HF_Y, HF_Z, HF_XS, HF_YS, HF_ZS, HF_XD, HF_YD, HF_XD2, HF_YD2, HF_OFF, HF_CELLS };
 // point-cloud (CAPT) header: top lower xyz, top upper xyz, r_point | nlog2, tests_off, aabbs_off,
 // starts_off, aff_off (uint32 bits).  aff = [n_aff][3][8] floats (x8 y8 z8), 16-B aligned.
-enum : int { PC_TOP = 0, PC_RPOINT = 6, PC_NLOG2 = 7, PC_TESTS, PC_AABBS, PC_STARTS, PC_AFF };
+// Device copies add the cell grid (vgpu_capt_grid.hip): origin xyz, 1/h, cell counts (uint32 and
+// float), the bound unit, and cells_off (0 = no grid; one uint2 per cell, x-fastest).
+enum : int {
+    PC_TOP = 0, PC_RPOINT = 6, PC_NLOG2 = 7, PC_TESTS, PC_AABBS, PC_STARTS, PC_AFF,
+    PC_GX = 12, PC_GY, PC_GZ, PC_GINVH, PC_GNX, PC_GNY, PC_GNZ, PC_GNXF, PC_GNYF, PC_GNZF, PC_GUNIT, PC_GCELLS
+};
+// Cell bounds are scaled by these before they decide a query (vgpu_capt_grid.hip: the float
+// rounding of the distance and of the bound itself is < 1e-6 relative)
+constexpr float kGridLoFac = 0.9999f, kGridHiFac = 1.0001f;
 
 // Robot base offsets of a staged pass (robots/panda/fk.hh:109-111, added to world-frame centres):
 // x y z of the robot -- and of the second arm, for the two-Panda composite's inter-arm checks
@@ -345,7 +353,7 @@ __device__ __forceinline__ bool hf_lane(const VGPU_CONST float* h, const float* 
 // LDS per workgroup: the descent's first L dependent loads become LDS reads instead of divergent
 // L2 gathers (SURVEY §8(a) a10 / north_star: "CAPT split planes staged in LDS").
 #ifndef VGPU_CAPT_LDS_LEVELS
-#define VGPU_CAPT_LDS_LEVELS 12
+#define VGPU_CAPT_LDS_LEVELS 0  // with the cell grid; 12 measured best without it (r02)
 #endif
 constexpr uint32_t kCaptLdsNodes = VGPU_CAPT_LDS_LEVELS > 0 ? (1u << VGPU_CAPT_LDS_LEVELS) - 1u : 1u;
 
@@ -375,6 +383,14 @@ __device__ __forceinline__ void capt_stage_lds(EnvView& env)
 // the implicit split tree (axis cycles x, y, z), leaf point-volume box test with
 // (r + r_point)^2, then the leaf's affordance vectors, inclusive distance test.  Sums of
 // squares in the FloatVector form fma(d0, d0, fma(d2, d2, d1 * d1)) (ref_probe "sql2").
+//
+// Cell grid (device copies, vgpu_capt_grid.hip): the centre's cell holds [lo, hi] -- over every
+// leaf the cell can descend to, the least distance from the cell to an affordance of that leaf,
+// and the largest over those leaves of the least farthest-corner distance to one -- and the
+// deepest split node whose region contains the whole cell.  (r + r_point)^2 below lo^2 is a miss
+// and above hi^2 a hit, whatever leaf the centre reaches (the leaf box always contains its
+// affordances, so its test never decides alone); anything between descends from that node.
+// Same answer as the reference's traversal, for ~5x fewer dependent loads per query.
 // lds_levels > 0: the tree's first lds_levels levels are read from capt_lds().
 __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float* __restrict__ base, float x, float y,
                                           float z, float r, int lds_levels = 0)
@@ -384,10 +400,34 @@ __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float
         return false;
     const int nlog2 = (int)hdr_u(h, PC_NLOG2);
     const float* __restrict__ tests = base + hdr_u(h, PC_TESTS);
+    const float rr = r + h[PC_RPOINT];
+    const float rc = rr * rr;
     uint32_t idx = 0;
-    float a = x, b = y, c = z;  // the axis of level i is i % 3
     int i = 0;
-    if (lds_levels > 0) {
+    const uint32_t goff = hdr_u(h, PC_GCELLS);
+    if (goff) {
+        const float fx = (x - h[PC_GX]) * h[PC_GINVH];
+        const float fy = (y - h[PC_GY]) * h[PC_GINVH];
+        const float fz = (z - h[PC_GZ]) * h[PC_GINVH];
+        if (fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < h[PC_GNXF] && fy < h[PC_GNYF] && fz < h[PC_GNZF]) {
+            const uint32_t cell =
+                ((uint32_t)fz * hdr_u(h, PC_GNY) + (uint32_t)fy) * hdr_u(h, PC_GNX) + (uint32_t)fx;
+            const uint2 rec = ((const uint2*)(base + goff))[cell];
+            const float lo = (float)(rec.x & 0xFFFFu) * h[PC_GUNIT];
+            if (rc < lo * lo * kGridLoFac) return false;
+            const uint32_t hq = rec.x >> 16;
+            const float hi = (float)hq * h[PC_GUNIT];
+            if (hq != 0xFFFFu && rc > hi * hi * kGridHiFac) return true;
+            idx = rec.y;
+            i = 31 - __builtin_clz(idx + 1u);  // the node's level
+        }
+    }
+    // the axis of level i is i % 3
+    const int rot = i % 3;
+    float a = rot == 0 ? x : (rot == 1 ? y : z);
+    float b = rot == 0 ? y : (rot == 1 ? z : x);
+    float c = rot == 0 ? z : (rot == 1 ? x : y);
+    if (lds_levels > i) {
         const float* top = capt_lds();
         for (; i < lds_levels; ++i) {
             idx = 2u * idx + 1u + ((a >= top[idx]) ? 1u : 0u);
@@ -406,8 +446,6 @@ __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float
     }
     const uint32_t leaf = nlog2 ? idx - ((1u << nlog2) - 1u) : 0u;
     const float* __restrict__ box = base + hdr_u(h, PC_AABBS) + 6u * leaf;
-    const float rr = r + h[PC_RPOINT];
-    const float rc = rr * rr;
     const float d0 = x - mm_min(mm_max(x, box[0]), box[3]);
     const float d1 = y - mm_min(mm_max(y, box[1]), box[4]);
     const float d2 = z - mm_min(mm_max(z, box[2]), box[5]);

@@ -42,7 +42,7 @@ def main():
         k = torch.from_numpy(k_np.view(np.int32)).to(dev)
         r = torch.from_numpy(r_np).to(dev)
         res = {}
-        for mode in ([2, 1] if n <= 400000 else [2]):
+        for mode in ([2, 1] if n <= int(os.environ.get("KNN_BRUTE_MAX", 400000)) else [2]):
             nbr = torch.zeros((n, kmax), dtype=torch.int32, device=dev)
             dd = torch.zeros((n, kmax), dtype=torch.float32, device=dev)
             cc = torch.zeros(n, dtype=torch.int32, device=dev)
