@@ -429,7 +429,7 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(n) / world, dev, world)
     # the kNN kernel alone (this rank's queries), HIP events on the launch stream, in both methods
     # of vgpu_set_knn_mode: brute force (the roofline: its flops are the ones executed) and the
-    # spatial index (auto's choice from 1e6 vertices; same lists, compared below)
+    # spatial index (auto's choice from 65536 vertices; same lists, compared below)
     nbr = torch.empty((max(qc, 1), kmax), dtype=torch.int32, device=dev)
     dd = torch.empty((max(qc, 1), kmax), dtype=torch.float32, device=dev)
     cc = torch.empty(max(qc, 1), dtype=torch.int32, device=dev)
@@ -510,7 +510,7 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                      "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
                      "traffic": None, "kernel_ms": knn_ms, "algorithmic_flops_per_vertex_pair": 24,
                      "vertex_pairs_rank0": pairs_scanned,
-                     "knn_ms": knn, "knn_mode_in_step": "index" if n >= 1_000_000 else "brute",
+                     "knn_ms": knn, "knn_mode_in_step": "index" if n >= 65536 else "brute",
                      "index_equals_brute": index_equals_brute,
                      "note": "roofline of the brute-force kernel (every pair evaluated); the index kernel's time is "
                              "beside it, not priced in flops (it skips pairs)"},

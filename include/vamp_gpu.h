@@ -218,7 +218,7 @@ int vgpu_prm_neighbor_params(int dim, double space_measure, double gamma_scale, 
 int vgpu_roadmap_knn(vgpu_ctx *ctx, int dim, const float *V, size_t n, const uint32_t *k, const float *r,
                      uint32_t kmax, uint32_t *nbr, float *dist, uint32_t *cnt);
 /* Neighbour-query method of the context: 0 auto (a spatial index -- Morton-sorted tiles with
- * box culling, vgpu_knn_index.hip -- from 1e6 vertices, else the brute-force scan), 1 brute
+ * box culling, vgpu_knn_index.hip -- from 65536 vertices, else the brute-force scan), 1 brute
  * force, 2 index.  Both give the same lists (the k smallest (distance, index) keys within r). */
 int vgpu_set_knn_mode(vgpu_ctx *ctx, int mode);
 /* The same for the queries q_first .. q_first+q_count-1 only (one rank's share of the edge

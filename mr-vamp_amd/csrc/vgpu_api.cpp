@@ -1864,7 +1864,7 @@ static bool knn_dim_ok(int dim) { return dim == 6 || dim == 7 || dim == 8 || dim
 // below this many vertices the brute-force scan is faster (MI355X, Fetch Halton vertices,
 // tools/knn_scale.py: 100k brute 11.8 / index 18.3 ms, 400k 95 / 104 ms, 2.7M index 1.40 s vs
 // ~4.3 s extrapolated brute)
-static constexpr size_t kKnnIndexMin = 1000000;
+static constexpr size_t kKnnIndexMin = 65536;  // group-query index: 3.6 vs 11.8 ms (brute) at 100k Fetch vertices
 
 extern "C" int vgpu_set_knn_mode(vgpu_ctx* c, int mode)
 {

@@ -9,7 +9,11 @@
 //   3. a stable radix sort of (key, vertex) -> perm (sorted position -> vertex);
 //   4. tiles of 64 consecutive sorted positions: the tile's coordinates (row-major, vertex
 //      order = sorted order), its axis-aligned box and its smallest vertex index.
-// Query: one wave = 64 queries that are consecutive in sorted order (spatially close).  The wave
+// Query (default, group_kernel below): one wave per 4 consecutive sorted queries, lane = candidate,
+// tiles culled per query through super-tile boxes -- MI355X, Fetch Halton vertices: 2.7M vertices
+// 219 ms vs 5433 ms brute force (1400 ms with the 64-query waves), 100k 3.6 vs 11.8 ms
+// (profiles/r03_knn_scale.log).
+// Query (VAMP_AMD_KNN_GROUP=0, query_kernel): one wave = 64 queries consecutive in sorted order.  The wave
 // visits the tiles outward from its own (home, home+1, home-1, ...) so its lists fill early;
 // a tile is skipped when no lane can take anything from it: its smallest vertex index is not
 // below the lane's vertex (the causal prefix), or the box's squared distance exceeds the lane's
@@ -24,6 +28,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "vgpu_device.hh"
 
@@ -337,10 +342,212 @@ __global__ __launch_bounds__(kQBlock) void query_kernel(const float* __restrict_
     }
 }
 
+// ---- group queries (the default): one wave per kGroup consecutive sorted queries ----------------
+// Each query's list lives across the wave (lane m holds its m-th key), candidates are one tile per
+// visit (lane = candidate), and tiles are culled PER QUERY of the group through a two-level box
+// hierarchy (super-tiles of kSuper tiles, then tiles): the 64-query waves above test every tile
+// and visit any tile one of 64 queries needs, which in 8-D is most of them.  Visiting order: the
+// home tile, the home super-tile, then the other super-tiles outward in chunks of 64 (one per
+// lane); a super-tile / tile is visited only if some query of the group can take from it.
+// Admission is the same full-key rule, so the lists are again exactly the brute force's.
+constexpr int kSuper = 64;  // tiles per super-tile
+
+// one wave per super-tile: the box of its tiles' boxes and their smallest vertex index
+template <int D>
+__global__ __launch_bounds__(64) void super_kernel(const float* __restrict__ tbox, const uint32_t* __restrict__ tmin,
+                                                   uint32_t T, float* __restrict__ sbox, uint32_t* __restrict__ smin)
+{
+    const uint32_t sp = blockIdx.x;
+    const uint32_t t = sp * kSuper + threadIdx.x;
+    const bool ok = t < T;
+    float lo[D], hi[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        lo[d] = wave_min(ok ? tbox[(size_t)t * 2 * D + d] : __builtin_inff());
+        hi[d] = wave_max(ok ? tbox[(size_t)t * 2 * D + D + d] : -__builtin_inff());
+    }
+    const uint32_t m = wave_umin(ok ? tmin[t] : 0xFFFFFFFFu);
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) {
+            sbox[(size_t)sp * 2 * D + d] = lo[d];
+            sbox[(size_t)sp * 2 * D + D + d] = hi[d];
+        }
+        smin[sp] = m;
+    }
+}
+
+template <int D>
+__device__ __forceinline__ float box_lb(const float* __restrict__ bx, const float* me)
+{
+    float lb = 0.0f;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float g = fmaxf(fmaxf(bx[d] - me[d], me[d] - bx[D + d]), 0.0f);
+        lb = __builtin_fmaf(g, g, lb);
+    }
+    return lb;
+}
+
+__device__ __forceinline__ float shfl_up1(float v) { return __shfl_up(v, 1, 64); }
+__device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1, 64); }
+
+template <int D, int QG>
+__global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict__ Vs, const uint32_t* __restrict__ perm,
+                                                        uint32_t n, uint32_t T, uint32_t S,
+                                                        const float* __restrict__ tbox,
+                                                        const uint32_t* __restrict__ tmin,
+                                                        const float* __restrict__ sbox,
+                                                        const uint32_t* __restrict__ smin,
+                                                        const uint32_t* __restrict__ qlist, uint32_t q_first,
+                                                        uint32_t q_count, const uint32_t* __restrict__ kq,
+                                                        const float* __restrict__ rq, uint32_t kmax,
+                                                        uint32_t* __restrict__ nbr, float* __restrict__ dist,
+                                                        uint32_t* __restrict__ cnt)
+{
+    const uint32_t wave = blockIdx.x * (kQBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t g0 = wave * QG;
+    if (g0 >= q_count) return;  // wave-uniform; the kernel has no block barrier
+    // the group's queries (wave-uniform values)
+    uint32_t qi[QG], kk[QG], c[QG], wi[QG];
+    float me[QG][D], wd[QG], thr[QG];
+    uint32_t p0 = 0;
+    // readfirstlane: the group's values are wave-uniform; kept in SGPRs they leave the VGPRs to the
+    // candidates (occupancy) -- the compiler cannot prove the loads uniform by itself
+    auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+    auto unf = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const uint32_t qo = g0 + q;
+        const bool inq = qo < q_count;
+        const uint32_t p = uni(inq ? (qlist ? qlist[qo] : qo) : 0u);
+        if (q == 0) p0 = p;
+        qi[q] = uni(inq ? perm[p] : 0xFFFFFFFFu);
+        const bool live = inq && qi[q] >= 2;  // vertices 0, 1 (start, goal) query nothing (prm.hh:228-233)
+#pragma unroll
+        for (int d = 0; d < D; ++d) me[q][d] = unf(inq ? Vs[(size_t)p * D + d] : 0.0f);
+        kk[q] = uni(live ? min(kq[qi[q]], 64u) : 0u);
+        wd[q] = unf(live ? rq[qi[q]] : -1.0f);  // admission bound: r while fewer than k are held, else the k-th key
+        wi[q] = 0xFFFFFFFFu;
+        c[q] = 0;
+        thr[q] = (live && kk[q]) ? wd[q] * wd[q] * 1.000001f : -1.0f;
+    }
+    // lane m holds key m of each query's list, ascending
+    float bd[QG];
+    uint32_t bi[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        bd[q] = __builtin_inff();
+        bi[q] = 0xFFFFFFFFu;
+    }
+    struct Cand {
+        float v[D];
+        uint32_t j;
+    };
+    auto load = [&](uint32_t t, Cand& cd) {
+        const uint32_t cp = t * kTile + lane;
+        const bool ok = cp < n;
+#pragma unroll
+        for (int d = 0; d < D; ++d) cd.v[d] = ok ? Vs[(size_t)cp * D + d] : 0.0f;
+        cd.j = ok ? perm[cp] : 0xFFFFFFFFu;  // a missing candidate is never < i
+    };
+    auto consider = [&](const Cand& cd) {
+        const float* cv = cd.v;
+        const uint32_t cj = cd.j;
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+            const float s = sumsq<D>(cv, me[q]);
+            uint64_t m = __builtin_amdgcn_ballot_w64(cj < qi[q] && s <= thr[q]);
+            if (m == 0ull) continue;
+            const float dl = __builtin_sqrtf(s);
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                const float d = bcast(dl, b);
+                const uint32_t j = bcast(cj, b);
+                // nn query semantics: distance <= r; once k are held, only a smaller key displaces the k-th
+                const bool take = c[q] < kk[q] ? d <= wd[q] : (d < wd[q] || (d == wd[q] && j < wi[q]));
+                if (!take) continue;
+                // every lane shuffles (a lane masked off by a short-circuit would not be read back)
+                const uint32_t lt = (d < bd[q] || (d == bd[q] && j < bi[q])) ? 1u : 0u;
+                const float pd = shfl_up1(bd[q]);
+                const uint32_t pi = shfl_up1(bi[q]);
+                const uint32_t plt_raw = shfl_up1(lt);
+                const bool plt = lane > 0 && plt_raw != 0u;
+                bd[q] = lt ? (plt ? pd : d) : bd[q];
+                bi[q] = lt ? (plt ? pi : j) : bi[q];
+                c[q] = min(c[q] + 1u, kk[q]);
+                if (c[q] == kk[q]) {
+                    wd[q] = bcast(bd[q], kk[q] - 1u);
+                    wi[q] = bcast(bi[q], kk[q] - 1u);
+                    thr[q] = wd[q] * wd[q] * 1.000001f;
+                }
+            }
+        }
+    };
+    // does some query of the group need the box (smallest index mn)?
+    auto need_box = [&](const float* __restrict__ bx, uint32_t mn) {
+        bool need = false;
+#pragma unroll
+        for (int q = 0; q < QG; ++q) need |= mn < qi[q] && box_lb<D>(bx, me[q]) <= thr[q] * 1.0001f;
+        return need;
+    };
+    // all needed tiles of super-tile sp except `skip`, the next tile's candidates loaded while the
+    // current one is tested
+    auto visit_super = [&](uint32_t sp, uint32_t skip) {
+        const uint32_t t = sp * kSuper + lane;
+        const bool need = t < T && t != skip && need_box(tbox + (size_t)t * 2 * D, tmin[t]);
+        uint64_t m = __builtin_amdgcn_ballot_w64(need);
+        if (m == 0ull) return;
+        Cand cur, nxt;
+        load(sp * kSuper + (uint32_t)__builtin_ctzll(m), cur);
+        m &= m - 1ull;
+        for (;;) {
+            const bool more = m != 0ull;
+            if (more) load(sp * kSuper + (uint32_t)__builtin_ctzll(m), nxt);
+            consider(cur);
+            if (!more) break;
+            m &= m - 1ull;
+            cur = nxt;
+        }
+    };
+    const uint32_t home_t = p0 / kTile, home_s = home_t / kSuper;
+    {
+        Cand h;
+        load(home_t, h);
+        consider(h);
+    }
+    visit_super(home_s, home_t);
+    const uint32_t chunks = (S + 63) / 64, home_c = home_s / 64;
+    for (uint32_t st = 0; st < 2 * chunks; ++st) {
+        const int64_t c64 = (st & 1u) ? (int64_t)home_c - (int64_t)((st + 1) / 2) : (int64_t)home_c + (int64_t)(st / 2);
+        if (c64 < 0 || c64 >= (int64_t)chunks) continue;
+        const uint32_t sp = (uint32_t)c64 * 64 + lane;
+        const bool need = sp < S && sp != home_s && need_box(sbox + (size_t)sp * 2 * D, smin[sp]);
+        uint64_t m = __builtin_amdgcn_ballot_w64(need);
+        while (m) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            visit_super((uint32_t)c64 * 64 + b, 0xFFFFFFFFu);
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        if (g0 + q >= q_count) break;
+        const size_t o = (size_t)(qi[q] - q_first);
+        if (lane == 0) cnt[o] = c[q];
+        if (lane < c[q]) {
+            nbr[o * kmax + lane] = bi[q];
+            dist[o * kmax + lane] = bd[q];
+        }
+    }
+}
+
 inline size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct Layout {
-    size_t part, ls, key0, key1, id0, perm, Vs, tbox, tmin, flag, qlist, nsel, tmp, total;
+    size_t part, ls, key0, key1, id0, perm, Vs, tbox, tmin, sbox, smin, flag, qlist, nsel, tmp, total;
 };
 
 template <int D>
@@ -370,6 +577,9 @@ hipError_t layout(uint32_t n, uint32_t q_count, Layout& L)
     L.Vs = take((size_t)n * D * 4);
     L.tbox = take((size_t)T * 2 * D * 4);
     L.tmin = take((size_t)T * 4);
+    const uint32_t S = (T + kSuper - 1) / kSuper;
+    L.sbox = take((size_t)S * 2 * D * 4);
+    L.smin = take((size_t)S * 4);
     L.flag = take(n);
     L.qlist = take((size_t)q_count * 4);
     L.nsel = take(4);
@@ -380,7 +590,8 @@ hipError_t layout(uint32_t n, uint32_t q_count, Layout& L)
 
 template <int D, int K>
 hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, const uint32_t* k, const float* r,
-               uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, char* pool, size_t pool_bytes, hipStream_t st)
+               uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, char* pool, size_t pool_bytes, int group,
+               hipStream_t st)
 {
     Layout L;
     hipError_t e = layout<D>(n, q_count, L);
@@ -424,20 +635,43 @@ hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, c
         if (e != hipSuccess) return e;
         ql = qlist;  // exactly q_count entries: perm is a permutation of 0 .. n-1
     }
-    const unsigned grid = (unsigned)((q_count + kQBlock - 1) / kQBlock);
-    hipLaunchKernelGGL((query_kernel<D, K>), dim3(grid), dim3(kQBlock), 0, st, Vs, perm, n, T, tbox, tmin, ql, q_first,
-                       q_count, k, r, kmax, nbr, dist, cnt);
+    if (group <= 0) {  // the 64-query waves (VAMP_AMD_KNN_GROUP=0, for A/B runs)
+        const unsigned grid = (unsigned)((q_count + kQBlock - 1) / kQBlock);
+        hipLaunchKernelGGL((query_kernel<D, K>), dim3(grid), dim3(kQBlock), 0, st, Vs, perm, n, T, tbox, tmin, ql,
+                           q_first, q_count, k, r, kmax, nbr, dist, cnt);
+        return hipGetLastError();
+    }
+    const uint32_t S = (T + kSuper - 1) / kSuper;
+    float* sbox = (float*)(pool + L.sbox);
+    uint32_t* smin = (uint32_t*)(pool + L.smin);
+    hipLaunchKernelGGL((super_kernel<D>), dim3(S), dim3(64), 0, st, tbox, tmin, T, sbox, smin);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint32_t QG = group >= 8 ? 8 : (group >= 4 ? 4 : (group >= 2 ? 2 : 1));
+    const uint64_t waves = (q_count + QG - 1) / QG;
+    const unsigned grid = (unsigned)((waves + kQBlock / 64 - 1) / (kQBlock / 64));
+#define VGPU_KNN_GROUP_LAUNCH(Q)                                                                                      \
+    hipLaunchKernelGGL((group_kernel<D, Q>), dim3(grid), dim3(kQBlock), 0, st, Vs, perm, n, T, S, tbox, tmin, sbox, \
+                       smin, ql, q_first, q_count, k, r, kmax, nbr, dist, cnt)
+    switch (QG) {
+    case 1: VGPU_KNN_GROUP_LAUNCH(1); break;
+    case 2: VGPU_KNN_GROUP_LAUNCH(2); break;
+    case 4: VGPU_KNN_GROUP_LAUNCH(4); break;
+    default: VGPU_KNN_GROUP_LAUNCH(8); break;
+    }
+#undef VGPU_KNN_GROUP_LAUNCH
     return hipGetLastError();
 }
 
 template <int D>
 hipError_t run_dim(const float* V, uint32_t n, uint32_t qf, uint32_t qc, const uint32_t* k, const float* r,
-                   uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, char* pool, size_t pb, hipStream_t st)
+                   uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, char* pool, size_t pb, int g,
+                   hipStream_t st)
 {
-    if (kmax <= 16) return run<D, 16>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, st);
-    if (kmax <= 32) return run<D, 32>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, st);
-    if (kmax <= 48) return run<D, 48>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, st);
-    return run<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, st);
+    if (g > 0) return run<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);  // K unused
+    if (kmax <= 16) return run<D, 16>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);
+    if (kmax <= 32) return run<D, 32>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);
+    if (kmax <= 48) return run<D, 48>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);
+    return run<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);
 }
 
 }  // namespace knnidx
@@ -468,11 +702,16 @@ hipError_t vgpu_launch_knn_index(int dim, const float* V, uint32_t n, uint32_t q
 {
     using namespace vgpu::knnidx;
     char* p = (char*)pool;
+    // queries per wave of the group kernel (VAMP_AMD_KNN_GROUP: 1, 2, 4 or 8; 0 = the 64-query waves)
+    static const int g = [] {
+        const char* s = std::getenv("VAMP_AMD_KNN_GROUP");
+        return s ? std::atoi(s) : 4;
+    }();
     switch (dim) {
-    case 6: return run_dim<6>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, st);
-    case 7: return run_dim<7>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, st);
-    case 8: return run_dim<8>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, st);
-    case 14: return run_dim<14>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, st);
+    case 6: return run_dim<6>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, st);
+    case 7: return run_dim<7>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, st);
+    case 8: return run_dim<8>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, st);
+    case 14: return run_dim<14>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, st);
     default: return hipErrorInvalidValue;
     }
 }

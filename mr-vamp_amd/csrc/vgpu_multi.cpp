@@ -153,7 +153,7 @@ extern "C" int vgpu_multi_sample_fkcc_host(vgpu_multi* m, const vgpu_robot* r, v
         vgpu_shard_range(n_draws, i, w, &lo, &cnt);
         if (!cnt) return VGPU_OK;
         vgpu_ctx* c = m->ctx[i];
-        hipSetDevice(m->device[i]);
+        if (hipSetDevice(m->device[i]) != hipSuccess) return VGPU_ERR_HIP;
         float *q = nullptr, *ro = nullptr;
         uint8_t* v = nullptr;
         uint32_t* ix = nullptr;

@@ -145,7 +145,7 @@ def test_knn_index_halton_ties_and_ranges(vamp, oracle):
 def test_knn_index_equals_brute_force_large(vamp, oracle, n):
     """Beyond the oracle's reach in a test, the indexed query equals the GPU brute force (which equals
     the oracle at the smaller sizes above) -- at 2e5 and at 1.3e6 Fetch vertices, the regime where
-    the auto mode picks the index (include/vamp_gpu.h vgpu_set_knn_mode: from 1e6)."""
+    the auto mode picks the index (include/vamp_gpu.h vgpu_set_knn_mode: from 65536)."""
     import time
     V = vamp.fetch.scale_configuration(vamp.halton(8, 1, n))
     sm = oracle.SPACE_MEASURE["fetch"]
