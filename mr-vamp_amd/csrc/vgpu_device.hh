@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #define VGPU_CONST __attribute__((address_space(4)))
 
 // ---- group reductions -----------------------------------------------------------------
@@ -85,6 +87,27 @@ struct Grp8 {
         return __uint_as_float(u);
     }
 };
+
+// Groups of the staged kernels with a point cloud: CAPT queries the cell grid cannot decide are
+// queued per wave and resolved in batches (capt_defer_* below) instead of inline.  TAG = the queue
+// tag of env_bits calls that pass none: -1 resolves them inline (bound kernels: their generated
+// calls pass the check's bit), kChildTag marks "a child of this lane hit" (children kernels).
+template <class G, int TAG>
+struct Deferred : G {
+    static constexpr int kDeferTag = TAG;
+};
+template <class G, class = void>
+struct DeferTagOf {
+    static constexpr bool on = false;
+    static constexpr int tag = -1;
+};
+template <class G>
+struct DeferTagOf<G, std::void_t<decltype(G::kDeferTag)>> {
+    static constexpr bool on = true;
+    static constexpr int tag = G::kDeferTag;
+};
+constexpr int kChildTag = 63;
+constexpr int kTagDefault = -2;  // env_bits: the group type's default tag
 
 // ---- FloatVector::sin()/cos() -----------------------------------------------------------
 __device__ __forceinline__ float vamp_sin(float x)
@@ -392,18 +415,15 @@ __device__ __forceinline__ void capt_stage_lds(EnvView& env)
 // affordances, so its test never decides alone); anything between descends from that node.
 // Same answer as the reference's traversal, for ~5x fewer dependent loads per query.
 // lds_levels > 0: the tree's first lds_levels levels are read from capt_lds().
-__device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float* __restrict__ base, float x, float y,
-                                          float z, float r, int lds_levels = 0)
+// Top box + cell grid: 0 = miss, 1 = hit, 2 = undecided -- node = the split node the traversal
+// starts from (0: the root, without a grid or outside it).
+__device__ __forceinline__ int capt_decide(const VGPU_CONST float* h, float x, float y, float z, float r,
+                                           const float* __restrict__ base, uint32_t& node)
 {
+    node = 0u;
     if (!((x + r >= h[0]) && (x - r <= h[3]) && (y + r >= h[1]) && (y - r <= h[4]) && (z + r >= h[2]) &&
           (z - r <= h[5])))
-        return false;
-    const int nlog2 = (int)hdr_u(h, PC_NLOG2);
-    const float* __restrict__ tests = base + hdr_u(h, PC_TESTS);
-    const float rr = r + h[PC_RPOINT];
-    const float rc = rr * rr;
-    uint32_t idx = 0;
-    int i = 0;
+        return 0;
     const uint32_t goff = hdr_u(h, PC_GCELLS);
     if (goff) {
         const float fx = (x - h[PC_GX]) * h[PC_GINVH];
@@ -413,16 +433,30 @@ __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float
             const uint32_t cell =
                 ((uint32_t)fz * hdr_u(h, PC_GNY) + (uint32_t)fy) * hdr_u(h, PC_GNX) + (uint32_t)fx;
             const uint2 rec = ((const uint2*)(base + goff))[cell];
+            const float rr = r + h[PC_RPOINT];
+            const float rc = rr * rr;
             const float lo = (float)(rec.x & 0xFFFFu) * h[PC_GUNIT];
-            if (rc < lo * lo * kGridLoFac) return false;
+            if (rc < lo * lo * kGridLoFac) return 0;
             const uint32_t hq = rec.x >> 16;
             const float hi = (float)hq * h[PC_GUNIT];
-            if (hq != 0xFFFFu && rc > hi * hi * kGridHiFac) return true;
-            idx = rec.y;
-            i = 31 - __builtin_clz(idx + 1u);  // the node's level
+            if (hq != 0xFFFFu && rc > hi * hi * kGridHiFac) return 1;
+            node = rec.y;
         }
     }
-    // the axis of level i is i % 3
+    return 2;
+}
+
+// The reference's traversal below `node` (whose region contains the centre): descent, leaf box,
+// affordance scan.
+__device__ __forceinline__ bool capt_resolve(const VGPU_CONST float* h, const float* __restrict__ base, float x,
+                                             float y, float z, float r, uint32_t node, int lds_levels = 0)
+{
+    const int nlog2 = (int)hdr_u(h, PC_NLOG2);
+    const float* __restrict__ tests = base + hdr_u(h, PC_TESTS);
+    const float rr = r + h[PC_RPOINT];
+    const float rc = rr * rr;
+    uint32_t idx = node;
+    int i = 31 - __builtin_clz(idx + 1u);  // the node's level; the axis of level i is i % 3
     const int rot = i % 3;
     float a = rot == 0 ? x : (rot == 1 ? y : z);
     float b = rot == 0 ? y : (rot == 1 ? z : x);
@@ -470,6 +504,109 @@ __device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float
     return false;
 }
 
+__device__ __forceinline__ bool capt_lane(const VGPU_CONST float* h, const float* __restrict__ base, float x, float y,
+                                          float z, float r, int lds_levels = 0)
+{
+    uint32_t node;
+    const int d = capt_decide(h, x, y, z, r, base, node);
+    return d == 2 ? capt_resolve(h, base, x, y, z, r, node, lds_levels) : d == 1;
+}
+
+// ---- deferred CAPT queries (staged kernels, kStagedBlock = 256 threads = 4 waves) ----------------
+// A wave appends its undecided queries (centre, radius, start node, owner thread, tag, cloud) to
+// its LDS queue; when a push would overflow, and at the end of the kernel's collision work, the
+// whole wave resolves the queue one entry per lane (capt_defer_flush), OR-ing a hit into the
+// owner's 64-bit tag mask.  Divergent single-lane traversals become full-wave batches.
+constexpr int kDeferCap = 128;
+constexpr int kDeferWaves = 4;
+struct DeferQ {
+    float x[kDeferCap], y[kDeferCap], z[kDeferCap], r[kDeferCap];
+    uint32_t node[kDeferCap], meta[kDeferCap];  // meta: owner thread | tag << 8 | cloud << 14
+};
+__device__ __forceinline__ DeferQ* defer_q()
+{
+    __shared__ DeferQ q[kDeferWaves];
+    return q;
+}
+__device__ __forceinline__ uint32_t* defer_cnt()
+{
+    __shared__ uint32_t c[kDeferWaves];
+    return c;
+}
+__device__ __forceinline__ unsigned long long* defer_hits()
+{
+    __shared__ unsigned long long m[kDeferWaves * 64];
+    return m;
+}
+// every thread of the block, before any return
+__device__ __forceinline__ void capt_defer_init()
+{
+    defer_hits()[threadIdx.x] = 0ull;
+    if ((threadIdx.x & 63) == 0) defer_cnt()[threadIdx.x >> 6] = 0u;
+    __builtin_amdgcn_wave_barrier();
+}
+// the active lanes of the wave resolve every queued entry
+__device__ __attribute__((noinline)) void capt_defer_flush(const VGPU_CONST float* pc, const float* base,
+                                                           int lds_levels)
+{
+    const uint32_t w = threadIdx.x >> 6;
+    DeferQ& q = defer_q()[w];
+    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)defer_cnt()[w]);
+    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+    const uint32_t na = (uint32_t)__builtin_popcountll(act);
+    const uint32_t rk = (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32),
+                                                            __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
+    for (uint32_t b = 0; b < cnt; b += na) {
+        const uint32_t i = b + rk;
+        if (i < cnt) {
+            const uint32_t meta = q.meta[i];
+            const uint32_t cloud = meta >> 14;
+            if (capt_resolve(pc + kExtHdr * cloud, base, q.x[i], q.y[i], q.z[i], q.r[i], q.node[i],
+                             cloud == 0 ? lds_levels : 0))
+                atomicOr(&defer_hits()[(w << 6) | (meta & 63u)], 1ull << ((meta >> 8) & 63u));
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (rk == 0) defer_cnt()[w] = 0u;
+    __builtin_amdgcn_wave_barrier();
+}
+__device__ __forceinline__ void capt_defer_push(bool pend, int tag, int cloud, float x, float y, float z, float r,
+                                                uint32_t node, const VGPU_CONST float* pc, const float* base,
+                                                int lds_levels)
+{
+    const uint64_t pm = __builtin_amdgcn_ballot_w64(pend);
+    if (pm == 0ull) return;
+    const uint32_t w = threadIdx.x >> 6;
+    uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)defer_cnt()[w]);
+    const uint32_t np = (uint32_t)__builtin_popcountll(pm);
+    if (c0 + np > (uint32_t)kDeferCap) {
+        capt_defer_flush(pc, base, lds_levels);
+        c0 = 0u;
+    }
+    if (pend) {
+        const uint32_t pos = c0 + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+        DeferQ& q = defer_q()[w];
+        q.x[pos] = x;
+        q.y[pos] = y;
+        q.z[pos] = z;
+        q.r[pos] = r;
+        q.node[pos] = node;
+        q.meta[pos] = (threadIdx.x & 63u) | ((uint32_t)tag << 8) | ((uint32_t)cloud << 14);
+    }
+    __builtin_amdgcn_wave_barrier();
+    defer_cnt()[w] = c0 + np;  // every active lane stores the same value
+    __builtin_amdgcn_wave_barrier();
+}
+// resolve what is left; this lane's tag mask
+__device__ __forceinline__ uint64_t capt_defer_finish(const VGPU_CONST float* pc, const float* base, int lds_levels)
+{
+    const uint32_t w = threadIdx.x >> 6;
+    if (__builtin_amdgcn_readfirstlane((int)defer_cnt()[w]) != 0) capt_defer_flush(pc, base, lds_levels);
+    __builtin_amdgcn_wave_barrier();
+    return defer_hits()[threadIdx.x];
+}
+
 #ifndef VGPU_ENV_LDS_FLOATS
 #define VGPU_ENV_LDS_FLOATS 4096
 #endif
@@ -511,8 +648,10 @@ __device__ __forceinline__ uint32_t scan_env_type(const EnvView& env, float emax
 
 // Returns acc with this lane's hits OR-ed into the sign bit.  A lane entering with its sign
 // bit already set (an earlier child hit) does not keep any obstacle loop alive.
+// tag: the deferred-query tag (kTagDefault: the group type's; bound kernels pass the check's bit)
 template <class Grp, bool EXT = false>
-__device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float y, float z, float r, uint32_t acc = 0u)
+__device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float y, float z, float r, uint32_t acc = 0u,
+                                             int tag = kTagDefault)
 {
     const float d = dot3(x, y, z, x, y, z);
     float me = sqrt_host(d, env.lut, env.kbits) + r;  // validity.hh:55-59
@@ -565,8 +704,20 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
         bool hit = (acc >> 31) != 0u;
         for (int i = 0; i < env.n_hf; ++i)
             if (!hit) hit = hf_lane(env.hf + kExtHdr * i, env.base, x, y, z, r);
-        for (int i = 0; i < env.n_pc; ++i)
-            if (!hit) hit = capt_lane(env.pc + kExtHdr * i, env.base, x, y, z, r, i == 0 ? env.pc_lds_levels : 0);
+        const int dtag = tag == kTagDefault ? DeferTagOf<Grp>::tag : tag;
+        if (DeferTagOf<Grp>::on && dtag >= 0) {
+            // undecided queries are queued under dtag; a hit found later is OR-ed by the kernel
+            for (int i = 0; i < env.n_pc; ++i) {
+                uint32_t node = 0u;
+                int d = 0;
+                if (!hit) d = capt_decide(env.pc + kExtHdr * i, x, y, z, r, env.base, node);
+                if (d == 1) hit = true;
+                capt_defer_push(d == 2, dtag, i, x, y, z, r, node, env.pc, env.base, env.pc_lds_levels);
+            }
+        } else {
+            for (int i = 0; i < env.n_pc; ++i)
+                if (!hit) hit = capt_lane(env.pc + kExtHdr * i, env.base, x, y, z, r, i == 0 ? env.pc_lds_levels : 0);
+        }
         if (hit) acc |= 0x80000000u;
     }
     return acc;

@@ -173,6 +173,19 @@ struct GrpOf<8> {
     using T = Grp8;
 };
 
+// the group type of a staged kernel: with a point cloud (EXT), undecided CAPT queries are deferred
+// (vgpu_device.hh capt_defer_*) -- in bound kernels under each check's bit (the generated calls pass
+// it), in children kernels under kChildTag
+template <int G, bool EXT, int TAG>
+using StagedGrp = std::conditional_t<EXT, Deferred<typename GrpOf<G>::T, TAG>, typename GrpOf<G>::T>;
+
+// OR of a 64-bit per-lane mask over the lane's group
+template <class Grp>
+__device__ __forceinline__ uint64_t group_or64(uint64_t v)
+{
+    return ((uint64_t)Grp::or_bits((uint32_t)(v >> 32)) << 32) | (uint64_t)Grp::or_bits((uint32_t)v);
+}
+
 template <class M>
 __device__ __forceinline__ int mask_ctz(M a)
 {
@@ -224,8 +237,11 @@ __global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void bound_kernel(Src
                                                                              typename R::Mask* __restrict__ mask,
                                                                              uint8_t* __restrict__ valid)
 {
-    using Grp = typename GrpOf<Src::G>::T;
-    if constexpr (EXT) capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
+    using Grp = StagedGrp<Src::G, EXT, -1>;
+    if constexpr (EXT) {
+        capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
+        capt_defer_init();
+    }
 #ifdef VGPU_ENV_LDS
     env_stage_lds(env);
 #endif
@@ -247,7 +263,8 @@ __global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void bound_kernel(Src
             for (int j = 0; j < R::D; ++j) src.q_out[R::D * (size_t)g + j] = v[j];
         }
     }
-    const typename R::Mask m = R::template bound<Grp, EXT>(v, env, bs);
+    typename R::Mask m = R::template bound<Grp, EXT>(v, env, bs);
+    if constexpr (EXT) m |= (typename R::Mask)group_or64<Grp>(capt_defer_finish(env.pc, env.base, env.pc_lds_levels));
     if (lane == 0) {
         mask[g] = m;
         if constexpr (Src::kInit) {
@@ -371,8 +388,11 @@ __global__ __launch_bounds__(kStagedBlock, ChildClasses<R>::waves(K)) void child
     Src src, const StagedPlan* __restrict__ plan, const uint32_t* __restrict__ items, EnvView env, Bases bs,
     uint8_t* __restrict__ valid)
 {
-    using Grp = typename GrpOf<Src::G>::T;
-    if constexpr (EXT) capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
+    using Grp = StagedGrp<Src::G, EXT, kChildTag>;
+    if constexpr (EXT) {
+        capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
+        capt_defer_init();
+    }
 #ifdef VGPU_ENV_LDS
     env_stage_lds(env);
 #endif
@@ -391,7 +411,8 @@ __global__ __launch_bounds__(kStagedBlock, ChildClasses<R>::waves(K)) void child
     const uint32_t g = items[item];
     float v[R::D];
     src.load(g, lane, v);
-    const bool hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bs) > 0;
+    bool hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bs) > 0;
+    if constexpr (EXT) hit = Grp::any(capt_defer_finish(env.pc, env.base, env.pc_lds_levels) != 0ull) || hit;
     if (hit && lane == 0) valid[src.out(g)] = 0;  // every writer stores 0: the race is benign
 }
 

@@ -776,8 +776,8 @@ class RobotGen:
             gated = {c: b for b, c in enumerate(gate["checks"])}
         for c, o in enumerate(order):
             kind, test, ck = self.bound_test(fr, o)
-            if kind == "env":
-                E.raw(f"if (Grp::any_bits({test})) mask |= {one} << {c};")
+            if kind == "env":  # the check's bit is its deferred-query tag (vgpu_device.hh capt_defer_*)
+                E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c}))) mask |= {one} << {c};")
             elif c in gated:
                 E.raw(f"if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c};")
             else:
@@ -842,8 +842,8 @@ class RobotGen:
             E.raw("uint64_t mask = 0u;")
             for c in range(k, min(k + chunk, len(order))):
                 kind, test, ck = self.bound_test(fr, order[c])
-                if kind == "env":
-                    E.raw(f"if (Grp::any_bits({test})) mask |= 1ull << {c - k};")
+                if kind == "env":  # the check's bit in the chunk mask is its deferred-query tag
+                    E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c - k}))) mask |= 1ull << {c - k};")
                 else:
                     E.raw(f"if (Grp::any({test})) mask |= 1ull << {c - k};")
             E.raw("return mask;")
@@ -854,6 +854,19 @@ class RobotGen:
                    ", ".join(f"{e:#x}ull" for e in envs) + "};")
         out += self.staged_children(order)
         return "\n".join(out)
+
+
+def gen_radii(paths) -> str:
+    """Host-and-device table of every robot's collision-sphere radii (reference order, the
+    Spheres<rake>::r of Robot::sphere_fk): used where a kernel needs the radii next to
+    sphere_fk's centres (filter_robot_from_pointcloud, bindings/common.hh:36-87)."""
+    out = ["// GENERATED by tools/gen_kernels.py --radii from model/*.json -- do not edit.", "#pragma once", ""]
+    for path in paths:
+        m = json.load(open(path))
+        vals = ", ".join(flit(sp["radius"]) for sp in m["spheres"])
+        out.append(f"constexpr int {m['robot']}_n_spheres_table = {len(m['spheres'])};")
+        out.append(f"constexpr float {m['robot']}_sphere_radii[{len(m['spheres'])}] = {{{vals}}};")
+    return "\n".join(out) + "\n"
 
 
 def main():
