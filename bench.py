@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--oracle-edges", type=int, default=1 << 18,
                     help="edges checked against the scalar oracle (the CPU rake checks every edge)")
     ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     ap.add_argument("--workload", default="validate",
                     choices=["validate", "capt", "fetch_prm", "prm_edges", "pair", "rrtc"],
                     help="validate: BASELINE configs[1] (the headline); capt: configs[2]; fetch_prm: configs[3] "
@@ -817,7 +817,7 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     # (2 * FETCH_SIZE + WRITE_SIZE) KB of the bound + children kernels (FETCH_SIZE doubled per
     # MI355X_MICROARCH.md; gathers are narrower than the streaming reads it was calibrated on, so
     # this is an upper estimate), plus their L2 hit rates
-    pmc = traffic_record(os.path.join(ROOT, "profiles", "r02_capt_pmc.json"))
+    pmc = traffic_record(os.path.join(ROOT, "profiles", "r03_capt_pmc.json"))
     traffic, l2 = None, None
     if pmc:
         ks = [v for k, v in pmc["kernels"].items() if k.startswith(("bound_kernel", "children_kernel"))]
@@ -833,10 +833,12 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         {"kernel": "fkcc (staged, point-cloud ext path)", "bound": "valu", "achieved": achieved,
          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
          "algorithmic_flops_per_config": f_cfg, "step_ms": kern_s * 1e3, "l2_hit_rate": l2,
-         "traffic_source": "profiles/r02_capt_pmc.json (tools/gpu_capt_pmc.sh: rocprofv3 --pmc FETCH_SIZE, "
+         "traffic_source": "profiles/r03_capt_pmc.json (tools/gpu_capt_pmc.sh: rocprofv3 --pmc FETCH_SIZE, "
                            "WRITE_SIZE, TCC_HIT_sum/TCC_MISS_sum in separate passes)",
-         "note": "gather/latency-bound descent + affordance scan; split tree's top 12 levels staged in LDS per "
-                 "workgroup; CAPT arrays (~4.7 MB) L2/MALL resident"},
+         "note": "latency-bound gathers, not FLOPs: the cell grid (vgpu_capt_grid.hip) decides most sphere queries "
+                 "with one dependent 8-B load after the sphere's FK; undecided ones are queued per wave in LDS and "
+                 "resolved a full wave at a time (descent from the cell's node, leaf box, affordance scan: "
+                 "~3-8 dependent L2 loads); CAPT arrays + grid (~21 MB) L2/MALL resident"},
         cpu)
     line["parity"] = parity
     line["raw_queries"] = {

@@ -545,9 +545,8 @@ __device__ __forceinline__ void capt_defer_init()
     if ((threadIdx.x & 63) == 0) defer_cnt()[threadIdx.x >> 6] = 0u;
     __builtin_amdgcn_wave_barrier();
 }
-// the active lanes of the wave resolve every queued entry
-__device__ __attribute__((noinline)) void capt_defer_flush(const VGPU_CONST float* pc, const float* base,
-                                                           int lds_levels)
+// the active lanes of the wave resolve every queued entry (once per kernel, at the end)
+__device__ __forceinline__ void capt_defer_flush(const VGPU_CONST float* pc, const float* base, int lds_levels)
 {
     const uint32_t w = threadIdx.x >> 6;
     DeferQ& q = defer_q()[w];
@@ -570,19 +569,19 @@ __device__ __attribute__((noinline)) void capt_defer_flush(const VGPU_CONST floa
     if (rk == 0) defer_cnt()[w] = 0u;
     __builtin_amdgcn_wave_barrier();
 }
-__device__ __forceinline__ void capt_defer_push(bool pend, int tag, int cloud, float x, float y, float z, float r,
+// queue this lane's undecided query; returns its hit when the queue is full and it was resolved here
+// instead (rare: no call, no flush inside the generated code -- a call would cost every kernel a stack)
+__device__ __forceinline__ bool capt_defer_push(bool pend, int tag, int cloud, float x, float y, float z, float r,
                                                 uint32_t node, const VGPU_CONST float* pc, const float* base,
                                                 int lds_levels)
 {
     const uint64_t pm = __builtin_amdgcn_ballot_w64(pend);
-    if (pm == 0ull) return;
+    if (pm == 0ull) return false;
     const uint32_t w = threadIdx.x >> 6;
-    uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)defer_cnt()[w]);
+    const uint32_t c0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)defer_cnt()[w]);
     const uint32_t np = (uint32_t)__builtin_popcountll(pm);
-    if (c0 + np > (uint32_t)kDeferCap) {
-        capt_defer_flush(pc, base, lds_levels);
-        c0 = 0u;
-    }
+    if (c0 + np > (uint32_t)kDeferCap)
+        return pend && capt_resolve(pc + kExtHdr * cloud, base, x, y, z, r, node, cloud == 0 ? lds_levels : 0);
     if (pend) {
         const uint32_t pos = c0 + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
                                                                      __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
@@ -597,6 +596,7 @@ __device__ __forceinline__ void capt_defer_push(bool pend, int tag, int cloud, f
     __builtin_amdgcn_wave_barrier();
     defer_cnt()[w] = c0 + np;  // every active lane stores the same value
     __builtin_amdgcn_wave_barrier();
+    return false;
 }
 // resolve what is left; this lane's tag mask
 __device__ __forceinline__ uint64_t capt_defer_finish(const VGPU_CONST float* pc, const float* base, int lds_levels)
@@ -712,7 +712,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
                 int d = 0;
                 if (!hit) d = capt_decide(env.pc + kExtHdr * i, x, y, z, r, env.base, node);
                 if (d == 1) hit = true;
-                capt_defer_push(d == 2, dtag, i, x, y, z, r, node, env.pc, env.base, env.pc_lds_levels);
+                if (capt_defer_push(d == 2, dtag, i, x, y, z, r, node, env.pc, env.base, env.pc_lds_levels)) hit = true;
             }
         } else {
             for (int i = 0; i < env.n_pc; ++i)

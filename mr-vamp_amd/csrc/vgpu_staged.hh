@@ -67,6 +67,17 @@ struct ChildClasses<R, std::void_t<decltype(R::kClassOf)>> {
     __host__ __device__ static constexpr int waves(int k) { return R::kClassWaves[k]; }
 };
 
+// waves/EU of a children kernel: with a point cloud (EXT) at most VGPU_EXT_CHILD_WAVES -- the deferred
+// queries' queue bookkeeping would spill at 8 (64 VGPRs)
+#ifndef VGPU_EXT_CHILD_WAVES
+#define VGPU_EXT_CHILD_WAVES 7
+#endif
+template <class R, int K, bool EXT>
+struct ChildWaves {
+    static constexpr int w = ChildClasses<R>::waves(K);
+    static constexpr int v = (EXT && w > VGPU_EXT_CHILD_WAVES) ? VGPU_EXT_CHILD_WAVES : w;
+};
+
 // Source kinds a robot's staged exports instantiate (bit k = kind k of StagedHost::with_source): all
 // by default; a robot may restrict them with R::kSourceKinds (the composite has no sampler and no
 // full-mask mode), which also cuts its compile time
@@ -384,7 +395,7 @@ __device__ __forceinline__ int children_of_class(uint32_t item0, const StagedPla
 }
 
 template <class R, class Src, bool EXT, int K>
-__global__ __launch_bounds__(kStagedBlock, ChildClasses<R>::waves(K)) void children_kernel(
+__global__ __launch_bounds__(kStagedBlock, (ChildWaves<R, K, EXT>::v)) void children_kernel(
     Src src, const StagedPlan* __restrict__ plan, const uint32_t* __restrict__ items, EnvView env, Bases bs,
     uint8_t* __restrict__ valid)
 {
