@@ -422,11 +422,43 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         pairs = roadmap.edges_shard(torch, robot, env, V, k, r, kmax, qf, qc, ctx)
         if world > 1:
             pairs = roadmap.allgather_pairs(torch, dist, pairs)
-        off, adj, comp = roadmap.assemble(n, pairs.cpu().numpy())
-        info.update(pairs=int(pairs.shape[0]), components=int(len(np.unique(comp))))
+        # adjacency + components on the device, then the host Roadmap the reference returns
+        off, adj, comp = roadmap.assemble_device(torch, n, pairs, ctx)
+        info.update(pairs=int(pairs.shape[0]), off=off.cpu(), adj=adj.cpu(), comp=comp.cpu())
 
     wall = timed_steps(a, torch, dist, dev, world, step)
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(n) / world, dev, world)
+    # where one step's time goes (an extra, synchronised step outside the timed region): kNN + edge gather +
+    # validation on the GPU, the pair exchange, the device-to-host copy of the valid pairs, host assembly
+    phases = {}
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    pairs = roadmap.edges_shard(torch, robot, env, V, k, r, kmax, qf, qc, ctx)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    if world > 1:
+        pairs = roadmap.allgather_pairs(torch, dist, pairs)
+    torch.cuda.synchronize(dev)
+    t2 = time.perf_counter()
+    off_d, adj_d, comp_d = roadmap.assemble_device(torch, n, pairs, ctx)
+    torch.cuda.synchronize(dev)
+    t3 = time.perf_counter()
+    off_h, adj_h, comp_h = off_d.cpu().numpy(), adj_d.cpu().numpy(), comp_d.cpu().numpy()
+    t4 = time.perf_counter()
+    ph = pairs.cpu().numpy()
+    t5 = time.perf_counter()
+    off_r, adj_r, comp_r = roadmap.assemble(n, ph)  # the host assembly: the checker, and its time
+    t6 = time.perf_counter()
+    assembly_equal = bool(np.array_equal(off_h, off_r) and np.array_equal(adj_h.view(np.uint32), adj_r) and
+                          np.array_equal(comp_h.view(np.uint32), comp_r))
+    info["components"] = int(len(np.unique(comp_h)))
+    phases = {"gpu_knn_gather_validate_ms": (t1 - t0) * 1e3, "exchange_ms": (t2 - t1) * 1e3,
+              "gpu_assembly_ms": (t3 - t2) * 1e3, "d2h_roadmap_ms": (t4 - t3) * 1e3,
+              "host_assembly_ms_for_comparison": (t6 - t5) * 1e3, "d2h_pairs_ms": (t5 - t4) * 1e3,
+              "pairs_bytes": int(ph.nbytes), "device_assembly_equals_host": assembly_equal}
+    del pairs, ph, off_d, adj_d, comp_d, off_h, adj_h, comp_h, off_r, adj_r, comp_r
+    for key in ("off", "adj", "comp"):
+        info.pop(key, None)
     # the kNN kernel alone (this rank's queries), HIP events on the launch stream, in both methods
     # of vgpu_set_knn_mode: brute force (the roofline: its flops are the ones executed) and the
     # spatial index (auto's choice from 65536 vertices; same lists, compared below)
@@ -515,8 +547,12 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                      "note": "roofline of the brute-force kernel (every pair evaluated); the index kernel's time is "
                              "beside it, not priced in flops (it skips pairs)"},
         "cpu_baseline": cpu,
+        "phases": phases,
     }
-    print(json.dumps(line))
+    print(json.dumps(line), flush=True)
+    if not (index_equals_brute and phases.get("device_assembly_equals_host", True)):
+        print("PARITY FAILURE (kNN index vs brute force, or device vs host roadmap assembly)", file=sys.stderr)
+        sys.exit(3)
 
 
 def timed_steps(a, torch, dist, dev, world, step):

@@ -238,6 +238,11 @@ int vgpu_roadmap_edge_gather(vgpu_ctx *ctx, int dim, const float *V, size_t q_fi
  * component (optional) = smallest vertex index of each vertex's connected component. */
 int vgpu_roadmap_assemble(size_t n, const uint32_t *pairs, size_t m, size_t *offsets, uint32_t *adj,
                           uint32_t *component);
+/* The same on the device (mr-vamp_amd/csrc/vgpu_roadmap_assemble.hip): pairs[m][2], offsets[n+1] (uint64),
+ * adj[2m], component[n] (optional) all device memory on ctx; identical output.  2m < 2^31; a pair
+ * index >= n fails with VGPU_ERR_INVALID_ARG.  Synchronous (one host read per hooking round). */
+int vgpu_roadmap_assemble_device(vgpu_ctx *ctx, size_t n, const uint32_t *pairs, size_t m, uint64_t *offsets,
+                                 uint32_t *adj, uint32_t *component);
 /* Roadmap::build_roadmap's graph for the vertex sequence V[n][dim] (start, goal, then the valid
  * samples in draw order -- vgpu_sample_fkcc + vgpu_compact): every vertex's neighbour query,
  * validate_motion(neighbor, vertex) of every candidate on the GPU, and the adjacency lists in

@@ -1982,6 +1982,36 @@ extern "C" int vgpu_roadmap_assemble(size_t n, const uint32_t* pairs, size_t m, 
     return VGPU_OK;
 }
 
+extern "C" size_t vgpu_roadmap_assemble_bytes(uint32_t n, size_t m);
+extern "C" hipError_t vgpu_launch_roadmap_assemble(uint32_t n, const uint32_t* pairs, size_t m, unsigned long long* offsets,
+                                                   uint32_t* adj, uint32_t* component, void* tmp, size_t tmp_bytes,
+                                                   uint32_t* flags, hipStream_t st);
+
+extern "C" int vgpu_roadmap_assemble_device(vgpu_ctx* c, size_t n, const uint32_t* pairs, size_t m, uint64_t* offsets,
+                                            uint32_t* adj, uint32_t* component)
+{
+    if (!c) return VGPU_ERR_INVALID_ARG;
+    if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many vertices");
+    if (2 * m >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many pairs (2m must be < 2^31)");
+    if (!offsets || (m && (!pairs || !adj))) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
+    if (m && n == 0) return fail(c, VGPU_ERR_INVALID_ARG, "pair index out of range");
+    HIPCHK(c, hipSetDevice(c->device));
+    const size_t bytes = vgpu_roadmap_assemble_bytes((uint32_t)n, m);
+    if (!bytes) return fail(c, VGPU_ERR_HIP, "roadmap assembly: scratch size query failed");
+    int rc;
+    // the kNN index pool: free again once the edge stage's queries are done (same stream)
+    if ((rc = grow(c, &c->knn_idx, &c->knn_idx_cap, (bytes + 3) / 4))) return rc;
+    if (n == 0) {
+        HIPCHK(c, hipMemsetAsync(offsets, 0, sizeof(uint64_t), c->cur));
+        return VGPU_OK;
+    }
+    uint32_t flags = 0;
+    HIPCHK(c, vgpu_launch_roadmap_assemble((uint32_t)n, pairs, m, (unsigned long long*)offsets, adj, component,
+                                           c->knn_idx, c->knn_idx_cap * 4, &flags, c->cur));
+    if (flags & 1u) return fail(c, VGPU_ERR_INVALID_ARG, "pair index out of range");
+    return VGPU_OK;
+}
+
 extern "C" int vgpu_build_roadmap_host(vgpu_ctx* c, const vgpu_robot* robot, vgpu_env* e, const float* V, size_t n,
                                        double space_measure, double gamma_scale, size_t* offsets, uint32_t* adj,
                                        size_t adj_cap, size_t* n_adj, uint32_t* component)

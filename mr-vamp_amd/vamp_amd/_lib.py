@@ -109,6 +109,7 @@ SIGNATURES = {
     "vgpu_roadmap_edge_gather": (C.c_int, [VP, C.c_int, VP, C.c_size_t, C.c_size_t, VP, C.c_uint32, VP, VP, VP,
                                            VP]),
     "vgpu_roadmap_assemble": (C.c_int, [C.c_size_t, U32P, C.c_size_t, C.POINTER(C.c_size_t), U32P, U32P]),
+    "vgpu_roadmap_assemble_device": (C.c_int, [VP, C.c_size_t, VP, C.c_size_t, VP, VP, VP]),
     "vgpu_cpu_fkcc_block": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.POINTER(C.c_int)]),
     "vgpu_cpu_fkcc_attach_block": (C.c_int, [C.POINTER(VgpuRobot), VP, F32P, C.POINTER(C.c_int)]),
     "vgpu_cpu_sphere_fk_block": (C.c_int, [C.POINTER(VgpuRobot), F32P, F32P]),

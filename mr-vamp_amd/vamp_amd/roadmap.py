@@ -292,6 +292,22 @@ def assemble(n: int, pairs: np.ndarray):
     return offsets.astype(np.int64), adj[:2 * len(p)], comp[:n]
 
 
+def assemble_device(torch, n: int, pairs, ctx):
+    """assemble() on the GPU (vgpu_roadmap_assemble_device) from the valid pairs as a device int32 tensor
+    [m, 2] (edges_shard / allgather_pairs output): (offsets int64 [n+1], adj int32 [2m], component int32 [n])
+    device tensors, equal to the host assembly's."""
+    from ._lib import check, load
+    dev = pairs.device
+    p = pairs.contiguous()
+    m = int(p.shape[0])
+    offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    adj = torch.empty(max(2 * m, 1), dtype=torch.int32, device=dev)
+    comp = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    check(load().vgpu_roadmap_assemble_device(ctx.h, n, p.data_ptr() if m else None, m, offsets.data_ptr(),
+                                              adj.data_ptr(), comp.data_ptr()), ctx.h)
+    return offsets, adj[:2 * m], comp[:n]
+
+
 def build_roadmap_edges_sharded(torch, dist, robot, environment, V, gamma_scale: float = 2.0, ctx=None,
                                 group=None) -> Roadmap:
     """The edge stage with the queries split over the ranks (query_split), each rank validating its

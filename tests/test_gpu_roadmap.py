@@ -187,3 +187,44 @@ def test_robot_roadmap_binding(vamp, oracle, max_iterations, max_samples):
     edges, _ = oracle.build_roadmap_edges("panda", oenv, want)
     assert rm.edges == edges
     assert rm.nanoseconds > 0 and np.array_equal(rm[5], want[5])
+
+
+def _query_order_pairs(n, m, seed):
+    """valid (vertex i, neighbour j < i) pairs in build_roadmap's query order: i ascending"""
+    rng = np.random.default_rng(seed)
+    i = np.sort(rng.integers(1, n, m)).astype(np.uint32) if n > 1 else np.zeros(0, np.uint32)
+    j = (rng.random(len(i)) * i).astype(np.uint32)
+    return np.stack([i, j], 1).astype(np.uint32)
+
+
+@pytest.mark.parametrize("n,m", [(1, 0), (2, 1), (1000, 0), (1000, 5000), (300000, 2000000)])
+def test_roadmap_assemble_device_equals_host(vamp, n, m):
+    """vgpu_roadmap_assemble_device (vgpu_roadmap_assemble.hip: stable radix sort of the expanded pairs,
+    atomicMin hooking + pointer jumping) == the host assembly: offsets, append-order adjacency and
+    components (smallest index), including isolated vertices and repeated pairs."""
+    import torch
+    from vamp_amd import roadmap
+    pairs = _query_order_pairs(n, m, 5 + n)
+    if m > 10:
+        pairs[5] = pairs[4]  # a repeated pair
+    dev = torch.device("cuda", 0)
+    ctx = vamp.context(0)
+    ctx.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+    tp = torch.from_numpy(pairs.view(np.int32)).to(dev).reshape(-1, 2)
+    off, adj, comp = roadmap.assemble_device(torch, n, tp, ctx)
+    torch.cuda.synchronize()
+    ho, ha, hc = roadmap.assemble(n, pairs)
+    assert np.array_equal(off.cpu().numpy(), ho)
+    assert np.array_equal(adj.cpu().numpy().view(np.uint32), ha)
+    assert np.array_equal(comp.cpu().numpy().view(np.uint32), hc)
+
+
+def test_roadmap_assemble_device_rejects_bad_index(vamp):
+    import torch
+    from vamp_amd import roadmap
+    from vamp_amd._lib import VgpuError
+    dev = torch.device("cuda", 0)
+    ctx = vamp.context(0)
+    tp = torch.tensor([[1, 0], [7, 2]], dtype=torch.int32, device=dev)
+    with pytest.raises(VgpuError):
+        roadmap.assemble_device(torch, 5, tp, ctx)
