@@ -43,8 +43,6 @@ hipError_t vgpu_launch_scatter_items(const uint32_t* cnt, const uint32_t* off, s
 hipError_t vgpu_launch_filter_robot(const float* pc, size_t n, float point_radius, const float* sph, int S,
                                    const EnvView* env, uint8_t* keep, hipStream_t st);
 hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long* out, hipStream_t st);
-hipError_t vgpu_launch_readback(const uint32_t* a, size_t stride, uint32_t na, const uint32_t* b, uint32_t nb,
-                                uint32_t* dst, uint32_t seq, hipStream_t st);
 #define VGPU_STAGED_DECL(NAME)                                                                                       \
     int vgpu_##NAME##_staged_checks(void);                                                                           \
     uint64_t vgpu_##NAME##_staged_env_checks(void);                                                                  \
@@ -253,12 +251,6 @@ struct vgpu_ctx {
     uint32_t* st_cnt = nullptr;   // per-(check, block) counts, then their exclusive scan, + scan temp
     size_t st_cnt_cap = 0;
     uint32_t* st_host = nullptr;  // pinned: the first round's segment boundaries of a staged pass
-    // mid-call read-backs (readback below): fine-grained host words the device writes directly, the host
-    // polls a sequence word; rb_state 0 = not set up, 1 = ready, -1 = unavailable (copy + stream sync)
-    uint32_t* rb_host = nullptr;
-    uint32_t* rb_dev = nullptr;
-    uint32_t rb_seq = 0;
-    int rb_state = 0;
     uint32_t* st_items = nullptr;
     size_t st_items_cap = 0;
     // roadmap kNN chunk lists (vgpu_roadmap.hip)
@@ -376,7 +368,6 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->st_cnt) (void)hipFree(c->st_cnt);
     if (c->st_items) (void)hipFree(c->st_items);
     if (c->st_host) (void)hipHostFree(c->st_host);
-    if (c->rb_host) (void)hipHostFree(c->rb_host);
     if (c->knn_part) (void)hipFree(c->knn_part);
     if (c->knn_idx) (void)hipFree(c->knn_idx);
     if (c->small) (void)hipFree(c->small);
@@ -1059,52 +1050,6 @@ static int grow(vgpu_ctx* c, uint32_t** p, size_t* cap, size_t need)
     return VGPU_OK;
 }
 
-// Read na words a[i * stride] and nb words b[i] (device) into out[] mid-call.  The readback kernel writes
-// them into fine-grained host memory and then a sequence word; the host spins on that word (no copy
-// engine, no stream synchronize), checking the stream for errors while it waits.  Opt-in
-// (VGPU_POLLED_READBACK=1); otherwise, or without fine-grained host memory: copy + stream sync.
-static int readback(vgpu_ctx* c, const uint32_t* a, size_t stride, uint32_t na, const uint32_t* b, uint32_t nb,
-                    uint32_t* out)
-{
-    if (c->rb_state == 0) {
-        c->rb_state = -1;
-        const char* pr = std::getenv("VGPU_POLLED_READBACK");  // opt-in until measured on MI355X
-        if (pr && std::atoi(pr) != 0 &&
-            hipHostMalloc((void**)&c->rb_host, 256 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped) ==
-                hipSuccess) {
-            if (hipHostGetDevicePointer((void**)&c->rb_dev, c->rb_host, 0) == hipSuccess) {
-                std::memset(c->rb_host, 0, 256 * sizeof(uint32_t));
-                c->rb_state = 1;
-            }
-        }
-        (void)hipGetLastError();
-    }
-    if (c->rb_state == 1) {
-        const uint32_t seq = ++c->rb_seq ? c->rb_seq : ++c->rb_seq;  // never 0 (the initial word)
-        HIPCHK(c, vgpu_launch_readback(a, stride, na, b, nb, c->rb_dev, seq, c->cur));
-        volatile uint32_t* flag = c->rb_host + 255;
-        for (uint64_t it = 1;; ++it) {
-            if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == seq) break;
-            if ((it & 4095u) == 0) {  // the stream finished (or failed) without the word: report it
-                const hipError_t q = hipStreamQuery(c->cur);
-                if (q == hipSuccess && __atomic_load_n(flag, __ATOMIC_ACQUIRE) != seq)
-                    return fail(c, VGPU_ERR_HIP, "read-back word not written");
-                if (q != hipSuccess && q != hipErrorNotReady) HIPCHK(c, q);
-            }
-            _mm_pause();
-        }
-        for (uint32_t i = 0; i < na + nb; ++i) out[i] = c->rb_host[i];
-        return VGPU_OK;
-    }
-    if (!c->st_host) HIPCHK(c, hipHostMalloc((void**)&c->st_host, 128 * sizeof(uint32_t), hipHostMallocDefault));
-    if (na) HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), a, stride * sizeof(uint32_t), sizeof(uint32_t), na,
-                                       hipMemcpyDeviceToHost, c->cur));
-    if (nb) HIPCHK(c, hipMemcpyAsync(c->st_host + na, b, nb * sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
-    HIPCHK(c, hipStreamSynchronize(c->cur));
-    for (uint32_t i = 0; i < na + nb; ++i) out[i] = c->st_host[i];
-    return VGPU_OK;
-}
-
 // the staged pipeline of one robot (vgpu_staged.hh instantiations)
 struct StagedOps {
     int (*checks)(void);
@@ -1202,10 +1147,11 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
     // every check's fired groups (all groups valid here): segment boundaries offs[k * nb], k = 0..checks
     HIPCHK(c, ops.count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, all, valid, counts, c->cur));
     HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
-    uint32_t bounds[65];
-    if ((rc = readback(c, offs, nb, (uint32_t)checks + 1, nullptr, 0, bounds))) return rc;
+    HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t), checks + 1,
+                               hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
     uint32_t fired[64];
-    for (int k = 0; k < checks; ++k) fired[k] = bounds[k + 1] - bounds[k];
+    for (int k = 0; k < checks; ++k) fired[k] = c->st_host[k + 1] - c->st_host[k];
     std::vector<uint64_t> rounds(c->rounds.begin(), c->rounds.end());
     if (rounds.empty()) {
         // Rounds from this batch's bounding statistics: (1) the first three environment checks
@@ -1325,11 +1271,12 @@ static int item_total(vgpu_ctx* c, const uint32_t* cnt, const uint32_t* off, siz
 {
     auto* t64 = (unsigned long long*)(((uintptr_t)tmp + tmp_bytes + 7) & ~(uintptr_t)7);
     HIPCHK(c, vgpu_launch_total64(cnt, n_edges, t64, c->cur));
-    uint32_t words[3];  // the 32-bit scan total, then the 64-bit sum
-    if (int rc = readback(c, off + n_edges, 1, 1, (const uint32_t*)t64, 2, words)) return rc;
+    HIPCHK(c, hipMemcpyAsync(c->total_host, off + n_edges, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipMemcpyAsync(c->total_host + 2, t64, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->cur));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
     unsigned long long total = 0;
-    std::memcpy(&total, words + 1, sizeof(total));
-    if (total != (unsigned long long)words[0] || total + n_edges >= (1ull << 32))
+    std::memcpy(&total, c->total_host + 2, sizeof(total));
+    if (total != (unsigned long long)c->total_host[0] || total + n_edges >= (1ull << 32))
         return fail(c, VGPU_ERR_INVALID_ARG, "edges too long: more than 2^32 rake blocks in one call (split the batch)");
     *n_items = (size_t)total;
     return VGPU_OK;

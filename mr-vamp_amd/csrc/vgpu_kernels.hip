@@ -156,23 +156,6 @@ __global__ __launch_bounds__(kBlock) void total64_kernel(const uint32_t* __restr
     }
 }
 
-// A few words the host must read mid-call, written straight into fine-grained host memory (dst is its
-// device mapping) instead of a copy + stream sync: dst[0 .. na) = a[i * stride], dst[na .. na + nb) =
-// b[i], then -- after a system-scope fence -- the sequence word dst[kReadbackSeq] = seq, which the host
-// polls (vgpu_api.cpp readback).
-constexpr int kReadbackSeq = 255;
-__global__ __launch_bounds__(256) void readback_kernel(const uint32_t* __restrict__ a, size_t stride, uint32_t na,
-                                                       const uint32_t* __restrict__ b, uint32_t nb, uint32_t* dst,
-                                                       uint32_t seq)
-{
-    const uint32_t i = threadIdx.x;
-    if (i < na) dst[i] = a[(size_t)i * stride];
-    else if (i < na + nb) dst[i] = b[i - na];
-    __threadfence_system();
-    __syncthreads();
-    if (i == 0) __hip_atomic_store(dst + kReadbackSeq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 }  // namespace vgpu
 
 static bool has_ext(const EnvView* env) { return env->n_hf > 0 || env->n_pc > 0; }
@@ -270,14 +253,6 @@ hipError_t vgpu_launch_panda_validate_head(const float* starts, const float* goa
     else
         hipLaunchKernelGGL(vgpu::panda_validate_head_kernel<false>, dim3(grid), dim3(vgpu::kBlock), 0, st, starts,
                            goals, n_edges, *env, bx, by, bz, ok, n_blocks, cnt);
-    return hipGetLastError();
-}
-
-hipError_t vgpu_launch_readback(const uint32_t* a, size_t stride, uint32_t na, const uint32_t* b, uint32_t nb,
-                                uint32_t* dst, uint32_t seq, hipStream_t st)
-{
-    if (na + nb > (uint32_t)vgpu::kReadbackSeq) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(vgpu::readback_kernel, dim3(1), dim3(256), 0, st, a, stride, na, b, nb, dst, seq);
     return hipGetLastError();
 }
 
