@@ -580,11 +580,8 @@ def contract_line(a, world, wall_max, units_all, metric, unit, scaling, data, co
             "roofline": roofline, "cpu_baseline": cpu}
 
 
-def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
-    """BASELINE configs[4] (SURVEY §8(d) config 5): two Pandas (bases (0,0,0) and (1,0,0)), 14-dof
-    edges between collision-free composite configurations, each arm's sub-edge capped at 1.0;
-    validate_motion over the composite (fkcc of both arms + inter-arm spheres).  Independent edge
-    shards per rank (weak scaling, no collective)."""
+def pair_scene_env(vamp):
+    """configs[4]'s scene (tests/oracle_py.py pair_scene: a table and 3 spheres) as an Environment"""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as op
 
@@ -594,11 +591,14 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         env.add_sphere(vamp.Sphere([x, y, z], r))
     for row in oenv.cuboids + oenv.zcuboids:
         env.add_cuboid(vamp.Cuboid.from_axes(row[0:3], row[3:6], row[6:9], row[9:12], row[12:15]))
-    robot = vamp.panda_pair
-    strong = a.scaling == "strong"
-    E = a.edges
+    return env, oenv
+
+
+def make_pair_edges(torch, robot, env, E, seed, dev, ctx):
+    """configs[4] edges: pairs of collision-free composite configurations (drawn on the device, checked
+    with the composite fkcc), each arm's sub-edge capped at length 1.0"""
     g = torch.Generator(device=dev)
-    g.manual_seed(shard_seed(0 if strong else rank))
+    g.manual_seed(seed)
     sm = torch.tensor(S_M * 2, device=dev)
     sa = torch.tensor(S_A * 2, device=dev)
     pool, have = [], 0
@@ -617,7 +617,22 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         d = torch.linalg.vector_norm((goals[:, sl] - starts[:, sl]).double(), dim=1)
         sc = torch.clamp(1.0 / torch.clamp(d, min=1e-9), max=1.0).float()
         goals[:, sl] = starts[:, sl] + (goals[:, sl] - starts[:, sl]) * sc[:, None]
-    goals = goals.contiguous()
+    return starts, goals.contiguous()
+
+
+def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
+    """BASELINE configs[4] (SURVEY §8(d) config 5): two Pandas (bases (0,0,0) and (1,0,0)), 14-dof
+    edges between collision-free composite configurations, each arm's sub-edge capped at 1.0;
+    validate_motion over the composite (fkcc of both arms + inter-arm spheres).  Independent edge
+    shards per rank (weak scaling, no collective)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as op
+
+    env, oenv = pair_scene_env(vamp)
+    robot = vamp.panda_pair
+    strong = a.scaling == "strong"
+    E = a.edges
+    starts, goals = make_pair_edges(torch, robot, env, E, shard_seed(0 if strong else rank), dev, ctx)
     if strong:  # one fixed batch, this rank's contiguous range, through pinned host memory
         lo, E = strong_slice(a.edges, rank, world)
         starts, goals = starts[lo:lo + E].contiguous(), goals[lo:lo + E].contiguous()

@@ -80,6 +80,8 @@ const char *vgpu_last_error(const vgpu_ctx *ctx);
  * the context's own stream. */
 int vgpu_ctx_set_stream(vgpu_ctx *ctx, void *hip_stream);
 int vgpu_sync(vgpu_ctx *ctx);
+/* the HIP device the context was created on */
+int vgpu_ctx_device(const vgpu_ctx *ctx, int *device);
 /* Per-phase kernel timing of vgpu_validate_motions (HIP events on the context stream; adds
  * one event synchronisation per call while enabled).  vgpu_phase_times returns and resets the
  * accumulated milliseconds: [0] head (first rake block), [1] scan + item count read-back,
@@ -401,6 +403,13 @@ typedef struct vgpu_comm vgpu_comm;
 int vgpu_comm_unique_id(uint8_t id[128]);
 int vgpu_comm_init(vgpu_ctx *ctx, int rank, int world, const uint8_t id[128], vgpu_comm **out);
 void vgpu_comm_destroy(vgpu_comm *comm);
+/* message of the communicator's last failed call (which rank failed, or what failed here) */
+const char *vgpu_comm_last_error(const vgpu_comm *comm);
+/* Collective calls below are failure-safe: a rank whose arguments, allocations or kernels fail still enters
+ * the first exchange, with a failure word in place of its count; then EVERY rank returns that rank's error
+ * code (the first failing rank's) and nobody blocks in the next all-gather.  Buffers and the exchange
+ * stream belong to the communicator (grown on demand, freed by vgpu_comm_destroy); ctx must live on the
+ * communicator's device (else VGPU_ERR_INVALID_ARG, reported to every rank). */
 /* The PRM vertex stage of BASELINE configs[3] sharded over the ranks with ONE exchange: this rank's
  * contiguous share of draws first .. first + n_draws_total - 1 through the fused sampler + fkcc +
  * compaction, then an all-gather of the counts and of the count-padded rows and draw indices.  rows[cap][dim]
@@ -409,6 +418,20 @@ void vgpu_comm_destroy(vgpu_comm *comm);
 int vgpu_prm_vertices_allgather(vgpu_ctx *ctx, vgpu_comm *comm, const vgpu_robot *robot, vgpu_env *env,
                                 uint64_t first, size_t n_draws_total, float *rows, uint64_t *draws, size_t cap,
                                 size_t *count);
+/* Query ranges of the sharded edge stage: equal prefix work (query i scans i vertices), boundaries at
+ * floor(n sqrt(k / world) + 0.5). */
+int vgpu_query_split(size_t n, int rank, int world, size_t *first, size_t *count);
+/* The PRM edge stage of BASELINE configs[3] sharded over the ranks (Roadmap::build_roadmap's graph,
+ * prm.hh:255-299, planning/roadmap.hh:49-56): this rank's queries (vgpu_query_split) through the neighbour
+ * query, the candidate gather and validate_motion(neighbor, vertex), the valid pairs selected on the device
+ * in query order; ONE exchange (counts, then the count-padded pairs); then every rank assembles the whole
+ * roadmap on its device in the reference's append order.  V[n][dim] device (identical on all ranks);
+ * offsets[n+1] (uint64), adj[adj_cap], component[n] (optional) device; *n_adj = required adjacency
+ * entries (2 x valid pairs) -- adj_cap < *n_adj fails with VGPU_ERR_INVALID_ARG on every rank.  Output
+ * equals vgpu_build_roadmap_host's for the same vertices. */
+int vgpu_prm_edges_allgather(vgpu_ctx *ctx, vgpu_comm *comm, const vgpu_robot *robot, vgpu_env *env, const float *V,
+                             size_t n, double space_measure, double gamma_scale, uint64_t *offsets, uint32_t *adj,
+                             size_t adj_cap, size_t *n_adj, uint32_t *component);
 /* a deep copy of an environment bound to ctx (NULL: host-only) */
 int vgpu_env_clone(const vgpu_env *src, vgpu_ctx *ctx, vgpu_env **out);
 

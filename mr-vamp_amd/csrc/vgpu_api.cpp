@@ -387,6 +387,13 @@ extern "C" int vgpu_ctx_set_stream(vgpu_ctx* c, void* s)
     return VGPU_OK;
 }
 
+extern "C" int vgpu_ctx_device(const vgpu_ctx* c, int* device)
+{
+    if (!c || !device) return VGPU_ERR_INVALID_ARG;
+    *device = c->device;
+    return VGPU_OK;
+}
+
 extern "C" int vgpu_sync(vgpu_ctx* c)
 {
     if (!c) return VGPU_ERR_INVALID_ARG;
@@ -1638,8 +1645,11 @@ extern "C" int vgpu_compact(vgpu_ctx* c, const float* rows, const uint8_t* valid
 }
 
 // ---- host conveniences ------------------------------------------------------------------
+// Also makes the context's device current for the calling thread: the staging buffer and everything the
+// *_host entry point enqueues after it belong to that device (HIP's current device is per thread).
 static int stage(vgpu_ctx* c, size_t bytes, char** p)
 {
+    HIPCHK(c, hipSetDevice(c->device));
     if (bytes > c->stage_bytes) {
         if (c->stage) {
             HIPCHK(c, hipStreamSynchronize(c->cur));

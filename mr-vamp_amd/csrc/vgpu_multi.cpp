@@ -9,12 +9,18 @@
 //     librccl.so.1 (no torch); vgpu_prm_vertices_allgather is the PRM vertex stage of BASELINE configs[3]
 //     -- each rank samples its contiguous draw range (Halton -> scale -> fkcc, compaction on the device),
 //     then ONE exchange: an all-gather of the per-rank counts and an all-gather of the count-padded rows
-//     and draw indices, concatenated in rank order = build_roadmap's vertex sequence (prm.hh:235-254).
+//     and draw indices, concatenated in rank order = build_roadmap's vertex sequence (prm.hh:235-254);
+//     vgpu_prm_edges_allgather is its edge stage (prm.hh:255-299) -- query ranges of equal prefix work, the
+//     valid pairs all-gathered, the roadmap assembled on every rank's device.
+//     Every rank-local failure (argument, allocation, kernel) still enters exchange 1 with a failure word in
+//     place of its count, so all ranks return the same error and none is left inside an all-gather.
 #include <dlfcn.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -100,7 +106,16 @@ static int per_device(vgpu_multi* m, Fn fn)
 {
     std::vector<int> rc(m->ctx.size(), VGPU_OK);
     std::vector<std::thread> th;
-    for (size_t i = 0; i < m->ctx.size(); ++i) th.emplace_back([&, i] { rc[i] = fn((int)i); });
+    // HIP's current device is per thread and a new thread starts on device 0: select the context's device
+    // before fn allocates or launches anything
+    for (size_t i = 0; i < m->ctx.size(); ++i)
+        th.emplace_back([&, i] {
+            if (hipSetDevice(m->device[i]) != hipSuccess) {
+                rc[i] = VGPU_ERR_HIP;
+                return;
+            }
+            rc[i] = fn((int)i);
+        });
     for (auto& t : th) t.join();
     for (size_t i = 0; i < rc.size(); ++i)
         if (rc[i] != VGPU_OK) {
@@ -153,12 +168,12 @@ extern "C" int vgpu_multi_sample_fkcc_host(vgpu_multi* m, const vgpu_robot* r, v
         vgpu_shard_range(n_draws, i, w, &lo, &cnt);
         if (!cnt) return VGPU_OK;
         vgpu_ctx* c = m->ctx[i];
-        if (hipSetDevice(m->device[i]) != hipSuccess) return VGPU_ERR_HIP;
         float *q = nullptr, *ro = nullptr;
         uint8_t* v = nullptr;
         uint32_t* ix = nullptr;
         int e = VGPU_OK;
-        if (hipMalloc(&q, cnt * dim * sizeof(float)) != hipSuccess || hipMalloc(&ro, cnt * dim * sizeof(float)) ||
+        if (hipMalloc(&q, cnt * dim * sizeof(float)) != hipSuccess ||
+            hipMalloc(&ro, cnt * dim * sizeof(float)) != hipSuccess ||
             hipMalloc(&v, cnt) != hipSuccess || hipMalloc(&ix, cnt * sizeof(uint32_t)) != hipSuccess)
             e = VGPU_ERR_OOM;
         if (e == VGPU_OK) e = vgpu_sample_fkcc(c, r, envs[i], first + lo, cnt, q, v);
@@ -217,11 +232,21 @@ Rccl& rccl()
     });
     return R;
 }
+
+// grow-only device buffers of a communicator, one per slot (the stages below name their slots)
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+constexpr int kSlots = 16;
 }  // namespace
 
 struct vgpu_comm {
     ncclComm_t comm = nullptr;
     int rank = 0, world = 1, device = 0;
+    hipStream_t st = nullptr;  // the exchanges' stream (the kernels run on the context's)
+    DevBuf buf[kSlots];
+    std::string err;
 };
 
 static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id is 128 bytes");
@@ -244,12 +269,17 @@ extern "C" int vgpu_comm_init(vgpu_ctx* ctx, int rank, int world, const uint8_t 
     Rccl& R = rccl();
     if (!R.ok) return VGPU_ERR_UNSUPPORTED;
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return VGPU_ERR_HIP;
+    if (vgpu_ctx_device(ctx, &dev) != VGPU_OK || hipSetDevice(dev) != hipSuccess) return VGPU_ERR_HIP;
     auto* c = new (std::nothrow) vgpu_comm();
     if (!c) return VGPU_ERR_OOM;
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return VGPU_ERR_HIP;
+    }
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     if (R.init(&c->comm, world, u, rank) != ncclSuccess) {
+        (void)hipStreamDestroy(c->st);
         delete c;
         return VGPU_ERR_HIP;
     }
@@ -263,8 +293,128 @@ extern "C" int vgpu_comm_init(vgpu_ctx* ctx, int rank, int world, const uint8_t 
 extern "C" void vgpu_comm_destroy(vgpu_comm* c)
 {
     if (!c) return;
+    (void)hipSetDevice(c->device);
+    if (c->st) (void)hipStreamSynchronize(c->st);
+    for (DevBuf& b : c->buf)
+        if (b.p) (void)hipFree(b.p);
+    if (c->st) (void)hipStreamDestroy(c->st);
     if (c->comm && rccl().ok) rccl().destroy(c->comm);
     delete c;
+}
+
+extern "C" const char* vgpu_comm_last_error(const vgpu_comm* c) { return c ? c->err.c_str() : "null comm"; }
+
+template <class T>
+static bool comm_buf(vgpu_comm* c, int slot, size_t count, T** out)
+{
+    DevBuf& b = c->buf[slot];
+    const size_t bytes = std::max<size_t>(count, 1) * sizeof(T);
+    if (bytes > b.cap) {
+        if (b.p) {
+            (void)hipStreamSynchronize(c->st);
+            (void)hipFree(b.p);
+            b.p = nullptr;
+            b.cap = 0;
+        }
+        if (hipMalloc(&b.p, bytes) != hipSuccess) {
+            b.p = nullptr;
+            return false;
+        }
+        b.cap = bytes;
+    }
+    *out = (T*)b.p;
+    return true;
+}
+
+// Rank-local fault injection for the failure-path tests: VGPU_FAULT_INJECT=<site>[@rank] makes that rank
+// (every rank without @) fail at <site> as an allocation failure would.
+static bool injected(const vgpu_comm* c, const char* site)
+{
+    const char* v = std::getenv("VGPU_FAULT_INJECT");
+    if (!v) return false;
+    const std::string s(v);
+    const size_t at = s.find('@');
+    if (s.substr(0, at) != site) return false;
+    return at == std::string::npos || std::atoi(s.c_str() + at + 1) == c->rank;
+}
+
+// A failing rank still enters every collective its peers enter: exchange 1 carries each rank's count, or
+// kFailTag | -code, so every rank sees the same failure and returns the same error instead of leaving its
+// peers blocked in the next all-gather.
+static constexpr uint64_t kFailTag = 0xFFFFFFFF00000000ull;
+
+static int exchange_counts(vgpu_comm* c, uint64_t* dev_words, int local_rc, uint64_t count, std::vector<uint64_t>& all)
+{
+    Rccl& R = rccl();
+    const int W = c->world;
+    const uint64_t mine = local_rc != VGPU_OK ? (kFailTag | (uint32_t)(-local_rc)) : count;
+    all.assign(W, 0);
+    if (hipMemcpyAsync(dev_words + W, &mine, 8, hipMemcpyHostToDevice, c->st) != hipSuccess ||
+        R.allgather(dev_words + W, dev_words, 1, ncclUint64, c->comm, c->st) != ncclSuccess ||
+        hipMemcpyAsync(all.data(), dev_words, W * 8, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
+        hipStreamSynchronize(c->st) != hipSuccess) {
+        c->err = "count exchange (RCCL all-gather) failed";
+        return VGPU_ERR_HIP;
+    }
+    for (int k = 0; k < W; ++k)
+        if (all[k] >= kFailTag) {
+            const int code = -(int)(uint32_t)(all[k] & 0xFFFFFFFFu);
+            if (local_rc == VGPU_OK) c->err = "rank " + std::to_string(k) + " failed (code " + std::to_string(code) + ")";
+            return code;
+        }
+    return VGPU_OK;
+}
+
+static int rank_fail(vgpu_comm* c, vgpu_ctx* ctx, int rc, const char* what)
+{
+    if (rc != VGPU_OK && c->err.empty()) c->err = std::string(what) + (ctx ? std::string(": ") + vgpu_last_error(ctx) : "");
+    return rc;
+}
+
+// exchange 2: every rank's first cnts[k] items of `send` (padded to max cnts) gathered and concatenated in
+// rank order into out; items are `words` u64 each
+static int gather_padded(vgpu_comm* c, const uint64_t* send, uint64_t* recv, const std::vector<uint64_t>& cnts,
+                         size_t words, uint64_t* out, size_t out_words_per_item_stride)
+{
+    Rccl& R = rccl();
+    uint64_t mx = 0;
+    for (uint64_t k : cnts) mx = std::max(mx, k);
+    if (!mx) return VGPU_OK;
+    if (R.allgather(send, recv, mx * words, ncclUint64, c->comm, c->st) != ncclSuccess) {
+        c->err = "RCCL all-gather failed";
+        return VGPU_ERR_HIP;
+    }
+    size_t at = 0;
+    for (size_t k = 0; k < cnts.size(); ++k) {
+        if (cnts[k] && hipMemcpyAsync(out + at * out_words_per_item_stride, recv + k * mx * words, cnts[k] * words * 8,
+                                      hipMemcpyDeviceToDevice, c->st) != hipSuccess) {
+            c->err = "device copy failed";
+            return VGPU_ERR_HIP;
+        }
+        at += cnts[k];
+    }
+    if (hipStreamSynchronize(c->st) != hipSuccess) {
+        c->err = "exchange stream failed";
+        return VGPU_ERR_HIP;
+    }
+    return VGPU_OK;
+}
+
+// the communicator's own device, and the context on it (argument errors a peer cannot see become a failed
+// exchange like any other rank-local error)
+static int comm_enter(vgpu_ctx* ctx, vgpu_comm* comm)
+{
+    int dev = -1;
+    if (vgpu_ctx_device(ctx, &dev) != VGPU_OK) return VGPU_ERR_INVALID_ARG;
+    if (dev != comm->device) {
+        comm->err = "context device differs from the communicator's";
+        return VGPU_ERR_INVALID_ARG;
+    }
+    if (hipSetDevice(comm->device) != hipSuccess) {
+        comm->err = "hipSetDevice failed";
+        return VGPU_ERR_HIP;
+    }
+    return VGPU_OK;
 }
 
 // PRM vertex stage of the whole job on this rank's device: draws first .. first + n_draws_total - 1, this
@@ -275,84 +425,211 @@ extern "C" int vgpu_prm_vertices_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const
                                            uint64_t first, size_t n_draws_total, float* rows, uint64_t* draws,
                                            size_t cap, size_t* count)
 {
-    if (!ctx || !comm || !count || !rows || !draws || first == 0) return VGPU_ERR_INVALID_ARG;
+    if (!comm || !count) return VGPU_ERR_INVALID_ARG;
     *count = 0;
-    const int dim = robot_dim(r);
-    if (dim < 1) return VGPU_ERR_INVALID_ARG;
-    Rccl& R = rccl();
-    if (!R.ok) return VGPU_ERR_UNSUPPORTED;
-    size_t lo, n;
-    vgpu_shard_range(n_draws_total, comm->rank, comm->world, &lo, &n);
+    comm->err.clear();
+    if (!rccl().ok) return VGPU_ERR_UNSUPPORTED;
     const int W = comm->world;
-    hipStream_t st = nullptr;
-    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return VGPU_ERR_HIP;
-    float *q = nullptr, *mine = nullptr, *all_rows = nullptr;
+    const int dim = robot_dim(r);
+    int rc = (!ctx || !rows || !draws || first == 0 || dim < 1) ? VGPU_ERR_INVALID_ARG : VGPU_OK;
+    if (rc == VGPU_OK) rc = comm_enter(ctx, comm);
+    size_t lo = 0, n = 0, share_max = (n_draws_total + W - 1) / W;
+    vgpu_shard_range(n_draws_total, comm->rank, W, &lo, &n);
+    float *q = nullptr, *pad_rows = nullptr, *all_rows = nullptr;
     uint8_t* v = nullptr;
     uint32_t* ix = nullptr;
-    uint64_t *cnt_d = nullptr, *mine_d = nullptr, *all_d = nullptr;
-    int rc = VGPU_OK;
+    uint64_t *words = nullptr, *pad_draws = nullptr, *all_d = nullptr;
+    // every buffer (both exchanges') up front, sized by the largest share: an allocation failure is known
+    // before exchange 1 and reported through it
+    if (rc == VGPU_OK &&
+        !(comm_buf(comm, 0, share_max * dim, &q) && comm_buf(comm, 1, share_max, &v) && comm_buf(comm, 2, share_max, &ix) &&
+          comm_buf(comm, 3, (size_t)W + 1, &words) && comm_buf(comm, 4, share_max * dim, &pad_rows) &&
+          comm_buf(comm, 5, share_max, &pad_draws) && comm_buf(comm, 6, W * share_max * dim, &all_rows) &&
+          comm_buf(comm, 7, W * share_max, &all_d)))
+        rc = VGPU_ERR_OOM, comm->err = "device allocation failed";
+    if (rc == VGPU_OK && injected(comm, "prm_vertices")) rc = VGPU_ERR_OOM, comm->err = "injected failure";
     size_t got = 0;
-    std::vector<uint64_t> cnts(W, 0);
-    auto bail = [&](int code) { rc = code; };
-    const size_t nn = std::max<size_t>(n, 1);
-    if (hipMalloc(&q, nn * dim * 4) || hipMalloc(&mine, nn * dim * 4) || hipMalloc(&v, nn) ||
-        hipMalloc(&ix, nn * 4) || hipMalloc(&cnt_d, (W + 1) * 8) || hipMalloc(&mine_d, nn * 8))
-        bail(VGPU_ERR_OOM);
-    // this rank's share, compacted on the device (the context's stream; joined before the collectives)
-    if (rc == VGPU_OK && n) rc = vgpu_sample_fkcc(ctx, r, e, first + lo, n, q, v);
-    if (rc == VGPU_OK && n) rc = vgpu_compact(ctx, q, v, n, dim, mine, ix, &got);
-    if (rc == VGPU_OK) rc = vgpu_sync(ctx);
-    if (rc == VGPU_OK) {
-        // draw indices (1-based) of the kept rows, as uint64
+    // this rank's share, compacted on the device straight into the exchange's send buffer
+    if (rc == VGPU_OK && n) rc = rank_fail(comm, ctx, vgpu_sample_fkcc(ctx, r, e, first + lo, n, q, v), "sample_fkcc");
+    if (rc == VGPU_OK && n) rc = rank_fail(comm, ctx, vgpu_compact(ctx, q, v, n, dim, pad_rows, ix, &got), "compact");
+    if (rc == VGPU_OK) rc = rank_fail(comm, ctx, vgpu_sync(ctx), "sync");
+    if (rc == VGPU_OK && got) {  // draw indices (1-based) of the kept rows, as uint64
         std::vector<uint32_t> hi(got);
         std::vector<uint64_t> hd(got);
-        if (got && hipMemcpy(hi.data(), ix, got * 4, hipMemcpyDeviceToHost)) bail(VGPU_ERR_HIP);
+        if (hipMemcpy(hi.data(), ix, got * 4, hipMemcpyDeviceToHost) != hipSuccess) rc = VGPU_ERR_HIP;
         for (size_t j = 0; j < got; ++j) hd[j] = first + lo + hi[j];
-        if (rc == VGPU_OK && got && hipMemcpy(mine_d, hd.data(), got * 8, hipMemcpyHostToDevice)) bail(VGPU_ERR_HIP);
-        const uint64_t g64 = got;
-        if (rc == VGPU_OK && hipMemcpy(cnt_d + W, &g64, 8, hipMemcpyHostToDevice)) bail(VGPU_ERR_HIP);
+        if (rc == VGPU_OK && hipMemcpy(pad_draws, hd.data(), got * 8, hipMemcpyHostToDevice) != hipSuccess)
+            rc = VGPU_ERR_HIP;
+        if (rc != VGPU_OK) comm->err = "draw index copy failed";
     }
-    // exchange 1: the counts
-    if (rc == VGPU_OK && R.allgather(cnt_d + W, cnt_d, 1, ncclUint64, comm->comm, st) != ncclSuccess) bail(VGPU_ERR_HIP);
-    if (rc == VGPU_OK && (hipStreamSynchronize(st) || hipMemcpy(cnts.data(), cnt_d, W * 8, hipMemcpyDeviceToHost)))
-        bail(VGPU_ERR_HIP);
-    uint64_t mx = 0, total = 0;
-    for (uint64_t c : cnts) mx = std::max(mx, c), total += c;
-    if (rc == VGPU_OK && total > cap) rc = VGPU_ERR_INVALID_ARG;
-    // exchange 2: the count-padded rows and draw indices
-    if (rc == VGPU_OK && mx) {
-        float* pad_rows = nullptr;
-        uint64_t* pad_draws = nullptr;
-        if (hipMalloc(&pad_rows, mx * dim * 4) || hipMalloc(&pad_draws, mx * 8) ||
-            hipMalloc(&all_rows, W * mx * dim * 4) || hipMalloc(&all_d, W * mx * 8))
-            bail(VGPU_ERR_OOM);
-        if (rc == VGPU_OK && got &&
-            (hipMemcpyAsync(pad_rows, mine, got * dim * 4, hipMemcpyDeviceToDevice, st) ||
-             hipMemcpyAsync(pad_draws, mine_d, got * 8, hipMemcpyDeviceToDevice, st)))
-            bail(VGPU_ERR_HIP);
-        if (rc == VGPU_OK &&
-            (R.allgather(pad_rows, all_rows, mx * dim, ncclFloat32, comm->comm, st) != ncclSuccess ||
-             R.allgather(pad_draws, all_d, mx, ncclUint64, comm->comm, st) != ncclSuccess))
-            bail(VGPU_ERR_HIP);
-        size_t at = 0;  // concatenate in rank order
-        for (int k = 0; rc == VGPU_OK && k < W; ++k) {
-            if (cnts[k] && (hipMemcpyAsync(rows + at * dim, all_rows + (size_t)k * mx * dim, cnts[k] * dim * 4,
-                                           hipMemcpyDeviceToDevice, st) ||
-                            hipMemcpyAsync(draws + at, all_d + (size_t)k * mx, cnts[k] * 8, hipMemcpyDeviceToDevice,
-                                           st)))
-                bail(VGPU_ERR_HIP);
+    // a null communicator word buffer cannot take part: nothing else to do (peers see a broken RCCL call)
+    if (!words) return rc != VGPU_OK ? rc : VGPU_ERR_OOM;
+    std::vector<uint64_t> cnts;
+    rc = exchange_counts(comm, words, rc, got, cnts);  // exchange 1, always entered
+    if (rc != VGPU_OK) return rc;
+    uint64_t total = 0;
+    for (uint64_t c : cnts) total += c;
+    if (total > cap) {  // every rank sees the same total
+        comm->err = "vertex capacity too small";
+        return VGPU_ERR_INVALID_ARG;
+    }
+    // exchange 2: the count-padded rows, then the draw indices
+    uint64_t mx = 0;
+    for (uint64_t c : cnts) mx = std::max(mx, c);
+    Rccl& R = rccl();
+    if (mx) {
+        if (R.allgather(pad_rows, all_rows, mx * dim, ncclFloat32, comm->comm, comm->st) != ncclSuccess) {
+            comm->err = "RCCL all-gather failed";
+            return VGPU_ERR_HIP;
+        }
+        size_t at = 0;
+        for (int k = 0; k < W; ++k) {
+            if (cnts[k] && hipMemcpyAsync(rows + at * dim, all_rows + (size_t)k * mx * dim, cnts[k] * dim * 4,
+                                          hipMemcpyDeviceToDevice, comm->st) != hipSuccess) {
+                comm->err = "device copy failed";
+                return VGPU_ERR_HIP;
+            }
             at += cnts[k];
         }
-        if (rc == VGPU_OK && hipStreamSynchronize(st)) bail(VGPU_ERR_HIP);
-        (void)hipStreamSynchronize(st);
-        for (void* p : {(void*)pad_rows, (void*)pad_draws})
-            if (p) (void)hipFree(p);
+        if ((rc = gather_padded(comm, pad_draws, all_d, cnts, 1, draws, 1)) != VGPU_OK) return rc;
     }
-    (void)hipStreamSynchronize(st);
-    for (void* p : {(void*)q, (void*)mine, (void*)v, (void*)ix, (void*)cnt_d, (void*)mine_d, (void*)all_rows,
-                    (void*)all_d})
-        if (p) (void)hipFree(p);
-    (void)hipStreamDestroy(st);
-    if (rc == VGPU_OK) *count = (size_t)total;
-    return rc;
+    *count = (size_t)total;
+    return VGPU_OK;
+}
+
+// Query ranges of equal prefix work: query i scans i candidates, so rank k takes [n sqrt(k/W), n sqrt((k+1)/W))
+// rounded half up (vamp_amd.roadmap.query_split is the same expression).
+extern "C" int vgpu_query_split(size_t n, int rank, int world, size_t* first, size_t* count)
+{
+    if (world < 1 || rank < 0 || rank >= world || !first || !count) return VGPU_ERR_INVALID_ARG;
+    auto bound = [&](int k) -> size_t {
+        if (k <= 0) return 0;
+        if (k >= world) return n;
+        const double b = std::floor((double)n * std::sqrt((double)k / (double)world) + 0.5);
+        return std::min(n, (size_t)b);
+    };
+    *first = bound(rank);
+    *count = bound(rank + 1) - *first;
+    return VGPU_OK;
+}
+
+extern "C" hipError_t vgpu_launch_valid_pairs(uint32_t q_first, uint32_t q_count, const uint32_t* nbr, uint32_t kmax,
+                                              const uint32_t* cnt, const uint32_t* off, const uint8_t* ok, size_t E,
+                                              unsigned long long* all, unsigned long long* out, uint32_t* count,
+                                              void* tmp, size_t* tmp_bytes, hipStream_t st);
+
+// PRM edge stage of the whole job (prm.hh:255-299): this rank's queries (vgpu_query_split) -- neighbour
+// query, candidate gather, validate_motion(neighbor, vertex) of every candidate, the valid pairs selected on
+// the device in query order -- then ONE exchange (counts, then the count-padded pairs), and the roadmap
+// assembled on the device from all ranks' pairs in rank order = query order.  V[n][dim] (device, identical on
+// every rank); offsets[n+1] (u64), adj[adj_cap], component[n] (optional) are device memory on ctx and come
+// out equal on every rank.  *n_adj = 2 x the valid pairs; adj_cap < *n_adj fails with VGPU_ERR_INVALID_ARG
+// on every rank (with *n_adj set).
+extern "C" int vgpu_prm_edges_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const vgpu_robot* r, vgpu_env* e,
+                                        const float* V, size_t n, double space_measure, double gamma_scale,
+                                        uint64_t* offsets, uint32_t* adj, size_t adj_cap, size_t* n_adj,
+                                        uint32_t* component)
+{
+    if (!comm || !n_adj) return VGPU_ERR_INVALID_ARG;
+    *n_adj = 0;
+    comm->err.clear();
+    if (!rccl().ok) return VGPU_ERR_UNSUPPORTED;
+    const int W = comm->world;
+    const int dim = robot_dim(r);
+    int rc = (!ctx || !offsets || (n && !V) || dim < 1 || n >= ((size_t)1 << 31)) ? VGPU_ERR_INVALID_ARG : VGPU_OK;
+    if (rc == VGPU_OK) rc = comm_enter(ctx, comm);
+    // the neighbour parameters and every rank's candidate bound (query i returns at most min(k_i, i)): the
+    // same on every rank, so buffer sizes and the cap check agree everywhere
+    std::vector<uint32_t> k(std::max<size_t>(n, 1));
+    std::vector<float> rad(std::max<size_t>(n, 1));
+    if (rc == VGPU_OK && vgpu_prm_neighbor_params(dim, space_measure, gamma_scale, n, k.data(), rad.data()) != VGPU_OK)
+        rc = VGPU_ERR_INVALID_ARG, comm->err = "neighbour parameters";
+    uint32_t kmax = 1;
+    for (size_t i = 0; i < n; ++i) kmax = std::max(kmax, k[i]);
+    kmax = (uint32_t)std::min<size_t>(kmax, std::max<size_t>(n, 1));
+    if (rc == VGPU_OK && kmax > 64) rc = VGPU_ERR_UNSUPPORTED, comm->err = "more than 64 neighbours per query";
+    size_t qf = 0, qc = 0;
+    vgpu_query_split(n, comm->rank, W, &qf, &qc);
+    size_t e_mine = 0, e_max = 0;
+    for (int w = 0; w < W; ++w) {
+        size_t f, c, b = 0;
+        vgpu_query_split(n, w, W, &f, &c);
+        for (size_t i = f; i < f + c; ++i) b += std::min<size_t>(k[i], i);
+        if (w == comm->rank) e_mine = b;
+        e_max = std::max(e_max, b);
+    }
+    if (rc == VGPU_OK && (e_max >= ((size_t)1 << 31) || (size_t)W * e_max >= ((size_t)1 << 30)))
+        rc = VGPU_ERR_UNSUPPORTED, comm->err = "too many candidate edges";
+    uint32_t *dk = nullptr, *nbr = nullptr, *cnt = nullptr, *off = nullptr, *selc = nullptr;
+    float *dr = nullptr, *dist = nullptr, *starts = nullptr, *goals = nullptr;
+    uint8_t* ok = nullptr;
+    unsigned long long *cand = nullptr, *sel = nullptr;
+    uint64_t *words = nullptr, *recv = nullptr, *pairs = nullptr;
+    char* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    if (rc == VGPU_OK &&
+        vgpu_launch_valid_pairs(0, 0, nullptr, 1, nullptr, nullptr, nullptr, e_mine, nullptr, nullptr, nullptr, nullptr,
+                                &tmp_bytes, nullptr) != hipSuccess)
+        rc = VGPU_ERR_HIP, comm->err = "selection scratch size";
+    if (rc == VGPU_OK &&
+        !(comm_buf(comm, 0, n, &dk) && comm_buf(comm, 1, n, &dr) && comm_buf(comm, 2, qc * kmax, &nbr) &&
+          comm_buf(comm, 3, qc * kmax, &dist) && comm_buf(comm, 4, qc + 1, &cnt) && comm_buf(comm, 5, qc + 1, &off) &&
+          comm_buf(comm, 6, e_mine * dim, &starts) && comm_buf(comm, 7, e_mine * dim, &goals) &&
+          comm_buf(comm, 8, e_mine, &ok) && comm_buf(comm, 9, e_mine, &cand) && comm_buf(comm, 10, e_max, &sel) &&
+          comm_buf(comm, 11, (size_t)W + 1 + 1, &words) && comm_buf(comm, 12, (size_t)W * e_max, &recv) &&
+          comm_buf(comm, 13, (size_t)W * e_max, &pairs) && comm_buf(comm, 14, tmp_bytes, &tmp)))
+        rc = VGPU_ERR_OOM, comm->err = "device allocation failed";
+    if (rc == VGPU_OK && injected(comm, "prm_edges")) rc = VGPU_ERR_OOM, comm->err = "injected failure";
+    selc = words ? (uint32_t*)(words + W + 1) : nullptr;
+    size_t got = 0;
+    if (rc == VGPU_OK && n) {
+        if (hipMemcpy(dk, k.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(dr, rad.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess)
+            rc = VGPU_ERR_HIP, comm->err = "parameter upload failed";
+    }
+    if (rc == VGPU_OK && qc)
+        rc = rank_fail(comm, ctx, vgpu_roadmap_knn_range(ctx, dim, V, n, qf, qc, dk, dr, kmax, nbr, dist, cnt), "knn");
+    size_t E = 0;
+    if (rc == VGPU_OK && qc) {  // candidate offsets (one host read: E sizes the validation)
+        std::vector<uint32_t> hc(qc), ho(qc + 1);
+        if (vgpu_sync(ctx) != VGPU_OK || hipMemcpy(hc.data(), cnt, qc * 4, hipMemcpyDeviceToHost) != hipSuccess)
+            rc = VGPU_ERR_HIP, comm->err = "candidate count read-back failed";
+        size_t acc = 0;
+        for (size_t i = 0; i < qc; ++i) ho[i] = (uint32_t)acc, acc += hc[i];
+        ho[qc] = (uint32_t)acc;
+        E = acc;
+        if (rc == VGPU_OK && E > e_mine) rc = VGPU_ERR_HIP, comm->err = "candidate count above its bound";
+        if (rc == VGPU_OK && hipMemcpy(off, ho.data(), (qc + 1) * 4, hipMemcpyHostToDevice) != hipSuccess)
+            rc = VGPU_ERR_HIP, comm->err = "offset upload failed";
+    }
+    if (rc == VGPU_OK && E)
+        rc = rank_fail(comm, ctx,
+                       vgpu_roadmap_edge_gather(ctx, dim, V, qf, qc, nbr, kmax, cnt, off, starts, goals), "edge gather");
+    if (rc == VGPU_OK && E)  // validate_motion(neighbor, vertex) of every candidate (prm.hh:267-276)
+        rc = rank_fail(comm, ctx, vgpu_validate_motions(ctx, r, e, starts, goals, E, ok, nullptr), "validate");
+    if (rc == VGPU_OK) rc = rank_fail(comm, ctx, vgpu_sync(ctx), "sync");
+    if (rc == VGPU_OK && E) {  // the valid pairs in query order, on the exchange stream
+        uint32_t hgot = 0;
+        if (vgpu_launch_valid_pairs((uint32_t)qf, (uint32_t)qc, nbr, kmax, cnt, off, ok, E, cand, sel, selc, tmp,
+                                    &tmp_bytes, comm->st) != hipSuccess ||
+            hipMemcpyAsync(&hgot, selc, 4, hipMemcpyDeviceToHost, comm->st) != hipSuccess ||
+            hipStreamSynchronize(comm->st) != hipSuccess)
+            rc = VGPU_ERR_HIP, comm->err = "pair selection failed";
+        got = hgot;
+    }
+    if (!words) return rc != VGPU_OK ? rc : VGPU_ERR_OOM;
+    std::vector<uint64_t> cnts;
+    rc = exchange_counts(comm, words, rc, got, cnts);  // exchange 1, always entered
+    if (rc != VGPU_OK) return rc;
+    uint64_t m = 0;
+    for (uint64_t c : cnts) m += c;
+    *n_adj = (size_t)(2 * m);
+    if (2 * m > adj_cap || (m && !adj)) {
+        comm->err = "adjacency capacity too small (*n_adj = required entries)";
+        return VGPU_ERR_INVALID_ARG;
+    }
+    if ((rc = gather_padded(comm, (const uint64_t*)sel, recv, cnts, 1, pairs, 1)) != VGPU_OK) return rc;  // exchange 2
+    return rank_fail(comm, ctx,
+                     vgpu_roadmap_assemble_device(ctx, n, (const uint32_t*)pairs, (size_t)m, offsets, adj, component),
+                     "roadmap assembly");
 }

@@ -19,6 +19,8 @@
 // keep the lower index first (nigh's tie order is not pinned: DESIGN.md).
 #include <algorithm>
 
+#include <hipcub/hipcub.hpp>
+
 #include "vgpu_device.hh"
 
 namespace vgpu {
@@ -250,6 +252,23 @@ __global__ __launch_bounds__(256) void edge_gather_kernel(const float* __restric
     }
 }
 
+// candidate e = off[i] + m of query i -> the pair (vertex q_first + i, neighbour nbr[i][m]) packed as
+// two u32 words (vertex first): the valid ones, selected in candidate order, are the pairs build_roadmap
+// connects (prm.hh:268-275) in query order, nearest first
+__global__ __launch_bounds__(256) void edge_pairs_kernel(uint32_t q_first, uint32_t n,
+                                                         const uint32_t* __restrict__ nbr, uint32_t kmax,
+                                                         const uint32_t* __restrict__ cnt,
+                                                         const uint32_t* __restrict__ off,
+                                                         unsigned long long* __restrict__ pairs)
+{
+    const size_t t = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t i = t / kmax;
+    const uint32_t m = (uint32_t)(t - i * kmax);
+    if (i >= n || m >= cnt[i]) return;
+    const unsigned long long v = q_first + (uint32_t)i, j = nbr[i * kmax + m];
+    pairs[(size_t)off[i] + m] = v | (j << 32);
+}
+
 }  // namespace vgpu
 
 template <int D, int K>
@@ -315,6 +334,25 @@ hipError_t vgpu_launch_edge_gather(const float* V, uint32_t q_first, uint32_t q_
     hipLaunchKernelGGL(vgpu::edge_gather_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, V, q_first,
                        q_count, dim, nbr, kmax, cnt, off, starts, goals);
     return hipGetLastError();
+}
+
+// The valid candidate pairs of queries q_first .. +q_count in candidate order: all[E] (scratch) then the
+// flagged selection into out[*count] (count: one device u32).  tmp == nullptr: *tmp_bytes = the
+// selection's scratch size, nothing launched.
+hipError_t vgpu_launch_valid_pairs(uint32_t q_first, uint32_t q_count, const uint32_t* nbr, uint32_t kmax,
+                                   const uint32_t* cnt, const uint32_t* off, const uint8_t* ok, size_t E,
+                                   unsigned long long* all, unsigned long long* out, uint32_t* count, void* tmp,
+                                   size_t* tmp_bytes, hipStream_t st)
+{
+    if (!tmp)
+        return hipcub::DeviceSelect::Flagged(nullptr, *tmp_bytes, all, ok, out, count, (int)std::max<size_t>(E, 1), st);
+    if (E == 0) return hipMemsetAsync(count, 0, sizeof(uint32_t), st);
+    const size_t threads = (size_t)q_count * kmax;
+    hipLaunchKernelGGL(vgpu::edge_pairs_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, q_first,
+                       q_count, nbr, kmax, cnt, off, all);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return hipcub::DeviceSelect::Flagged(tmp, *tmp_bytes, all, ok, out, count, (int)E, st);
 }
 
 }  // extern "C"

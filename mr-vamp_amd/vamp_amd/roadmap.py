@@ -18,6 +18,7 @@ without the HIP library the calls raise.
 """
 from __future__ import annotations
 
+import math
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -214,8 +215,9 @@ def build_roadmap(robot, start, goal, environment, max_iterations: int = 100000,
 # ---- the edge stage sharded over ranks (every rank holds all vertices after the all-gather) ----
 def query_split(n: int, rank: int, world: int) -> Tuple[int, int]:
     """(first, count) of this rank's queries: contiguous ranges with equal sum of prefix lengths
-    (query i scans i candidates), boundaries at n * sqrt(r / world)."""
-    b = [0] + [min(n, int(round(n * (r / world) ** 0.5))) for r in range(1, world)] + [n]
+    (query i scans i candidates), boundaries at floor(n * sqrt(r / world) + 0.5) -- the same double
+    expression as the C ABI's vgpu_query_split (vgpu_prm_edges_allgather's split)."""
+    b = [0] + [min(n, int(math.floor(n * math.sqrt(r / world) + 0.5))) for r in range(1, world)] + [n]
     return b[rank], b[rank + 1] - b[rank]
 
 
@@ -331,3 +333,119 @@ def build_roadmap_edges_sharded(torch, dist, robot, environment, V, gamma_scale:
         pairs = allgather_pairs(torch, dist, pairs, group)
     offsets, adj, comp = assemble(n, pairs.cpu().numpy())
     return Roadmap(V.cpu().numpy(), offsets, adj, comp)
+
+
+# ---- the C-level collectives (vgpu_comm_*, include/vamp_gpu.h): RCCL without torch.distributed --------
+class Comm:
+    """An RCCL communicator owned by the library (vgpu_comm_init; librccl loaded at run time): the
+    C-level sharded stages (vgpu_prm_vertices_allgather, vgpu_prm_edges_allgather) run over it.  The
+    128-byte id is made on rank 0 and shipped by the caller -- ``from_torch`` ships it over an
+    initialised torch.distributed group (any backend), which then carries no data-path traffic."""
+
+    def __init__(self, ctx, rank: int, world: int, uid: bytes):
+        import ctypes as C
+
+        from ._lib import check, load
+        self.ctx, self.rank, self.world = ctx, rank, world
+        self.h = C.c_void_p()
+        buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        check(load().vgpu_comm_init(ctx.h, rank, world, buf, C.byref(self.h)), ctx.h)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes as C
+
+        from ._lib import check, load
+        buf = (C.c_uint8 * 128)()
+        check(load().vgpu_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def from_torch(cls, torch, dist, ctx, group=None):
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        uid = cls.unique_id() if rank == 0 else bytes(128)
+        if world > 1:
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" \
+                else torch.device("cpu")
+            t = torch.tensor(list(uid), dtype=torch.uint8, device=dev)
+            dist.broadcast(t, 0, group=group)
+            uid = bytes(t.cpu().tolist())
+        return cls(ctx, rank, world, uid)
+
+    def last_error(self) -> str:
+        from ._lib import load
+        m = load().vgpu_comm_last_error(self.h)
+        return m.decode() if m else ""
+
+    def check(self, rc: int):
+        from ._lib import ERRORS, VgpuError
+        if rc != 0:
+            raise VgpuError(f"vamp_gpu: {ERRORS.get(rc, rc)}: {self.last_error()} / {self.ctx_error()}", rc)
+
+    def ctx_error(self) -> str:
+        from ._lib import load
+        m = load().vgpu_last_error(self.ctx.h)
+        return m.decode() if m else ""
+
+    def close(self):
+        from ._lib import load
+        if self.h:
+            load().vgpu_comm_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def query_split_c(n: int, rank: int, world: int) -> Tuple[int, int]:
+    """vgpu_query_split (the C edge stage's ranges)."""
+    import ctypes as C
+
+    from ._lib import check, load
+    f, c = C.c_size_t(), C.c_size_t()
+    check(load().vgpu_query_split(n, rank, world, C.byref(f), C.byref(c)))
+    return f.value, c.value
+
+
+class EdgeStageBuffers:
+    """Device outputs of vgpu_prm_edges_allgather for n vertices, grown on demand (offsets int64 [n+1],
+    adj int32, component int32 [n])."""
+
+    def __init__(self, torch, n: int, dev, adj_cap: int = 0):
+        self.torch, self.dev = torch, dev
+        self.offsets = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        self.comp = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+        self.adj = torch.empty(max(adj_cap, 1), dtype=torch.int32, device=dev)
+
+
+def build_roadmap_edges_comm(torch, robot, environment, V, comm: "Comm", gamma_scale: float = 2.0, ctx=None,
+                             bufs: Optional[EdgeStageBuffers] = None):
+    """build_roadmap's edge stage through the C ABI's collective (vgpu_prm_edges_allgather): the queries
+    split over the communicator's ranks, one exchange of the valid pairs, the roadmap assembled on every
+    rank's device.  V: [n, dim] float32 CUDA tensor, identical on all ranks.  Returns (offsets, adj,
+    component) device tensors, equal to build_roadmap_edges_sharded's graph."""
+    import ctypes as C
+
+    from ._lib import load
+    ctx = ctx or comm.ctx
+    n, dim = V.shape
+    V = V.contiguous()
+    if bufs is None:  # adjacency sized by the candidate bound (query i returns at most min(k_i, i))
+        k, _ = prm_neighbor_params(dim, robot.space_measure(), n, gamma_scale)
+        bound = int(np.minimum(k.astype(np.int64), np.arange(n, dtype=np.int64)).sum())
+        bufs = EdgeStageBuffers(torch, n, V.device, 2 * bound)
+    n_adj = C.c_size_t()
+    lib = load()
+    args = lambda: (ctx.h, comm.h, C.byref(robot.c_robot), environment.handle(ctx), V.data_ptr(), n,  # noqa: E731
+                    robot.space_measure(), float(gamma_scale), bufs.offsets.data_ptr(), bufs.adj.data_ptr(),
+                    bufs.adj.numel(), C.byref(n_adj), bufs.comp.data_ptr())
+    rc = lib.vgpu_prm_edges_allgather(*args())
+    if rc == -1 and n_adj.value > bufs.adj.numel():  # too small: every rank saw the same size -> grow, retry
+        bufs.adj = torch.empty(n_adj.value, dtype=torch.int32, device=V.device)
+        rc = lib.vgpu_prm_edges_allgather(*args())
+    comm.check(rc)
+    return bufs.offsets, bufs.adj[:n_adj.value], bufs.comp[:n]

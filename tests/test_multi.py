@@ -41,7 +41,11 @@ def multi():
     assert vamp_amd.context(0) is not None
     lib = load()
     m = C.c_void_p()
-    devs = (C.c_int * 2)(0, 0)  # two contexts on one device: two host threads, two contiguous ranges
+    import torch
+    # two devices when the box has them (device placement of the per-thread work is then exercised);
+    # else two contexts on one device: two host threads, two contiguous ranges
+    pair = (0, 1) if torch.cuda.device_count() > 1 else (0, 0)
+    devs = (C.c_int * 2)(*pair)
     check(lib.vgpu_multi_create(devs, 2, C.byref(m)))
     yield vamp_amd, lib, m
     lib.vgpu_multi_destroy(m)
@@ -124,3 +128,118 @@ def test_rccl_vertex_allgather_world1(oracle):
         assert np.array_equal(draws[:cnt.value].cpu().numpy(), 1 + np.nonzero(v)[0])
     finally:
         lib.vgpu_comm_destroy(comm)
+
+
+def _comm(vamp, ctx):
+    from vamp_amd import roadmap
+    try:
+        uid = roadmap.Comm.unique_id()
+    except Exception as e:  # librccl not loadable: VGPU_ERR_UNSUPPORTED
+        pytest.skip(f"RCCL unavailable: {e}")
+    return roadmap.Comm(ctx, 0, 1, uid)
+
+
+@pytest.mark.gpu
+def test_rccl_edges_allgather_world1_equals_oracle(oracle):
+    """vgpu_prm_edges_allgather at world size 1 (query split, kNN, validate, pair selection, the two
+    exchanges, device assembly) == build_roadmap_edges_sharded == the oracle's build_roadmap graph"""
+    import torch
+
+    import vamp_amd as vamp
+    from vamp_amd import roadmap
+    ctx = vamp.context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    comm = _comm(vamp, ctx)
+    try:
+        rng = np.random.default_rng(24)
+        oenv = random_scene(oracle, rng, 4, 4, 2)
+        env = gpu_env_from_oracle(vamp, oenv)
+        q = oracle.robot_scale("fetch", rng.random((5000, 8), dtype=F))
+        V = q[oracle.robot_fkcc_threads("fetch", oenv, q)][:2000]
+        Vd = torch.from_numpy(V).cuda()
+        off, adj, comp = roadmap.build_roadmap_edges_comm(torch, vamp.fetch, env, Vd, comm)
+        off, adj, comp = off.cpu().numpy(), adj.cpu().numpy(), comp.cpu().numpy()
+        edges, _ = oracle.build_roadmap_edges("fetch", oenv, V)
+        assert [adj[off[i]:off[i + 1]].tolist() for i in range(len(V))] == edges
+        assert np.array_equal(comp, oracle.components(len(V), edges))
+        rm = roadmap.build_roadmap_edges_sharded(torch, None, vamp.fetch, env, Vd)
+        assert np.array_equal(off, rm.offsets) and np.array_equal(adj.view(np.uint32), rm.adj)
+        # a second call on the same communicator reuses its buffers and gives the same graph
+        off2, adj2, _ = roadmap.build_roadmap_edges_comm(torch, vamp.fetch, env, Vd, comm)
+        assert np.array_equal(off2.cpu().numpy(), off) and np.array_equal(adj2.cpu().numpy(), adj)
+    finally:
+        comm.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("site", ["prm_vertices", "prm_edges"])
+def test_rccl_failure_is_reported_not_hung(oracle, site, monkeypatch):
+    """A rank-local failure (VGPU_FAULT_INJECT forces the allocation-failure path) still enters the count
+    exchange and comes back as an error code from every rank -- here world size 1 -- instead of leaving
+    peers inside an all-gather; the communicator stays usable for the next call."""
+    import ctypes as Cc
+
+    import torch
+
+    import vamp_amd as vamp
+    from vamp_amd import roadmap
+    from vamp_amd._lib import load
+    ctx = vamp.context(0)
+    ctx.set_stream(torch.cuda.current_stream().cuda_stream)
+    comm = _comm(vamp, ctx)
+    lib = load()
+    try:
+        env = vamp.Environment()
+        env.add_sphere(vamp.Sphere([0.5, 0.0, 0.5], 0.3))
+        n = 20000
+        rows = torch.zeros((n, 7), dtype=torch.float32, device="cuda")
+        draws = torch.zeros(n, dtype=torch.int64, device="cuda")
+        cnt = Cc.c_size_t()
+
+        def vertices():
+            return lib.vgpu_prm_vertices_allgather(ctx.h, comm.h, Cc.byref(vamp.panda_0_0.c_robot), env.handle(ctx), 1,
+                                                   n, Cc.c_void_p(rows.data_ptr()), Cc.c_void_p(draws.data_ptr()), n,
+                                                   Cc.byref(cnt))
+
+        def edges():
+            V = rows[:2000].contiguous()
+            bufs = roadmap.EdgeStageBuffers(torch, 2000, V.device, 200000)
+            n_adj = Cc.c_size_t()
+            return lib.vgpu_prm_edges_allgather(ctx.h, comm.h, Cc.byref(vamp.panda_0_0.c_robot), env.handle(ctx),
+                                                V.data_ptr(), 2000, vamp.panda_0_0.space_measure(), 2.0,
+                                                bufs.offsets.data_ptr(), bufs.adj.data_ptr(), bufs.adj.numel(),
+                                                Cc.byref(n_adj), bufs.comp.data_ptr())
+
+        assert vertices() == 0 and cnt.value > 2000
+        call = vertices if site == "prm_vertices" else edges
+        monkeypatch.setenv("VGPU_FAULT_INJECT", site)
+        assert call() == -3  # VGPU_ERR_OOM, returned (not hung)
+        assert "injected" in comm.last_error()
+        monkeypatch.setenv("VGPU_FAULT_INJECT", site + "@1")  # another rank's fault: not this one
+        assert call() == 0
+        monkeypatch.delenv("VGPU_FAULT_INJECT")
+        assert call() == 0
+        # a capacity too small is reported to every rank alike
+        assert lib.vgpu_prm_vertices_allgather(ctx.h, comm.h, Cc.byref(vamp.panda_0_0.c_robot), env.handle(ctx), 1, n,
+                                               Cc.c_void_p(rows.data_ptr()), Cc.c_void_p(draws.data_ptr()), 10,
+                                               Cc.byref(cnt)) == -1
+    finally:
+        comm.close()
+
+
+@pytest.mark.gpu
+def test_host_staging_lands_on_the_context_device():
+    """vgpu_*_host stage their buffers after selecting the context's device (HIP's current device is per
+    thread): with a context on device 1 and the calling thread on device 0, the staging buffer must live
+    on device 1.  Needs two GPUs; skipped (and visible as skipped) on a one-GPU box."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU: the cross-device placement case needs device 1")
+    import vamp_amd as vamp
+    ctx1 = vamp.context(1)
+    torch.cuda.set_device(0)
+    env = vamp.Environment()
+    env.add_sphere(vamp.Sphere([0.5, 0.0, 0.5], 0.2))
+    q = np.zeros((64, 7), F)
+    got = vamp.panda_0_0.fkcc_batch(q, env, ctx1)
+    assert got.shape == (64,)

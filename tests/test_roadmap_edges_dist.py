@@ -91,3 +91,12 @@ def test_sharded_edges_gloo(world):
         got = [adj[off[i]:off[i + 1]].tolist() for i in range(len(V))]
         assert got == edges, rank
         assert np.array_equal(cmp_, comp), rank
+
+
+def test_query_split_python_equals_c_abi():
+    """roadmap.query_split (the torch path) and vgpu_query_split (the C collective) draw the same ranges"""
+    from vamp_amd import roadmap
+    for n in (0, 1, 2, 5, 99, 100000, 2681709, 4_000_000):
+        for w in (1, 2, 3, 4, 7, 8):
+            for r in range(w):
+                assert roadmap.query_split(n, r, w) == roadmap.query_split_c(n, r, w), (n, r, w)

@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""Per-workload profile record from tools/pmc_drive.py runs (development tool).
+
+    python tools/pmc_report.py W DIR OUT.json
+
+DIR holds the rocprofv3 outputs of one workload: trace/ (--kernel-trace --stats) and pmc_<i>/ (one
+--pmc pass each), plus gpurun_out/pmc_inputs/W.meta.json.  Only the dispatches between the two
+spin_kernel markers pmc_drive.py places around its calls are counted; every figure is divided by the
+profiled call count (warm-up + measured), giving per-call kernel time, SQ instruction counts, wave
+cycles and HBM bytes (2 x FETCH_SIZE + WRITE_SIZE, per MI355X_MICROARCH.md's gfx950 correction).
+bench.py reads the record's per-unit figures to report executed VALU-issue and FP fractions.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2  # 1024 SIMDs, one wave64 VALU instruction per 2 cycles at 2.4 GHz
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "").replace("vgpu::", "").strip()
+
+
+def window(rows):
+    """rows between the first and last spin_kernel marker (by Dispatch_Id)"""
+    marks = sorted(int(r["Dispatch_Id"]) for r in rows if "spin_kernel" in r["Kernel_Name"])
+    if len(marks) < 2:
+        raise SystemExit("markers not found")
+    lo, hi = marks[0], marks[-1]
+    return [r for r in rows if lo < int(r["Dispatch_Id"]) < hi]
+
+
+def main():
+    w, d, out = sys.argv[1:4]
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    meta = json.load(open(os.path.join(root, "gpurun_out", "pmc_inputs", f"{w}.meta.json")))
+    calls = meta["calls_profiled"]
+    kern = collections.defaultdict(lambda: {"dispatches": 0, "ns": 0.0})
+    tr = glob.glob(f"{d}/trace/**/*kernel_trace.csv", recursive=True)
+    for f in tr:
+        for r in window(list(csv.DictReader(open(f)))):
+            k = kern[short(r["Kernel_Name"])]
+            k["dispatches"] += 1
+            k["ns"] += float(r["End_Timestamp"]) - float(r["Start_Timestamp"])
+    ctr = collections.defaultdict(lambda: collections.defaultdict(float))
+    for f in glob.glob(f"{d}/pmc_*/**/*counter_collection.csv", recursive=True):
+        for r in window(list(csv.DictReader(open(f)))):
+            ctr[short(r["Kernel_Name"])][r["Counter_Name"]] += float(r["Counter_Value"])
+    kernels = {}
+    tot = collections.defaultdict(float)
+    for name in sorted(set(kern) | set(ctr)):
+        rec = {"dispatches_per_call": kern[name]["dispatches"] / calls, "ms_per_call": kern[name]["ns"] / calls / 1e6}
+        for c, v in ctr[name].items():
+            rec[c] = v / calls
+        kernels[name] = rec
+        tot["ms"] += rec["ms_per_call"]
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32",
+                  "SQ_INSTS_VALU_TRANS_F32", "SQ_INSTS_SALU", "SQ_INSTS_SMEM", "SQ_WAVES", "SQ_WAVE_CYCLES",
+                  "SQ_WAIT_INST_ANY", "FETCH_SIZE", "WRITE_SIZE"):
+            tot[c] += rec.get(c, 0.0)
+    units = meta["units_per_call"]
+    fp = 64.0 * (tot["SQ_INSTS_VALU_ADD_F32"] + tot["SQ_INSTS_VALU_MUL_F32"] + 2 * tot["SQ_INSTS_VALU_FMA_F32"])
+    rec = {
+        "workload": w, "unit": meta["unit"], "units_per_call": units, "calls_profiled": calls,
+        "ms_per_call_events": meta["ms_per_call"],
+        "kernel_ms_per_call": tot["ms"],
+        "valu_insts_per_call": tot["SQ_INSTS_VALU"],
+        "fp32_ops_per_call": fp,
+        "hbm_bytes_per_call": (2 * tot["FETCH_SIZE"] + tot["WRITE_SIZE"]) * 1024.0 if tot["FETCH_SIZE"] else None,
+        "wait_frac": tot["SQ_WAIT_INST_ANY"] / tot["SQ_WAVE_CYCLES"] if tot["SQ_WAVE_CYCLES"] else None,
+        "per_unit": {"valu_insts": tot["SQ_INSTS_VALU"] / units, "fp32_ops": fp / units,
+                     "fp_insts_share_of_valu": (tot["SQ_INSTS_VALU_ADD_F32"] + tot["SQ_INSTS_VALU_MUL_F32"] +
+                                                tot["SQ_INSTS_VALU_FMA_F32"]) / tot["SQ_INSTS_VALU"]
+                     if tot["SQ_INSTS_VALU"] else None},
+        "valu_issue_frac_at_trace_time": tot["SQ_INSTS_VALU"] / (tot["ms"] * 1e-3) / VALU_ISSUE_PER_S if tot["ms"] else None,
+        "kernels": kernels,
+        "method": "tools/pmc_drive.py run (warm-up + measured calls between spin_kernel markers) under rocprofv3 "
+                  "--kernel-trace --stats and one --pmc pass per counter group; per-call = totals / calls_profiled",
+    }
+    with open(out, "w") as f:
+        json.dump(rec, f, indent=1)
+    print(json.dumps({k: v for k, v in rec.items() if k != "kernels"}))
+
+
+if __name__ == "__main__":
+    main()
