@@ -312,11 +312,15 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    s0.record(stream)
     for _ in range(a.steps):
         n_vertices = step()
+    s1.record(stream)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
+    step_ev_ms = s0.elapsed_time(s1) / a.steps
     if world > 1:
         dist.barrier()
     wall_max, units_all = reduce_over_ranks(dist, torch, t1 - t0, float(n), dev, world)
@@ -388,7 +392,10 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         "roofline": {"kernel": "fetch_sample_fkcc_kernel", "bound": "valu", "achieved": achieved,
                      "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
                      "traffic": None, "kernel_ms": kern_ms, "algorithmic_flops_per_sample": f_sample,
-                     "algorithmic_bytes_per_sample": 8 * 4 + 1},
+                     "algorithmic_bytes_per_sample": 8 * 4 + 1, "step_ms_events": step_ev_ms,
+                     "frac_meaning": FRAC_MEANING,
+                     "executed": executed_record("fetch_prm", n, step_ev_ms) if world == 1 else None,
+                     "executed_note": "over the whole step (fused sample + fkcc, compaction, index conversion)"},
         "cpu_baseline": cpu,
         "parity": parity,
     }
@@ -398,11 +405,14 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
 def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     """BASELINE configs[3] edge stage (SURVEY §8f rank 1): Roadmap::build_roadmap's graph over the
     first V vertices of the Fetch vertex sequence (two valid draws as start and goal, then the
-    valid Halton<8> draws in order; MBM table_pick scene): every vertex's PRM* neighbour query
-    (causal kNN kernel), validate_motion of every candidate edge, the exchange of valid pairs and
-    the host adjacency/component assembly.  Queries split over ranks by equal prefix work; total
-    vertices fixed (strong scaling).  One step = the whole edge stage."""
+    valid Halton<8> draws in order; MBM table_pick scene).  One step = the C ABI's sharded stage
+    vgpu_prm_edges_allgather (each rank's queries by equal prefix work: neighbour queries, candidate
+    gather, validate_motion of every candidate, device pair selection; one RCCL all-gather of the
+    valid pairs; the roadmap assembled on every rank's device) plus the copy of the Roadmap
+    (offsets, adjacency, components) into pinned host memory -- the host Roadmap the reference
+    returns.  Total vertices fixed (strong scaling)."""
     from vamp_amd import roadmap
+    from vamp_amd._lib import check, load
 
     env, fx = fetch_scene(vamp)
     robot = vamp.fetch
@@ -411,26 +421,37 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     rows, _, cnt = roadmap.sample_valid_shard(torch, robot, env, 1, draws, ctx, dev)
     n = min(a.vertices, cnt)
     V = rows[:n].contiguous()
+    del rows
     k_np, r_np = roadmap.prm_neighbor_params(dim, robot.space_measure(), n)
     kmax = int(max(1, min(int(k_np.max()), n)))
-    k = torch.from_numpy(k_np.view(np.int32)).to(dev)
-    r = torch.from_numpy(r_np).to(dev)
-    qf, qc = roadmap.query_split(n, rank, world)
+    bound = int(np.minimum(k_np.astype(np.int64), np.arange(n, dtype=np.int64)).sum())
+    comm = roadmap.Comm.from_torch(torch, dist, ctx)
+    bufs = roadmap.EdgeStageBuffers(torch, n, dev, 2 * bound)
+    off_h = torch.empty(n + 1, dtype=torch.int64, pin_memory=True)
+    adj_h = torch.empty(max(2 * bound, 1), dtype=torch.int32, pin_memory=True)
+    comp_h = torch.empty(max(n, 1), dtype=torch.int32, pin_memory=True)
     info = {}
 
     def step():
-        pairs = roadmap.edges_shard(torch, robot, env, V, k, r, kmax, qf, qc, ctx)
-        if world > 1:
-            pairs = roadmap.allgather_pairs(torch, dist, pairs)
-        # adjacency + components on the device, then the host Roadmap the reference returns
-        off, adj, comp = roadmap.assemble_device(torch, n, pairs, ctx)
-        info.update(pairs=int(pairs.shape[0]), off=off.cpu(), adj=adj.cpu(), comp=comp.cpu())
+        off, adj, comp = roadmap.build_roadmap_edges_comm(torch, robot, env, V, comm, ctx=ctx, bufs=bufs)
+        m = adj.numel()
+        off_h.copy_(off, non_blocking=True)
+        adj_h[:m].copy_(adj, non_blocking=True)
+        comp_h[:n].copy_(comp, non_blocking=True)
+        info["n_adj"] = m
 
-    wall = timed_steps(a, torch, dist, dev, world, step)
+    ev = []
+    wall = timed_steps(a, torch, dist, dev, world, step, ev)
+    step_ev_ms = ev[0]
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(n) / world, dev, world)
-    # where one step's time goes (an extra, synchronised step outside the timed region): kNN + edge gather +
-    # validation on the GPU, the pair exchange, the device-to-host copy of the valid pairs, host assembly
-    phases = {}
+    # parity of the step's graph: the torch-path pieces (edges_shard = kNN + gather + validate on this rank's
+    # queries, all-gather over torch.distributed) assembled on the host by vgpu_roadmap_assemble
+    k = torch.from_numpy(k_np.view(np.int32)).to(dev)
+    r = torch.from_numpy(r_np).to(dev)
+    qf, qc = roadmap.query_split(n, rank, world)
+    assert (qf, qc) == roadmap.query_split_c(n, rank, world)
+    # where one step's time goes (extra synchronised pieces outside the timed region): kNN, candidate gather
+    # + validation, the pair exchange, device assembly, the device-to-host copy of the Roadmap
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     pairs = roadmap.edges_shard(torch, robot, env, V, k, r, kmax, qf, qc, ctx)
@@ -443,32 +464,23 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     off_d, adj_d, comp_d = roadmap.assemble_device(torch, n, pairs, ctx)
     torch.cuda.synchronize(dev)
     t3 = time.perf_counter()
-    off_h, adj_h, comp_h = off_d.cpu().numpy(), adj_d.cpu().numpy(), comp_d.cpu().numpy()
-    t4 = time.perf_counter()
     ph = pairs.cpu().numpy()
-    t5 = time.perf_counter()
-    off_r, adj_r, comp_r = roadmap.assemble(n, ph)  # the host assembly: the checker, and its time
-    t6 = time.perf_counter()
-    assembly_equal = bool(np.array_equal(off_h, off_r) and np.array_equal(adj_h.view(np.uint32), adj_r) and
-                          np.array_equal(comp_h.view(np.uint32), comp_r))
-    info["components"] = int(len(np.unique(comp_h)))
-    phases = {"gpu_knn_gather_validate_ms": (t1 - t0) * 1e3, "exchange_ms": (t2 - t1) * 1e3,
-              "gpu_assembly_ms": (t3 - t2) * 1e3, "d2h_roadmap_ms": (t4 - t3) * 1e3,
-              "host_assembly_ms_for_comparison": (t6 - t5) * 1e3, "d2h_pairs_ms": (t5 - t4) * 1e3,
-              "pairs_bytes": int(ph.nbytes), "device_assembly_equals_host": assembly_equal}
-    del pairs, ph, off_d, adj_d, comp_d, off_h, adj_h, comp_h, off_r, adj_r, comp_r
-    for key in ("off", "adj", "comp"):
-        info.pop(key, None)
-    # the kNN kernel alone (this rank's queries), HIP events on the launch stream, in both methods
-    # of vgpu_set_knn_mode: brute force (the roofline: its flops are the ones executed) and the
-    # spatial index (auto's choice from 65536 vertices; same lists, compared below)
+    off_r, adj_r, comp_r = roadmap.assemble(n, ph)  # the host assembly: the checker
+    m = info["n_adj"]
+    step_equal = bool(np.array_equal(off_h.numpy(), off_r) and np.array_equal(adj_h[:m].numpy().view(np.uint32), adj_r)
+                      and np.array_equal(comp_h[:n].numpy().view(np.uint32), comp_r))
+    info["components"] = int(len(np.unique(comp_r)))
+    info["pairs"] = int(len(ph))
+    del pairs, ph, off_d, adj_d, comp_d, off_r, adj_r, comp_r
+    # the pieces alone with HIP events on the launch stream: the kNN kernel (both methods of vgpu_set_knn_mode:
+    # brute force -- the roofline, its flops are the ones executed -- and the spatial index, auto's choice from
+    # 65536 vertices), then gather + validate_motion of the candidates
     nbr = torch.empty((max(qc, 1), kmax), dtype=torch.int32, device=dev)
     dd = torch.empty((max(qc, 1), kmax), dtype=torch.float32, device=dev)
     cc = torch.empty(max(qc, 1), dtype=torch.int32, device=dev)
-    from vamp_amd._lib import check, load
     knn = {}
     lists = {}
-    for mode, name in ((1, "brute"), (2, "index")):
+    for mode, name in ((2, "index"), (1, "brute")):
         check(load().vgpu_set_knn_mode(ctx.h, mode), ctx.h)
         reps = 1 if n >= 1_000_000 else a.steps
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -481,32 +493,65 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         knn[name] = e0.elapsed_time(e1) / reps
         lists[name] = (nbr[:qc].clone(), cc[:qc].clone())
     check(load().vgpu_set_knn_mode(ctx.h, 0), ctx.h)
-    knn_ms = knn["brute"]
-    (nb_b, cc_b), (nb_i, cc_i) = lists["brute"], lists["index"]
-    width = torch.arange(kmax, device=dev)[None, :] < cc_b[:, None].long()
-    index_equals_brute = bool(torch.equal(cc_b, cc_i)) and bool(torch.equal(nb_b[width], nb_i[width]))
-    del lists, nb_b, nb_i, cc_b, cc_i
-    candidates = int(cc[:qc].long().sum())
+    if "brute" in lists:
+        (nb_b, cc_b), (nb_i, cc_i) = lists["brute"], lists["index"]
+        width = torch.arange(kmax, device=dev)[None, :] < cc_b[:, None].long()
+        index_equals_brute = bool(torch.equal(cc_b, cc_i)) and bool(torch.equal(nb_b[width], nb_i[width]))
+        del nb_b, cc_b
+    else:
+        index_equals_brute = None
+    nb_i, cc_i = lists["index"]
+    del lists
+    candidates = int(cc_i.long().sum())
+    offs = torch.zeros(qc + 1, dtype=torch.int32, device=dev)
+    offs[1:] = torch.cumsum(cc_i, 0)
+    starts = torch.empty((max(candidates, 1), dim), dtype=torch.float32, device=dev)
+    goals = torch.empty_like(starts)
+    okc = torch.empty(max(candidates, 1), dtype=torch.uint8, device=dev)
+    nbc = torch.empty(max(candidates, 1), dtype=torch.int32, device=dev)
+    e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+    e0.record(stream)
+    check(load().vgpu_roadmap_edge_gather(ctx.h, dim, V.data_ptr(), qf, qc, nb_i.data_ptr(), kmax, cc_i.data_ptr(),
+                                          offs.data_ptr(), starts.data_ptr(), goals.data_ptr()), ctx.h)
+    e1.record(stream)
+    robot.validate_device(starts.data_ptr(), goals.data_ptr(), candidates, env, okc.data_ptr(), nbc.data_ptr(), ctx=ctx)
+    e2.record(stream)
+    torch.cuda.synchronize(dev)
+    gather_ms, validate_ms = e0.elapsed_time(e1), e1.elapsed_time(e2)
+    cand_interp = float(8 * nbc[:candidates].long().sum().item())
+    del starts, goals, okc, nbc, nb_i, cc_i, offs
+    phases = {"knn_index_ms": knn["index"], "gather_ms": gather_ms, "validate_ms": validate_ms,
+              "validate_candidates": candidates, "validate_interpolants_full_mask_count": cand_interp,
+              "validate_interpolants_per_s_full_mask_count": cand_interp / (validate_ms * 1e-3),
+              "rest_of_step_ms (selection, exchange, assembly, D2H)": step_ev_ms - knn["index"] - gather_ms - validate_ms,
+              "torch_path_gpu_knn_gather_validate_ms": (t1 - t0) * 1e3, "torch_path_exchange_ms": (t2 - t1) * 1e3,
+              "torch_path_device_assembly_ms": (t3 - t2) * 1e3,
+              "step_roadmap_equals_host_assembly_of_torch_path_pairs": step_equal,
+              "roadmap_d2h_bytes": int((n + 1) * 8 + m * 4 + n * 4)}
+    comm.close()
     if rank != 0:
         return
     # algorithmic work of the brute-force query kernel: one Space<8>::distance per (vertex, earlier
     # vertex) pair = 8 sub + 8 mul + 7 add + 1 sqrt (nn.hh:53-57)
     pairs_scanned = sum(range(qf, qf + qc))
     flops = 24.0 * pairs_scanned
-    achieved = flops / (knn_ms * 1e-3) / 1e12
+    knn_ms = knn.get("brute")
+    achieved = flops / (knn_ms * 1e-3) / 1e12 if knn_ms else None
     cpu = None
     if not a.no_cpu and world == 1:
         # the reference's host path for the stage: an exact k-d tree neighbour query (nigh's role,
         # planning/nn.hh:89-95; csrc/cpu/vcpu_roadmap.cpp) and validate_motion on the AVX2 rake
-        # (csrc/cpu), over a prefix of the same vertex sequence, all host threads of this rank
-        threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        # (csrc/cpu), over a prefix of the same vertex sequence, all host threads of this rank; at full
+        # size (>= 1M vertices) the prefix is at least 1M vertices
+        threads = host_threads()
         Vh = V.cpu().numpy()
-        m = 4000
+        m_min = min(n, 1_000_000) if n >= 1_000_000 else 0
+        m = min(n, max(4000, m_min))
         while True:  # grow the prefix until the stage takes ~cpu_seconds / 3
             t = time.perf_counter()
             nb_, _, cn_ = roadmap.cpu_knn(Vh[:m], np.arange(m), robot.space_measure(), threads=threads)
             qi = np.repeat(np.arange(m), cn_.astype(np.int64))
-            qm = np.concatenate([np.arange(c) for c in cn_]).astype(np.int64)
+            qm = (np.arange(len(qi)) - np.repeat(np.cumsum(cn_.astype(np.int64)) - cn_, cn_.astype(np.int64)))
             qj = nb_[qi, qm].astype(np.int64)
             t_nn = time.perf_counter() - t
             robot.cpu_validate_batch(Vh[qj], Vh[qi], env, threads=threads)
@@ -534,43 +579,88 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         "dtype": "f32",
         "data": "synthetic (the Halton<8> vertex sequence of configs[3] on MBM table_pick_fetch scene0001)",
         "config": {"workload": f"BASELINE configs[3] edge stage: build_roadmap graph over {n} Fetch vertices, queries "
-                               f"split over {world} GPU(s), one exchange of valid pairs",
+                               f"split over {world} GPU(s) (vgpu_prm_edges_allgather, C ABI over RCCL), one exchange "
+                               f"of valid pairs, Roadmap copied to pinned host memory",
                    "robot": "Fetch", "vertices": n, "kmax": kmax, "candidate_edges_rank0": candidates,
                    "valid_edges": info.get("pairs"), "components": info.get("components"),
                    "parallelism": f"dp{world} (query ranges of equal prefix work, one all-gather)"},
-        "roofline": {"kernel": "knn_kernel<8, K> (causal neighbour queries)", "bound": "valu", "achieved": achieved,
-                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-                     "traffic": None, "kernel_ms": knn_ms, "algorithmic_flops_per_vertex_pair": 24,
-                     "vertex_pairs_rank0": pairs_scanned,
+        "roofline": {"kernel": "knn_kernel<8, K> (causal neighbour queries, brute force)", "bound": "valu",
+                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP32_PEAK_TFLOPS if achieved else None,
+                     "traffic": None, "kernel_ms": knn_ms, "step_kernel_ms_events": step_ev_ms,
+                     "algorithmic_flops_per_vertex_pair": 24, "vertex_pairs_rank0": pairs_scanned,
                      "knn_ms": knn, "knn_mode_in_step": "index" if n >= 65536 else "brute",
                      "index_equals_brute": index_equals_brute,
+                     "executed": executed_record("prm_edges" if n <= 200_000 else "prm_edges_full", n, step_ev_ms),
                      "note": "roofline of the brute-force kernel (every pair evaluated); the index kernel's time is "
-                             "beside it, not priced in flops (it skips pairs)"},
+                             "beside it, not priced in flops (it skips pairs); `executed` is over the whole step"},
         "cpu_baseline": cpu,
         "phases": phases,
     }
     print(json.dumps(line), flush=True)
-    if not (index_equals_brute and phases.get("device_assembly_equals_host", True)):
-        print("PARITY FAILURE (kNN index vs brute force, or device vs host roadmap assembly)", file=sys.stderr)
+    if not (index_equals_brute is not False and step_equal):
+        print("PARITY FAILURE (kNN index vs brute force, or the C edge stage vs the host assembly)", file=sys.stderr)
         sys.exit(3)
 
 
-def timed_steps(a, torch, dist, dev, world, step):
-    """warmup, then exactly `steps` steps between barrier + synchronize; returns wall seconds"""
+def timed_steps(a, torch, dist, dev, world, step, events=None):
+    """warmup, then exactly `steps` steps between barrier + synchronize; returns wall seconds.  events: a
+    list that receives the per-step milliseconds between HIP events recorded on the current (launch)
+    stream around the steps"""
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    e0.record()
     for _ in range(a.steps):
         step()
+    e1.record()
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
+    if events is not None:
+        events.append(e0.elapsed_time(e1) / a.steps)
     return t1 - t0
+
+
+VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2  # 1024 SIMDs x one wave64 VALU instruction per 2 cycles at 2.4 GHz
+
+
+def executed_record(workload, units, kernel_ms):
+    """Hardware utilisation beside the reference-work `frac`: the executed VALU instructions and FP32
+    operations per unit from the committed PMC record of the same workload (profiles/r04_prof_<w>.json:
+    tools/pmc_drive.py under rocprofv3, tools/pmc_report.py), times this run's units, over this run's
+    kernel time.  valu_issue_frac = SQ_INSTS_VALU / (time x 1.2288e12 wave-instructions/s);
+    fp32_exec_frac = 64 x (ADD + MUL + 2 FMA) / time / peak."""
+    path = os.path.join(ROOT, "profiles", f"r04_prof_{workload}.json")
+    if not os.path.exists(path) or not kernel_ms:
+        return None
+    with open(path) as f:
+        rec = json.load(f)
+    pu = rec.get("per_unit") or {}
+    if not pu.get("valu_insts"):
+        return None
+    t = kernel_ms * 1e-3
+    hbm = rec.get("hbm_bytes_per_call")
+    return {"valu_issue_frac": pu["valu_insts"] * units / t / VALU_ISSUE_PER_S,
+            "fp32_exec_frac": pu["fp32_ops"] * units / t / 1e12 / FP32_PEAK_TFLOPS,
+            "fp_share_of_valu_insts": pu.get("fp_insts_share_of_valu"),
+            "wait_frac": rec.get("wait_frac"),
+            "valu_insts_per_unit": pu["valu_insts"], "fp32_ops_per_unit": pu["fp32_ops"],
+            "hbm_bytes_per_call_pmc": hbm * units / rec["units_per_call"] if hbm else None,
+            "pmc_kernel_ms_per_call": rec.get("kernel_ms_per_call"), "pmc_units_per_call": rec.get("units_per_call"),
+            "source": os.path.relpath(path, ROOT) + " (committed PMC of the same workload's step; per-unit counts x "
+                                                   "this run's units / this run's kernel time)"}
+
+
+FRAC_MEANING = ("reference-work throughput: the float ops the reference executes for these inputs (its early exits "
+                "included, counted by the instrumented oracle) / kernel time / FP32 peak -- work the GPU skips (the "
+                "wrist gate, bounding-first inter-arm tests) still counts; `executed` is the hardware utilisation")
 
 
 def contract_line(a, world, wall_max, units_all, metric, unit, scaling, data, config, roofline, cpu):
@@ -646,7 +736,9 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         else:
             robot.validate_device(starts.data_ptr(), goals.data_ptr(), E, env, okd.data_ptr(), nb.data_ptr(), ctx)
 
-    wall = timed_steps(a, torch, dist, dev, world, step)
+    ev = []
+    wall = timed_steps(a, torch, dist, dev, world, step, ev)
+    kern_ms = ev[0]
     # rake/early-exit units from the CPU rake on the same edges (bit-identical results), as configs[1]
     _, c_nb, c_ne = robot.cpu_validate_batch(starts.cpu().numpy(), goals.cpu().numpy(), env, threads=host_threads())
     units = float(8 * c_ne.astype(np.int64).sum())
@@ -657,7 +749,7 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     s_np, g_np = starts[:256].cpu().numpy(), goals[:256].cpu().numpy()
     fl = op.pair_validate_flops(oenv, s_np, g_np)  # executed float ops per edge, reference semantics
     f_edge = float(np.mean(fl))
-    kern_s = wall / a.steps
+    kern_s = kern_ms * 1e-3
     achieved = f_edge * E / kern_s / 1e12
     cpu = None
     parity = None
@@ -695,7 +787,9 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "parallelism": f"dp{world} (independent edge shards, no collective)"},
         {"kernel": "pair_validate_head/tail kernels (one validate_motions call)", "bound": "valu",
          "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-         "traffic": None, "algorithmic_flops_per_edge": f_edge, "step_ms": kern_s * 1e3},
+         "traffic": None, "algorithmic_flops_per_edge": f_edge, "kernel_ms": kern_ms,
+         "step_ms_wall": wall / a.steps * 1e3, "frac_meaning": FRAC_MEANING,
+         "executed": executed_record("pair", E, kern_ms) if not strong else None},
         cpu)
     line["counting"] = "rake_early_exit (8 x rake blocks the reference evaluates)"
     line["value_full_mask_count"] = units_full_all * a.steps / wall_max
@@ -801,7 +895,9 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     def step():
         robot.fkcc_device(q.data_ptr(), N, env, ok.data_ptr(), ctx)
 
-    wall = timed_steps(a, torch, dist, dev, world, step)
+    ev = []
+    wall = timed_steps(a, torch, dist, dev, world, step, ev)
+    kern_ms = ev[0]
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(N), dev, world)
     # configs[2]'s "1M collision queries" as raw CAPT::collides_simd sphere queries (scenes.raw_queries:
     # x, y ~ U[-1, 1], z ~ U[0, 1.2], r ~ U[r_min, r_max]), outside the contract's timed region
@@ -828,6 +924,20 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     env.handle(ctx)
     torch.cuda.synchronize(dev)
     upload_ms = (time.perf_counter() - t) * 1e3
+    # an incremental change (Environment.attach / detach, environment.cc:161-163): only the blob's tail is
+    # re-sent, the cloud and its cell grid stay (vgpu_env_upload_stats counts the grid builds)
+    from vamp_amd._lib import check as _check, load as _load
+    att = vamp.Attachment([0.0, 0.0, 0.1], [0.0, 0.0, 0.0, 1.0])
+    att.add_sphere(vamp.Sphere([0.0, 0.0, 0.05], 0.03))
+    st0 = env.upload_stats(ctx)
+    t = time.perf_counter()
+    for _ in range(10):
+        env.attach(att)
+        _check(_load().vgpu_env_upload(env.handle(ctx)), ctx.h)
+        env.detach()
+        _check(_load().vgpu_env_upload(env.handle(ctx)), ctx.h)
+    incr_ms = (time.perf_counter() - t) * 1e3 / 20
+    st1 = env.upload_stats(ctx)
     del hp
     if rank != 0:
         return
@@ -839,7 +949,7 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     qs = q[:2048].cpu().numpy()
     _, _, _, fl = op.fkcc(oenv, qs, (0, 0, 0), stats=True)
     f_cfg = float(fl.mean())
-    kern_s = wall / a.steps
+    kern_s = kern_ms * 1e-3
     achieved = f_cfg * N / kern_s / 1e12
     cpu = None
     parity = None
@@ -883,7 +993,8 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "parallelism": f"dp{world} (independent shards, no collective)"},
         {"kernel": "fkcc (staged, point-cloud ext path)", "bound": "valu", "achieved": achieved,
          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
-         "algorithmic_flops_per_config": f_cfg, "step_ms": kern_s * 1e3, "l2_hit_rate": l2,
+         "algorithmic_flops_per_config": f_cfg, "kernel_ms": kern_ms, "step_ms_wall": wall / a.steps * 1e3,
+         "l2_hit_rate": l2, "frac_meaning": FRAC_MEANING, "executed": executed_record("capt", N, kern_ms),
          "traffic_source": "profiles/r03_capt_pmc.json (tools/gpu_capt_pmc.sh: rocprofv3 --pmc FETCH_SIZE, "
                            "WRITE_SIZE, TCC_HIT_sum/TCC_MISS_sum in separate passes)",
          "note": "latency-bound gathers, not FLOPs: the cell grid (vgpu_capt_grid.hip) decides most sphere queries "
@@ -899,7 +1010,11 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         "note": "one lane per sphere, CAPT::collides_simd semantics (capt.hh:457-541) through the cell grid; HIP events"}
     line["environment_upload_ms"] = {"ms": upload_ms, "note": "one re-realisation of the environment on the device: "
                                                               "handle create, CAPT arrays from the host twin, blob upload, "
-                                                              "cell-grid build (host wall clock)"}
+                                                              "cell-grid build (host wall clock)",
+                                     "incremental_ms": incr_ms,
+                                     "incremental_grid_builds": st1["grids"] - st0["grids"],
+                                     "incremental_note": "Environment.attach or detach + vgpu_env_upload (tail only, "
+                                                         "in place), mean of 20, host wall clock"}
     print(json.dumps(line))
 
 
@@ -1130,6 +1245,10 @@ def main():
                 "phase_ms": {"head": head_ms, "scan_and_count": scan_ms, "tail": tail_ms},
                 "phase_frac": {"head": achieved / FP32_PEAK_TFLOPS,
                                "tail": f_tail * E / (max(tail_ms, 1e-9) * 1e-3) / 1e12 / FP32_PEAK_TFLOPS},
+                "frac_meaning": FRAC_MEANING,
+                "executed": executed_record({("B", "000", "cage"): "validate", ("A", "000", "cage"): "validate_setA"}
+                                            .get((a.edge_set, a.base, a.scene), "none"), E, kern_ms)
+                            if not strong else None,
             },
             "roofline_hbm_fk": fk_leg,
             "full_mask": full_mask,

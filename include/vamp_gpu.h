@@ -149,8 +149,13 @@ int vgpu_env_attach(vgpu_env *env, const float tf[7], const float *spheres, size
 /* Environment::detach (environment.cc:163) */
 int vgpu_env_detach(vgpu_env *env);
 /* Copy the (sorted) environment to the device.  Called implicitly by the batch functions
- * when the environment changed since the last upload. */
+ * when the environment changed since the last upload.  Incremental: the point clouds (CAPT arrays
+ * and their cell grids) form the blob's prefix and are re-sent -- and their grids rebuilt -- only when
+ * a cloud was added; obstacles, heightfields and the attachment (add_*, attach, detach) form the tail,
+ * rewritten in place (environment.cc:107-163 mutate the reference's environment just as cheaply). */
 int vgpu_env_upload(vgpu_env *env);
+/* out[0] whole-blob uploads, out[1] tail-only uploads, out[2] cell-grid builds of this environment */
+int vgpu_env_upload_stats(const vgpu_env *env, uint64_t out[3]);
 
 /* ---- batched hot path (device pointers, asynchronous) ------------------------------------ */
 /* Robot::sphere_fk for n configurations q[n][dim] -> xyz[3][n_spheres][ld] (SoA, world frame,

@@ -279,16 +279,22 @@ struct vgpu_env {
     bool attached = false;  // Environment::attachments (environment.hh:21)
     std::array<float, 7> att_tf{};
     std::vector<std::array<float, 4>> att_spheres;
-    size_t hf_off = 0, pc_off = 0, att_off = 0;
+    struct Layout {  // section offsets (floats) of one copy of the blob
+        size_t off[OBS_TYPES] = {0, 0, 0, 0, 0};
+        int cnt[OBS_TYPES] = {0, 0, 0, 0, 0};
+        size_t hf_off = 0, pc_off = 0, att_off = 0;
+    };
+    Layout dev_lay, host_lay;  // the device copy carries cell grids the host copy has not: offsets differ
     std::vector<vgpu::CaptGridArgs> pc_grid;  // device copy: each cloud's cell grid (cells_off 0 = none)
-    bool dirty = true;       // device copy stale
+    bool dirty = true;       // device copy stale (obstacles, heightfields, attachment: the blob's tail)
+    bool pc_dirty = true;    // device copy's point clouds stale (the blob's prefix: trees + cell grids)
     bool host_dirty = true;  // host copy (the CPU rake's view, csrc/cpu/) stale
+    size_t tail_off = 0;     // first float of the tail section (device copy)
+    uint64_t n_full = 0, n_tail = 0, n_grids = 0;  // device uploads: whole blob, tail only; grid builds
     std::vector<float> host_blob;
     std::mutex host_mu;
     float* dev = nullptr;
     size_t dev_floats = 0;
-    size_t off[OBS_TYPES] = {0, 0, 0, 0, 0};
-    int cnt[OBS_TYPES] = {0, 0, 0, 0, 0};
 };
 
 #define HIPCHK(ctx, expr)                                                                          \
@@ -639,7 +645,7 @@ extern "C" int vgpu_env_add_pointcloud(vgpu_env* e, const float* points, size_t 
     e->pointclouds.emplace_back();
     vgpu::capt_build(points, n, r_min, r_max, r_point, e->pointclouds.back());
     if (build_ns) *build_ns = e->pointclouds.back().build_ns;
-    e->dirty = e->host_dirty = true;
+    e->dirty = e->pc_dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -660,7 +666,7 @@ extern "C" int vgpu_env_add_pointcloud_device(vgpu_ctx* c, vgpu_env* e, const fl
     HIPCHK(c, vgpu::capt_build_device(points, n, r_min, r_max, r_point, c->cur, t));
     if (build_ns) *build_ns = t.build_ns;
     e->pointclouds.push_back(std::move(t));
-    e->dirty = e->host_dirty = true;
+    e->dirty = e->pc_dirty = e->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -696,7 +702,7 @@ extern "C" int vgpu_env_copy_pointcloud(vgpu_env* dst, const vgpu_env* src, int 
     } else {
         dst->pointclouds.push_back(src->pointclouds[index]);
     }
-    dst->dirty = dst->host_dirty = true;
+    dst->dirty = dst->pc_dirty = dst->host_dirty = true;
     return VGPU_OK;
 }
 
@@ -775,56 +781,19 @@ static bool grid_cells(size_t& cells)
     return !(v && cells == 0);
 }
 
-static int build_blob(vgpu_env* e, std::vector<float>& blob, bool device = false)
+// The blob in two sections.  Prefix: the point clouds (headers, then each cloud's arrays and, in device
+// copies, its cell grid) -- rebuilt only when the set of clouds changes.  Tail (from tail_off): the five
+// obstacle sections, heightfields, the attachment -- small, rewritten in place on add_sphere / attach /
+// detach ... without touching the clouds or relaunching their grid builds (environment.cc:107-163 mutate
+// the reference's environment in place just as cheaply).
+static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& blob, bool device)
 {
-    sort_md(e->spheres);
-    sort_md(e->capsules);
-    sort_md(e->zcapsules);
-    sort_md(e->cuboids);
-    sort_md(e->zcuboids);
     blob.clear();
     if (device) e->pc_grid.clear();
-    auto put = [&](auto& v, int type, int np) {
-        const int S = kObsStride[type];
-        e->off[type] = blob.size();
-        e->cnt[type] = (int)v.size();
-        for (auto& row : v) {
-            const size_t base = blob.size();
-            blob.resize(base + S, 0.0f);
-            blob[base] = row[np];  // min_distance is the last field of the host row
-            for (int i = 0; i < np; ++i) blob[base + 1 + i] = row[i];
-        }
-        for (int k = 0; k < kObsPad; ++k) {
-            const size_t base = blob.size();
-            blob.resize(base + S, 0.0f);
-            blob[base] = __builtin_inff();
-        }
-        while (blob.size() % 16) blob.push_back(0.0f);
-    };
-    put(e->spheres, OBS_SPHERE, 4);
-    put(e->capsules, OBS_CAPSULE, 8);
-    put(e->zcapsules, OBS_ZCAPSULE, 8);
-    put(e->cuboids, OBS_CUBOID, 15);
-    put(e->zcuboids, OBS_ZCUBOID, 15);
-    // heightfields and point clouds: kExtHdr-float headers, then their arrays (16-B aligned)
     auto hdr_u = [](uint32_t u) { return u2f(u); };
     auto align16 = [&]() { while (blob.size() % 4) blob.push_back(0.0f); };
-    e->hf_off = blob.size();
-    blob.resize(blob.size() + (size_t)kExtHdr * e->heightfields.size(), 0.0f);
-    e->pc_off = blob.size();
+    L.pc_off = blob.size();
     blob.resize(blob.size() + (size_t)kExtHdr * e->pointclouds.size(), 0.0f);
-    for (size_t i = 0; i < e->heightfields.size(); ++i) {
-        const auto& h = e->heightfields[i];
-        align16();
-        const size_t data_off = blob.size();
-        blob.insert(blob.end(), h.data.begin(), h.data.end());
-        float* hd = &blob[e->hf_off + kExtHdr * i];
-        const float v[HF_OFF] = {h.x, h.y, h.z, h.xs, h.ys, h.zs, (float)h.xd, (float)h.yd, (float)(h.xd / 2),
-                                 (float)(h.yd / 2)};
-        std::copy(v, v + HF_OFF, hd);
-        hd[HF_OFF] = hdr_u((uint32_t)data_off);
-        hd[HF_CELLS] = hdr_u((uint32_t)(h.xd * h.yd));
-    }
     for (size_t i = 0; i < e->pointclouds.size(); ++i) {
         const auto& t = e->pointclouds[i];
         align16();
@@ -839,7 +808,7 @@ static int build_blob(vgpu_env* e, std::vector<float>& blob, bool device = false
         align16();
         const size_t o_aff = blob.size();
         blob.insert(blob.end(), t.aff.begin(), t.aff.end());
-        float* hd = &blob[e->pc_off + kExtHdr * i];
+        float* hd = &blob[L.pc_off + kExtHdr * i];
         std::copy(t.top, t.top + 6, hd);
         hd[PC_RPOINT] = t.r_point;
         hd[PC_NLOG2] = hdr_u((uint32_t)t.nlog2);
@@ -857,7 +826,7 @@ static int build_blob(vgpu_env* e, std::vector<float>& blob, bool device = false
             g.aff_off = (uint32_t)o_aff;
             g.cells_off = (uint32_t)blob.size();
             blob.resize(blob.size() + 2 * (size_t)g.nx * g.ny * g.nz, 0.0f);
-            hd = &blob[e->pc_off + kExtHdr * i];
+            hd = &blob[L.pc_off + kExtHdr * i];
             const float gv[] = {g.x0, g.y0, g.z0, g.inv_h};
             std::copy(gv, gv + 4, hd + PC_GX);
             hd[PC_GNX] = hdr_u(g.nx);
@@ -871,12 +840,74 @@ static int build_blob(vgpu_env* e, std::vector<float>& blob, bool device = false
         }
         if (device) e->pc_grid.push_back(g);
     }
+    while (blob.size() % 16) blob.push_back(0.0f);
+}
+
+// The tail section as its own vector; its offsets are recorded relative to the blob, starting at base.
+static void build_tail(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& tail, size_t base)
+{
+    sort_md(e->spheres);
+    sort_md(e->capsules);
+    sort_md(e->zcapsules);
+    sort_md(e->cuboids);
+    sort_md(e->zcuboids);
+    tail.clear();
+    auto put = [&](auto& v, int type, int np) {
+        const int S = kObsStride[type];
+        L.off[type] = base + tail.size();
+        L.cnt[type] = (int)v.size();
+        for (auto& row : v) {
+            const size_t at = tail.size();
+            tail.resize(at + S, 0.0f);
+            tail[at] = row[np];  // min_distance is the last field of the host row
+            for (int i = 0; i < np; ++i) tail[at + 1 + i] = row[i];
+        }
+        for (int k = 0; k < kObsPad; ++k) {
+            const size_t at = tail.size();
+            tail.resize(at + S, 0.0f);
+            tail[at] = __builtin_inff();
+        }
+        while (tail.size() % 16) tail.push_back(0.0f);
+    };
+    put(e->spheres, OBS_SPHERE, 4);
+    put(e->capsules, OBS_CAPSULE, 8);
+    put(e->zcapsules, OBS_ZCAPSULE, 8);
+    put(e->cuboids, OBS_CUBOID, 15);
+    put(e->zcuboids, OBS_ZCUBOID, 15);
+    // heightfields: kExtHdr-float headers, then their arrays (16-B aligned)
+    auto hdr_u = [](uint32_t u) { return u2f(u); };
+    auto align16 = [&]() { while (tail.size() % 4) tail.push_back(0.0f); };
+    L.hf_off = base + tail.size();
+    tail.resize(tail.size() + (size_t)kExtHdr * e->heightfields.size(), 0.0f);
+    for (size_t i = 0; i < e->heightfields.size(); ++i) {
+        const auto& h = e->heightfields[i];
+        align16();
+        const size_t data_off = base + tail.size();
+        tail.insert(tail.end(), h.data.begin(), h.data.end());
+        float* hd = &tail[L.hf_off - base + kExtHdr * i];
+        const float v[HF_OFF] = {h.x, h.y, h.z, h.xs, h.ys, h.zs, (float)h.xd, (float)h.yd, (float)(h.xd / 2),
+                                 (float)(h.yd / 2)};
+        std::copy(v, v + HF_OFF, hd);
+        hd[HF_OFF] = hdr_u((uint32_t)data_off);
+        hd[HF_CELLS] = hdr_u((uint32_t)(h.xd * h.yd));
+    }
     // the attachment: frame (7 floats + pad), then its spheres (16-B aligned)
     align16();
-    e->att_off = blob.size();
-    blob.resize(blob.size() + kAttHdr, 0.0f);
-    std::copy(e->att_tf.begin(), e->att_tf.end(), blob.begin() + e->att_off);
-    for (const auto& sp : e->att_spheres) blob.insert(blob.end(), sp.begin(), sp.end());
+    L.att_off = base + tail.size();
+    tail.resize(tail.size() + kAttHdr, 0.0f);
+    std::copy(e->att_tf.begin(), e->att_tf.end(), tail.begin() + (L.att_off - base));
+    for (const auto& sp : e->att_spheres) tail.insert(tail.end(), sp.begin(), sp.end());
+}
+
+static int build_blob(vgpu_env* e, std::vector<float>& blob, bool device = false)
+{
+    vgpu_env::Layout& L = device ? e->dev_lay : e->host_lay;
+    build_prefix(e, L, blob, device);
+    std::vector<float> tail;
+    const size_t base = blob.size();
+    build_tail(e, L, tail, base);
+    blob.insert(blob.end(), tail.begin(), tail.end());
+    if (device) e->tail_off = base;
     if (blob.size() >= ((size_t)1 << 32)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "environment larger than 16 GiB");
     return VGPU_OK;
 }
@@ -886,25 +917,53 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     if (!e) return VGPU_ERR_INVALID_ARG;
     vgpu_ctx* c = e->ctx;
     if (!c) return VGPU_ERR_INVALID_ARG;  // host-only environment
-    if (!e->dirty && e->dev) return VGPU_OK;
-    std::lock_guard<std::mutex> lock(e->host_mu);  // build_blob re-sorts the host rows
+    if (!e->dirty && !e->pc_dirty && e->dev) return VGPU_OK;
+    std::lock_guard<std::mutex> lock(e->host_mu);  // the builds re-sort the host rows
+    HIPCHK(c, hipSetDevice(c->device));
+    if (e->dev && !e->pc_dirty) {  // the tail alone, in place, when it still fits the allocation
+        std::vector<float> tail;
+        build_tail(e, e->dev_lay, tail, e->tail_off);
+        if (e->tail_off + tail.size() <= e->dev_floats) {
+            HIPCHK(c, hipMemcpyAsync(e->dev + e->tail_off, tail.data(), tail.size() * sizeof(float),
+                                     hipMemcpyHostToDevice, c->cur));
+            HIPCHK(c, hipStreamSynchronize(c->cur));  // tail is a host temporary
+            e->dirty = false;
+            ++e->n_tail;
+            return VGPU_OK;
+        }
+    }
     std::vector<float> blob;
     if (int rc = build_blob(e, blob, true)) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    // room for the tail to grow in place (obstacles added later, an attachment)
+    const size_t want = blob.size() + std::max<size_t>(blob.size() - e->tail_off, 4096);
     if (blob.size() > e->dev_floats) {
         if (e->dev) {
             HIPCHK(c, hipStreamSynchronize(c->cur));
             HIPCHK(c, hipFree(e->dev));
             e->dev = nullptr;
+            e->dev_floats = 0;
         }
-        HIPCHK(c, hipMalloc(&e->dev, blob.size() * sizeof(float)));
-        e->dev_floats = blob.size();
+        HIPCHK(c, hipMalloc(&e->dev, want * sizeof(float)));
+        e->dev_floats = want;
     }
     HIPCHK(c, hipMemcpyAsync(e->dev, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice, c->cur));
     for (const auto& g : e->pc_grid)
-        if (g.cells_off) HIPCHK(c, vgpu_launch_capt_grid(e->dev, &g, c->cur));
+        if (g.cells_off) {
+            HIPCHK(c, vgpu_launch_capt_grid(e->dev, &g, c->cur));
+            ++e->n_grids;
+        }
     HIPCHK(c, hipStreamSynchronize(c->cur));  // blob is a host temporary
-    e->dirty = false;
+    e->dirty = e->pc_dirty = false;
+    ++e->n_full;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_env_upload_stats(const vgpu_env* e, uint64_t out[3])
+{
+    if (!e || !out) return VGPU_ERR_INVALID_ARG;
+    out[0] = e->n_full;
+    out[1] = e->n_tail;
+    out[2] = e->n_grids;
     return VGPU_OK;
 }
 
@@ -919,16 +978,17 @@ int vgpu_env_host_view(vgpu_env* e, vgpu::HostEnvView* v)
         e->host_dirty = false;
     }
     const float* b = e->host_blob.data();
+    const vgpu_env::Layout& L = e->host_lay;
     for (int t = 0; t < OBS_TYPES; ++t) {
-        v->obs[t] = b + e->off[t];
-        v->n[t] = e->cnt[t];
+        v->obs[t] = b + L.off[t];
+        v->n[t] = L.cnt[t];
     }
-    v->hf = b + e->hf_off;
-    v->pc = b + e->pc_off;
+    v->hf = b + L.hf_off;
+    v->pc = b + L.pc_off;
     v->base = b;
     v->n_hf = (int)e->heightfields.size();
     v->n_pc = (int)e->pointclouds.size();
-    v->att = b + e->att_off;
+    v->att = b + L.att_off;
     v->n_att = e->attached ? (int)e->att_spheres.size() : 0;
     v->attached = e->attached;
     return VGPU_OK;
@@ -937,23 +997,20 @@ int vgpu_env_host_view(vgpu_env* e, vgpu::HostEnvView* v)
 static EnvView make_view(const vgpu_env* e)
 {
     EnvView v{};
+    const vgpu_env::Layout& L = e->dev_lay;
     for (int t = 0; t < OBS_TYPES; ++t) {
-        v.obs[t] = (const VGPU_CONST float*)(e->dev + e->off[t]);
-        v.n[t] = e->cnt[t];
+        v.obs[t] = (const VGPU_CONST float*)(e->dev + L.off[t]);
+        v.n[t] = L.cnt[t];
     }
     v.lut = e->ctx->lut_dev;
     v.kbits = e->ctx->kbits;
-    v.hf = (const VGPU_CONST float*)(e->dev + e->hf_off);
-    v.pc = (const VGPU_CONST float*)(e->dev + e->pc_off);
+    v.hf = (const VGPU_CONST float*)(e->dev + L.hf_off);
+    v.pc = (const VGPU_CONST float*)(e->dev + L.pc_off);
     v.base = e->dev;
     v.n_hf = (int)e->heightfields.size();
     v.n_pc = (int)e->pointclouds.size();
-    v.att = (const VGPU_CONST float*)(e->dev + e->att_off);
+    v.att = (const VGPU_CONST float*)(e->dev + L.att_off);
     v.n_att = e->attached ? (int)e->att_spheres.size() : 0;
-    // the five obstacle sections are contiguous in the blob (records + sentinels, 16-float aligned)
-    v.obs_floats = (int)(e->off[OBS_ZCUBOID] + (size_t)(e->cnt[OBS_ZCUBOID] + kObsPad) * kObsStride[OBS_ZCUBOID] -
-                         e->off[OBS_SPHERE]);
-    v.obs_lds = 0;
     return v;
 }
 

@@ -209,10 +209,6 @@ struct EnvView {
     // levels of the first point cloud's split tree staged in this workgroup's LDS by
     // capt_stage_lds (0: none -- the host-built view, and kernels that do not stage)
     int pc_lds_levels;
-    // floats of the five obstacle sections (obs[0] .. end of obs[4], contiguous in the blob): what
-    // the VGPU_ENV_LDS variant copies into LDS per workgroup (env_stage_lds); 0 = not staged
-    int obs_floats;
-    int obs_lds;
 };
 constexpr int kAttHdr = 8;
 constexpr int kExtHdr = 32;
@@ -297,22 +293,11 @@ template <int S>
 struct ObsRec {
     float v[S];
 };
-// obstacle records are read through the scalar cache (address space 4, s_load) -- or, in the
-// VGPU_ENV_LDS A/B variant, from a per-workgroup LDS copy (address space 3, ds_read broadcast)
-#define VGPU_LDS_AS __attribute__((address_space(3)))
-template <int AS, class T>
-struct ObsPtr;
-template <class T>
-struct ObsPtr<4, T> {
-    using type = const VGPU_CONST T*;
-};
-template <class T>
-struct ObsPtr<3, T> {
-    using type = const VGPU_LDS_AS T*;
-};
-template <int TYPE, int AS = 4, class TestFn>
-__device__ __forceinline__ uint32_t scan_type(typename ObsPtr<AS, float>::type o, float emax, uint32_t acc,
-                                              TestFn test)
+// obstacle records are read through the scalar cache (address space 4, s_load): every lane of a wave reads
+// the same record, one s_load into SGPRs the tests use directly (a per-workgroup LDS copy measured 7-11 %
+// slower in round 3: a ds_read broadcast per field plus the copy and barrier)
+template <int TYPE, class TestFn>
+__device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float emax, uint32_t acc, TestFn test)
 {
     // The lane state is kept as VALU bit masks (acc: sign bit = hit) instead of per-lane bools:
     // combining divergent bools costs a 64-bit SALU op each, and the scalar unit -- shared by
@@ -320,7 +305,7 @@ __device__ __forceinline__ uint32_t scan_type(typename ObsPtr<AS, float>::type o
     constexpr int S = kObsStride[TYPE];
     constexpr int U = VGPU_SCAN_UNROLL;
     using Rec = ObsRec<S>;  // one record: a single s_load per field group
-    typename ObsPtr<AS, Rec>::type p = (typename ObsPtr<AS, Rec>::type)o;
+    const VGPU_CONST Rec* p = (const VGPU_CONST Rec*)o;
     float md[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) md[u] = p[u].v[0];
@@ -607,42 +592,9 @@ __device__ __forceinline__ uint64_t capt_defer_finish(const VGPU_CONST float* pc
     return defer_hits()[threadIdx.x];
 }
 
-#ifndef VGPU_ENV_LDS_FLOATS
-#define VGPU_ENV_LDS_FLOATS 4096
-#endif
-#ifdef VGPU_ENV_LDS
-__device__ __forceinline__ float* env_lds()
-{
-    __shared__ float e[VGPU_ENV_LDS_FLOATS];  // one per workgroup of every kernel that stages
-    return e;
-}
-#endif
-// VGPU_ENV_LDS variant: every thread of the workgroup copies the obstacle sections into LDS (ends in
-// a barrier; call before any return).  Environments larger than the LDS copy keep the scalar path.
-__device__ __forceinline__ void env_stage_lds(EnvView& env)
-{
-#ifdef VGPU_ENV_LDS
-    env.obs_lds = env.obs_floats > 0 && env.obs_floats <= VGPU_ENV_LDS_FLOATS;
-    if (env.obs_lds) {
-        float* e = env_lds();
-        const VGPU_CONST float* src = env.obs[0];
-        for (int i = threadIdx.x; i < env.obs_floats; i += blockDim.x) e[i] = src[i];
-    }
-    __syncthreads();
-#else
-    (void)env;
-#endif
-}
-
 template <int TYPE, class TestFn>
 __device__ __forceinline__ uint32_t scan_env_type(const EnvView& env, float emax, uint32_t acc, TestFn test)
 {
-#ifdef VGPU_ENV_LDS
-    if (env.obs_lds) {
-        const VGPU_LDS_AS float* base = (const VGPU_LDS_AS float*)env_lds();
-        return scan_type<TYPE, 3>(base + (env.obs[TYPE] - env.obs[0]), emax, acc, test);
-    }
-#endif
     return scan_type<TYPE>(env.obs[TYPE], emax, acc, test);
 }
 

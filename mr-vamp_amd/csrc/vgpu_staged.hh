@@ -253,9 +253,6 @@ __global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void bound_kernel(Src
         capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
         capt_defer_init();
     }
-#ifdef VGPU_ENV_LDS
-    env_stage_lds(env);
-#endif
     const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
     const uint32_t g = (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);
@@ -404,9 +401,6 @@ __global__ __launch_bounds__(kStagedBlock, (ChildWaves<R, K, EXT>::v)) void chil
         capt_stage_lds(env);  // the split tree's top levels into LDS (before any return)
         capt_defer_init();
     }
-#ifdef VGPU_ENV_LDS
-    env_stage_lds(env);
-#endif
     const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
     const uint32_t item = plan->lo[K] + (uint32_t)(tid / Src::G);
     const int lane = (int)(tid % Src::G);

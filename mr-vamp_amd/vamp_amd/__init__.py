@@ -241,36 +241,52 @@ class Environment:
         self._n_clouds = 0  # point clouds in the twin (built once; realised by copying their arrays)
 
     def _changed(self):
+        """Drop every realised copy (the next use re-creates it from the op list)."""
         for dev, h in list(self._handles.items()):
             load().vgpu_env_destroy(h)
         self._handles.clear()
 
+    def _apply_live(self, op):
+        """Apply one op to every realised copy in place: the library re-sends only the section it touches
+        (vgpu_env_upload: obstacles / attachment in the blob's tail; the point clouds and their cell grids
+        stay on the device unless a cloud is added)."""
+        lib = load()
+        for key, h in list(self._handles.items()):
+            self._apply(lib, h, None, op)
+
+    def _push(self, op):
+        self._ops.append(op)
+        self._apply_live(op)
+
     def add_sphere(self, s: Sphere):
-        self._ops.append(("sphere", s))
-        self._changed()
+        self._push(("sphere", s))
 
     def add_cuboid(self, c: Cuboid):
-        self._ops.append(("cuboid", c))
-        self._changed()
+        self._push(("cuboid", c))
 
     def add_capsule(self, c: Cylinder):
-        self._ops.append(("capsule", c))
-        self._changed()
+        self._push(("capsule", c))
 
     def add_heightfield(self, h: HeightField):
-        self._ops.append(("heightfield", h))
-        self._changed()
+        self._push(("heightfield", h))
 
     def attach(self, a: Attachment):
         """Environment.attach (bindings/environment.cc:161-162): validate_motion then checks its
         first rake block through Robot::fkcc_attach (planning/validate.hh:43)."""
-        self._ops = [op for op in self._ops if op[0] != "attach"] + [("attach", (a.tf.copy(), a._rows()))]
-        self._changed()
+        self._ops = [op for op in self._ops if op[0] != "attach"]
+        self._push(("attach", (a.tf.copy(), a._rows())))
 
     def detach(self):
         """Environment.detach (bindings/environment.cc:163)."""
         self._ops = [op for op in self._ops if op[0] != "attach"]
-        self._changed()
+        self._apply_live(("detach", None))
+
+    def upload_stats(self, ctx: Optional["Context"] = None) -> dict:
+        """vgpu_env_upload_stats of the copy on ctx: whole-blob uploads, tail-only uploads, cell-grid builds."""
+        ctx = ctx or context()
+        out = (C.c_uint64 * 3)()
+        check(load().vgpu_env_upload_stats(self.handle(ctx), out), ctx.h)
+        return {"full": int(out[0]), "tail": int(out[1]), "grids": int(out[2])}
 
     @property
     def attached(self) -> bool:
@@ -291,9 +307,8 @@ class Environment:
         ns = C.c_int64()
         check(load().vgpu_env_add_pointcloud(host, pc.points.ctypes.data_as(_lib.F32P), pc.points.shape[0],
                                              pc.r_min, pc.r_max, pc.r_point, C.byref(ns)))
-        self._ops.append(("pointcloud", self._n_clouds))
         self._n_clouds += 1
-        self._changed()
+        self._push(("pointcloud", self._n_clouds - 1))
         return int(ns.value)
 
     def add_pointcloud_device(self, points_ptr: int, n: int, r_min: float, r_max: float, r_point: float,
@@ -307,9 +322,8 @@ class Environment:
         ns = C.c_int64()
         args = (C.c_void_p(int(points_ptr)), int(n), float(r_min), float(r_max), float(r_point))
         check(load().vgpu_env_add_pointcloud_device(ctx.h, host, *args, C.byref(ns)), ctx.h)
-        self._ops.append(("pointcloud", self._n_clouds))
         self._n_clouds += 1
-        self._changed()
+        self._push(("pointcloud", self._n_clouds - 1))
         return int(ns.value)
 
     def pointcloud_arrays(self, index: int = 0) -> dict:
@@ -374,32 +388,38 @@ class Environment:
         return h
 
     def _realise(self, lib, h, ctx_h):
-        for kind, s in self._ops:
-            if kind == "sphere":
-                rc = lib.vgpu_env_add_sphere(h, _f3(s.center), float(np.float32(s.r)))
-            elif kind == "cuboid":
-                if s.axes is not None:
-                    rc = lib.vgpu_env_add_cuboid_axes(h, _f3(s.center), _f3(s.axes[0]), _f3(s.axes[1]),
-                                                      _f3(s.axes[2]), _f3(s.half))
-                else:
-                    rc = lib.vgpu_env_add_cuboid_euler(h, _f3(s.center), _f3(s.euler), _f3(s.half))
-            elif kind == "heightfield":
-                rc = lib.vgpu_env_add_heightfield(h, _f3(s.center), _f3(s.scale), s.xd, s.yd,
-                                                  s.data.ctypes.data_as(_lib.F32P))
-            elif kind == "attach":
-                tf, rows = s
-                rows = np.ascontiguousarray(rows, np.float32)
-                rc = lib.vgpu_env_attach(h, tf.ctypes.data_as(_lib.F32P), rows.ctypes.data_as(_lib.F32P),
-                                         rows.shape[0])
-            elif kind == "pointcloud":  # s = index of the cloud in the host twin
-                rc = lib.vgpu_env_copy_pointcloud(h, self._host, int(s))
+        for op in self._ops:
+            self._apply(lib, h, ctx_h, op)
+
+    def _apply(self, lib, h, ctx_h, op):
+        kind, s = op
+        if kind == "detach":
+            rc = lib.vgpu_env_detach(h)
+        elif kind == "sphere":
+            rc = lib.vgpu_env_add_sphere(h, _f3(s.center), float(np.float32(s.r)))
+        elif kind == "cuboid":
+            if s.axes is not None:
+                rc = lib.vgpu_env_add_cuboid_axes(h, _f3(s.center), _f3(s.axes[0]), _f3(s.axes[1]),
+                                                  _f3(s.axes[2]), _f3(s.half))
             else:
-                if s.center is None:
-                    rc = lib.vgpu_env_add_capsule_endpoints(h, _f3(s.p1), _f3(s.p2), float(np.float32(s.r)))
-                else:
-                    rc = lib.vgpu_env_add_capsule_euler(h, _f3(s.center), _f3(s.euler), float(np.float32(s.r)),
-                                                        float(np.float32(s.length)))
-            check(rc, ctx_h)
+                rc = lib.vgpu_env_add_cuboid_euler(h, _f3(s.center), _f3(s.euler), _f3(s.half))
+        elif kind == "heightfield":
+            rc = lib.vgpu_env_add_heightfield(h, _f3(s.center), _f3(s.scale), s.xd, s.yd,
+                                              s.data.ctypes.data_as(_lib.F32P))
+        elif kind == "attach":
+            tf, rows = s
+            rows = np.ascontiguousarray(rows, np.float32)
+            rc = lib.vgpu_env_attach(h, tf.ctypes.data_as(_lib.F32P), rows.ctypes.data_as(_lib.F32P),
+                                     rows.shape[0])
+        elif kind == "pointcloud":  # s = index of the cloud in the host twin
+            rc = lib.vgpu_env_copy_pointcloud(h, self._host, int(s))
+        else:
+            if s.center is None:
+                rc = lib.vgpu_env_add_capsule_endpoints(h, _f3(s.p1), _f3(s.p2), float(np.float32(s.r)))
+            else:
+                rc = lib.vgpu_env_add_capsule_euler(h, _f3(s.center), _f3(s.euler), float(np.float32(s.r)),
+                                                    float(np.float32(s.length)))
+        check(rc, ctx_h)
 
     def counts(self, ctx: Optional[Context] = None) -> List[int]:
         ctx = ctx or context()

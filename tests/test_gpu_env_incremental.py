@@ -1,0 +1,84 @@
+"""Incremental environment uploads (vgpu_env_upload, SURVEY §8(b) ownership row): after the first
+realisation, add_sphere / attach / detach rewrite only the blob's tail in place -- the point clouds and
+their cell grids stay on the device and capt_grid_kernel is not relaunched (counted by
+vgpu_env_upload_stats) -- and every result equals a freshly realised environment with the same
+obstacles and the oracle (bindings/environment.cc:107-163 mutate the reference's environment in place)."""
+import numpy as np
+import pytest
+
+import scenes
+from test_gpu_attach import both
+
+pytestmark = pytest.mark.gpu
+F = np.float32
+
+
+@pytest.fixture(scope="module")
+def vamp():
+    import vamp_amd
+    assert vamp_amd.context(0) is not None
+    return vamp_amd
+
+
+def fresh(vamp, pts, spheres, att=None):
+    env = vamp.Environment()
+    env.add_pointcloud(pts, scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    for c, r in spheres:
+        env.add_sphere(vamp.Sphere(c, r))
+    if att is not None:
+        env.attach(att)
+    return env
+
+
+def test_attach_detach_add_sphere_do_not_rebuild_clouds(vamp, oracle):
+    pts = scenes.cage_points(4000, seed=3)
+    rng = np.random.default_rng(61)
+    q = oracle.scale(rng.random((8192, 7), dtype=F))
+    robot = vamp.panda_0_0
+    spheres = [((0.5, 0.0, 0.4), 0.15)]
+    env = fresh(vamp, pts, spheres)
+    oenv = oracle.Env().add_pointcloud(pts, scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    oenv.add_sphere((0.5, 0.0, 0.4), F(0.15))
+    got0 = robot.fkcc_batch(q, env)
+    assert np.array_equal(got0, oracle.fkcc_threads(oenv, q))
+    st0 = env.upload_stats()
+    assert st0["full"] == 1 and st0["grids"] == 1
+    a, o = both(vamp, oracle)
+    env.attach(a)
+    got_att = robot.fkcc_attach_batch(q, env)
+    assert np.array_equal(got_att, oracle.robot_fkcc_attach_threads("panda", oenv, o, q, (0, 0, 0)))
+    assert np.array_equal(got_att, robot.fkcc_attach_batch(q, fresh(vamp, pts, spheres, a)))
+    env.detach()
+    assert np.array_equal(robot.fkcc_batch(q, env), got0)
+    spheres.append(((-0.3, 0.3, 0.6), 0.1))
+    env.add_sphere(vamp.Sphere(*spheres[-1]))
+    oenv.add_sphere((-0.3, 0.3, 0.6), F(0.1))
+    got2 = robot.fkcc_batch(q, env)
+    assert np.array_equal(got2, oracle.fkcc_threads(oenv, q))
+    assert np.array_equal(got2, robot.fkcc_batch(q, fresh(vamp, pts, spheres)))
+    st = env.upload_stats()
+    assert st["full"] == 1 and st["grids"] == 1, st  # the cloud and its grid were never re-sent or rebuilt
+    assert st["tail"] >= 3, st
+    # a new point cloud does rebuild (the prefix changed): one more full upload and two grid builds
+    env.add_pointcloud(scenes.cage_points(2000, seed=4), scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    robot.fkcc_batch(q[:64], env)
+    st2 = env.upload_stats()
+    assert st2["full"] == 2 and st2["grids"] == 3, st2
+
+
+def test_many_tail_updates_grow_in_place_or_rebuild(vamp, oracle):
+    """Obstacles added one by one past the tail's headroom: the copy is re-laid out as needed and the
+    results stay equal to the oracle's."""
+    pts = scenes.cage_points(1000, seed=5)
+    env = fresh(vamp, pts, [])
+    oenv = oracle.Env().add_pointcloud(pts, scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    rng = np.random.default_rng(62)
+    q = oracle.scale(rng.random((2048, 7), dtype=F))
+    robot = vamp.panda_0_0
+    for k in range(300):
+        c = (rng.uniform(-1, 1), rng.uniform(-1, 1), rng.uniform(0, 1.2))
+        r = float(rng.uniform(0.01, 0.05))
+        env.add_sphere(vamp.Sphere(c, r))
+        oenv.add_sphere(c, F(r))
+        if k % 50 == 49:
+            assert np.array_equal(robot.fkcc_batch(q, env), oracle.fkcc_threads(oenv, q))

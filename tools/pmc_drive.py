@@ -12,7 +12,8 @@ workload's step, and writes gpurun_out/pmc_inputs/W.meta.json (units per call, c
 tools/pmc_report.py.  Workloads: validate (configs[1] set B, 2^20 edges), validate_setA, capt
 (configs[2], 2^20 configurations), fetch_prm (configs[3] vertex stage, 4M draws: the fused
 sample+fkcc and the compaction), prm_edges (configs[3] edge stage: kNN + gather + validation +
-pair selection + device assembly through vgpu_prm_edges_allgather at world size 1), pair
+pair selection + device assembly through vgpu_prm_edges_allgather at world size 1; prm_edges_full: at
+the 2,681,709 valid vertices of 4M draws), pair
 (configs[4], 2^20 composite edges).
 """
 import argparse
@@ -30,7 +31,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import bench  # noqa: E402
 
 OUT = os.path.join(ROOT, "gpurun_out", "pmc_inputs")
-WORKLOADS = ("validate", "validate_setA", "capt", "fetch_prm", "prm_edges", "pair")
+WORKLOADS = ("validate", "validate_setA", "capt", "fetch_prm", "prm_edges", "prm_edges_full", "pair")
 
 
 def setup(torch, vamp, w, dev, ctx, prep, inp, a):
@@ -87,8 +88,10 @@ def setup(torch, vamp, w, dev, ctx, prep, inp, a):
         env.handle(ctx)
         D = a.draws
         return (lambda: roadmap.sample_valid_shard(torch, vamp.fetch, env, 1, D, ctx, dev), D, "draws", {})
-    if w == "prm_edges":
+    if w in ("prm_edges", "prm_edges_full"):
         from vamp_amd import roadmap
+        if w == "prm_edges_full":
+            a.vertices = 2681709  # the valid vertices of configs[3]'s 4M draws
         env, _ = bench.fetch_scene(vamp)
         if prep:
             draws = int(a.vertices / 0.6) + 4096
