@@ -82,6 +82,13 @@ int vgpu_ctx_set_stream(vgpu_ctx *ctx, void *hip_stream);
 int vgpu_sync(vgpu_ctx *ctx);
 /* the HIP device the context was created on */
 int vgpu_ctx_device(const vgpu_ctx *ctx, int *device);
+/* Debug builds (make -C mr-vamp_amd DEBUG=1 -> vamp_amd/libvampgpu_debug.so): bounds checks on the
+ * data-dependent indices of the staged, CAPT and kNN-index kernels; a failed check is counted (the index
+ * clamped, no fault).  vgpu_debug_build() = 1 in such a build.  vgpu_debug_violations reads and resets the
+ * counters of the context and (optional) of an environment's device copy: out[0] = violations, out[1] =
+ * the first failing site (vgpu_device.hh DBG_*). */
+int vgpu_debug_build(void);
+int vgpu_debug_violations(vgpu_ctx *ctx, vgpu_env *env, uint32_t out[2]);
 /* Per-phase kernel timing of vgpu_validate_motions (HIP events on the context stream; adds
  * one event synchronisation per call while enabled).  vgpu_phase_times returns and resets the
  * accumulated milliseconds: [0] head (first rake block), [1] scan + item count read-back,

@@ -56,12 +56,12 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
     hipError_t vgpu_##NAME##_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \
                                           uint32_t* counts, hipStream_t st);                                         \
-    hipError_t vgpu_##NAME##_staged_plan(const uint32_t* offs, uint32_t nb, uint32_t W, uint64_t set, void* plan,    \
-                                         hipStream_t st);                                                            \
+    hipError_t vgpu_##NAME##_staged_plan(const uint32_t* offs, uint32_t nb, uint32_t W, uint64_t set,                \
+                                         uint32_t n_groups, void* plan, hipStream_t st);                             \
     hipError_t vgpu_##NAME##_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           const void* mask, uint32_t n_groups, uint64_t set, const void* plan,       \
                                           const uint8_t* valid, const uint32_t* offs, uint32_t* items,               \
-                                          hipStream_t st);                                                           \
+                                          const void* dbg, hipStream_t st);                                          \
     hipError_t vgpu_##NAME##_staged_children(int kind, const void* s0, const void* s1, const void* s2,               \
                                              const void* s3, uint64_t first, const void* plan, const uint32_t* ub,   \
                                              const uint32_t* items, const EnvView* env, const float* bases,          \
@@ -243,6 +243,7 @@ struct vgpu_ctx {
     size_t aux_bytes = 0;
     // staged checks (vgpu_staged.hip): bounding masks, per-check counts/cursors, item list
     bool staged = true;
+    bool stats = false;  // print each staged pass's per-check bounding counts (VAMP_AMD_STAGED_STATS)
     std::vector<uint64_t> rounds;  // check sets run in order (staged); empty = chosen per batch
     uint32_t* st_mask = nullptr;
     size_t st_mask_cap = 0;
@@ -263,6 +264,8 @@ struct vgpu_ctx {
     size_t knn_idx_cap = 0;
     // filter_robot_from_pointcloud: the configuration, its sphere_fk<1> centres and the radii
     float* small = nullptr;
+    // debug-check words of the kernels without an environment (kNN index): VGPU_DCHECK, make DEBUG=1
+    uint32_t* dbg = nullptr;
     // optional phase timing
     bool prof = false;
     hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -334,6 +337,7 @@ extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
     c->cur = c->own;
     if (const char* s = std::getenv("VAMP_AMD_STAGED")) c->staged = std::strcmp(s, "0") != 0;
     if (const char* s = std::getenv("VAMP_AMD_KNN")) c->knn_mode = std::atoi(s);
+    if (const char* s = std::getenv("VAMP_AMD_STAGED_STATS")) c->stats = std::strcmp(s, "0") != 0;
     if (const char* s = std::getenv("VAMP_AMD_ROUNDS")) {  // A/B: comma-separated check bit masks
         for (const char* p = s; *p;) {
             char* end = nullptr;
@@ -350,12 +354,42 @@ extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
         return rc;
     }
     if (hipMalloc(&c->lut_dev, c->lut.size() * 4) != hipSuccess ||
-        hipMemcpy(c->lut_dev, c->lut.data(), c->lut.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        hipMemcpy(c->lut_dev, c->lut.data(), c->lut.size() * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMalloc((void**)&c->dbg, 16) != hipSuccess || hipMemset(c->dbg, 0, 16) != hipSuccess) {
+        if (c->lut_dev) (void)hipFree(c->lut_dev);
         (void)hipStreamDestroy(c->own);
         delete c;
         return VGPU_ERR_HIP;
     }
     *out = c;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_debug_build(void)
+{
+#ifdef VGPU_DEBUG
+    return 1;
+#else
+    return 0;
+#endif
+}
+
+// The debug-check words (VGPU_DCHECK, debug builds): the context's (kNN index) and, when env is given, the
+// environment copy's (staged and CAPT kernels).  out[0] = violations, out[1] = first site id; read and reset.
+extern "C" int vgpu_debug_violations(vgpu_ctx* c, vgpu_env* e, uint32_t out[2])
+{
+    if (!c || !out) return VGPU_ERR_INVALID_ARG;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    uint32_t a[2] = {0, 0}, b[2] = {0, 0};
+    HIPCHK(c, hipMemcpy(a, c->dbg, 8, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemset(c->dbg, 0, 8));
+    if (e && e->ctx == c && e->dev) {
+        HIPCHK(c, hipMemcpy(b, e->dev, 8, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemset(e->dev, 0, 8));
+    }
+    out[0] = a[0] + b[0];
+    out[1] = a[1] ? a[1] : b[1];
     return VGPU_OK;
 }
 
@@ -377,6 +411,7 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->knn_part) (void)hipFree(c->knn_part);
     if (c->knn_idx) (void)hipFree(c->knn_idx);
     if (c->small) (void)hipFree(c->small);
+    if (c->dbg) (void)hipFree(c->dbg);
     if (c->total_host) (void)hipHostFree(c->total_host);
     for (auto& ev : c->ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -788,7 +823,7 @@ static bool grid_cells(size_t& cells)
 // the reference's environment in place just as cheaply).
 static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& blob, bool device)
 {
-    blob.clear();
+    blob.assign(kDbgWords, 0.0f);  // the debug-check words (vgpu_device.hh VGPU_DCHECK), zero at every full upload
     if (device) e->pc_grid.clear();
     auto hdr_u = [](uint32_t u) { return u2f(u); };
     auto align16 = [&]() { while (blob.size() % 4) blob.push_back(0.0f); };
@@ -1126,9 +1161,9 @@ struct StagedOps {
                         const float*, int, void*, uint8_t*, hipStream_t);
     hipError_t (*count)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
                         const uint8_t*, uint32_t*, hipStream_t);
-    hipError_t (*plan)(const uint32_t*, uint32_t, uint32_t, uint64_t, void*, hipStream_t);
+    hipError_t (*plan)(const uint32_t*, uint32_t, uint32_t, uint64_t, uint32_t, void*, hipStream_t);
     hipError_t (*queue)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
-                        const void*, const uint8_t*, const uint32_t*, uint32_t*, hipStream_t);
+                        const void*, const uint8_t*, const uint32_t*, uint32_t*, const void*, hipStream_t);
     hipError_t (*children)(int, const void*, const void*, const void*, const void*, uint64_t, const void*,
                            const uint32_t*, const uint32_t*, const EnvView*, const float*, uint8_t*, hipStream_t);
 };
@@ -1216,6 +1251,11 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
     HIPCHK(c, hipStreamSynchronize(c->cur));
     uint32_t fired[64];
     for (int k = 0; k < checks; ++k) fired[k] = c->st_host[k + 1] - c->st_host[k];
+    if (c->stats) {  // VAMP_AMD_STAGED_STATS=1: the pass's bounding statistics (development)
+        std::fprintf(stderr, "staged kind=%d chain=%d groups=%zu fired:", kind, chain, n);
+        for (int k = 0; k < checks; ++k) std::fprintf(stderr, " %u", fired[k]);
+        std::fprintf(stderr, "\n");
+    }
     std::vector<uint64_t> rounds(c->rounds.begin(), c->rounds.end());
     if (rounds.empty()) {
         // Rounds from this batch's bounding statistics: (1) the first three environment checks
@@ -1246,8 +1286,9 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
             HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
         }
         first_round = false;
-        HIPCHK(c, ops.plan(offs, (uint32_t)nb, W, set, plan, c->cur));
-        HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, plan, valid, offs, c->st_items, c->cur));
+        HIPCHK(c, ops.plan(offs, (uint32_t)nb, W, set, (uint32_t)n, plan, c->cur));
+        HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, plan, valid, offs, c->st_items, v->base,
+                            c->cur));
         HIPCHK(c, ops.children(kind, s0, s1, s2, s3, first, plan, ub, c->st_items, v, bases, valid, c->cur));
     }
     return VGPU_OK;
@@ -1923,7 +1964,7 @@ extern "C" int vgpu_prm_neighbor_params(int dim, double space_measure, double ga
 extern "C" size_t vgpu_knn_index_bytes(int dim, uint32_t n, uint32_t q_count);
 extern "C" hipError_t vgpu_launch_knn_index(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
                                             const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr,
-                                            float* dist, uint32_t* cnt, void* pool, size_t pool_bytes,
+                                            float* dist, uint32_t* cnt, void* pool, size_t pool_bytes, uint32_t* dbg,
                                             hipStream_t st);
 
 static bool knn_dim_ok(int dim) { return dim == 6 || dim == 7 || dim == 8 || dim == 14; }
@@ -1959,7 +2000,7 @@ extern "C" int vgpu_roadmap_knn_range(vgpu_ctx* c, int dim, const float* V, size
         if (!bytes) return fail(c, VGPU_ERR_HIP, "roadmap kNN index: scratch size query failed");
         if ((rc = grow(c, &c->knn_idx, &c->knn_idx_cap, (bytes + 3) / 4))) return rc;
         HIPCHK(c, vgpu_launch_knn_index(dim, V, (uint32_t)n, (uint32_t)q_first, (uint32_t)q_count, k, r, kmax, nbr,
-                                        dist, cnt, c->knn_idx, c->knn_idx_cap * 4, c->cur));
+                                        dist, cnt, c->knn_idx, c->knn_idx_cap * 4, c->dbg, c->cur));
         return VGPU_OK;
     }
     uint32_t S = 0;

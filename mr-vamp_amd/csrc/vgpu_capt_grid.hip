@@ -29,10 +29,38 @@ namespace vgpu {
 
 constexpr double kSlack = 1e-3;
 constexpr int kMaxLeaves = 64;
+constexpr int kGridBlock = 256;
+constexpr int kStackDepth = 32;  // a depth-first walk of a tree of depth nlog2 <= 26 holds <= nlog2 + 1 nodes
 
-__global__ __launch_bounds__(256) void capt_grid_kernel(float* __restrict__ base, CaptGridArgs g)
+// the float next to finite f toward -inf / +inf
+__device__ __forceinline__ float next_down(float f)
 {
-    const uint32_t cell = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t b = __float_as_uint(f);
+    if (f == 0.0f) return -__uint_as_float(1u);
+    return __uint_as_float(f > 0.0f ? b - 1u : b + 1u);
+}
+__device__ __forceinline__ float next_up(float f) { return -next_down(-f); }
+__device__ __forceinline__ float round_down(double x)
+{
+    const float f = (float)x;
+    return (double)f > x ? next_down(f) : f;
+}
+__device__ __forceinline__ float round_up(double x)
+{
+    const float f = (float)x;
+    return (double)f < x ? next_up(f) : f;
+}
+
+// One thread per cell.  The walk's stack lives in LDS (a private array indexed by a variable would go to
+// scratch memory), and the affordance loop runs in float over the expanded cell rounded OUTWARD to float
+// (a larger box: lo can only shrink and hi only grow), so its float rounding (< 1e-6 relative on distances
+// of a few metres) only loosens bounds that are then rounded by a further whole unit (h / 256) -- every
+// bound stays conservative.  The descent and the choice of leaves compare the split values with the
+// double cell bounds, as before.
+__global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict__ base, CaptGridArgs g)
+{
+    __shared__ uint32_t stk[kStackDepth][kGridBlock];
+    const uint32_t cell = blockIdx.x * (uint32_t)kGridBlock + threadIdx.x;
     const uint32_t n_cells = g.nx * g.ny * g.nz;
     if (cell >= n_cells) return;
     const uint32_t ix = cell % g.nx, iy = (cell / g.nx) % g.ny, iz = cell / (g.nx * g.ny);
@@ -40,9 +68,12 @@ __global__ __launch_bounds__(256) void capt_grid_kernel(float* __restrict__ base
     const double o[3] = {(double)g.x0, (double)g.y0, (double)g.z0};
     const uint32_t ic[3] = {ix, iy, iz};
     double L[3], U[3];
+    float Lf[3], Uf[3];
     for (int k = 0; k < 3; ++k) {
         L[k] = o[k] + ((double)ic[k] - kSlack) * h;
         U[k] = o[k] + ((double)ic[k] + 1.0 + kSlack) * h;
+        Lf[k] = round_down(L[k]);
+        Uf[k] = round_up(U[k]);
     }
     const float* __restrict__ tests = base + g.tests_off;
     const uint32_t* __restrict__ starts = (const uint32_t*)(base + g.starts_off);
@@ -59,58 +90,62 @@ __global__ __launch_bounds__(256) void capt_grid_kernel(float* __restrict__ base
         else break;
     }
     // the leaves reachable from it, depth first
-    double lo2 = __builtin_inf(), hi2 = 0.0;
+    float lo2 = __builtin_inff(), hi2 = 0.0f;
     int leaves = 0;
-    bool bounded = true;
-    uint32_t stack[64];
+    bool bounded = nlog2 < kStackDepth;
     int sp = 0;
-    stack[sp++] = node;
+    const uint32_t tx = threadIdx.x;
+    stk[sp++][tx] = node;
     const uint32_t first_leaf = (1u << nlog2) - 1u;
     while (sp > 0 && bounded) {
-        const uint32_t n = stack[--sp];
+        const uint32_t n = stk[--sp][tx];
         if (n >= first_leaf) {
             if (++leaves > kMaxLeaves) {
                 bounded = false;
                 break;
             }
             const uint32_t leaf = n - first_leaf;
-            double lmin = __builtin_inf(), hmin = __builtin_inf();
+            float lmin = __builtin_inff(), hmin = __builtin_inff();
             for (uint32_t j = starts[leaf], e = starts[leaf + 1]; j < e; ++j) {
                 const float* v = aff + 24u * j;
+#pragma unroll
                 for (int l = 0; l < 8; ++l) {
-                    const double p[3] = {(double)v[l], (double)v[8 + l], (double)v[16 + l]};
+                    const float p[3] = {v[l], v[8 + l], v[16 + l]};
                     if (!(__builtin_isfinite(p[0]) && __builtin_isfinite(p[1]) && __builtin_isfinite(p[2]))) continue;
-                    double dn = 0.0, df = 0.0;
+                    float dn = 0.0f, df = 0.0f;
+#pragma unroll
                     for (int k = 0; k < 3; ++k) {
-                        const double a = L[k] - p[k], b = p[k] - U[k];
-                        const double near = a > 0.0 ? a : (b > 0.0 ? b : 0.0);
-                        const double far = fmax(fabs(p[k] - L[k]), fabs(p[k] - U[k]));
-                        dn += near * near;
-                        df += far * far;
+                        const float a = Lf[k] - p[k], b = p[k] - Uf[k];
+                        const float near = fmaxf(fmaxf(a, b), 0.0f);
+                        const float far = fmaxf(fabsf(p[k] - Lf[k]), fabsf(p[k] - Uf[k]));
+                        dn = __builtin_fmaf(near, near, dn);
+                        df = __builtin_fmaf(far, far, df);
                     }
-                    lmin = fmin(lmin, dn);
-                    hmin = fmin(hmin, df);
+                    lmin = fminf(lmin, dn);
+                    hmin = fminf(hmin, df);
                 }
             }
-            lo2 = fmin(lo2, lmin);
-            hi2 = fmax(hi2, hmin);  // an empty leaf: +inf, no hit bound
+            lo2 = fminf(lo2, lmin);
+            hi2 = fmaxf(hi2, hmin);  // an empty leaf: +inf, no hit bound
             continue;
         }
         const int lv = 31 - __builtin_clz(n + 1u);
         const float t = tests[n];
         const int ax = lv % 3;
-        if (sp + 2 > 64) {
+        if (sp + 2 > kStackDepth) {
             bounded = false;
             break;
         }
-        if (U[ax] >= (double)t) stack[sp++] = 2u * n + 2u;             // some a >= t
-        if (L[ax] < (double)t || t != t) stack[sp++] = 2u * n + 1u;    // some a < t (or NaN t)
+        if (U[ax] >= (double)t) stk[sp++][tx] = 2u * n + 2u;             // some a >= t
+        if (L[ax] < (double)t || t != t) stk[sp++][tx] = 2u * n + 1u;    // some a < t (or NaN t)
     }
     uint32_t lq = 0u, hq = 0xFFFFu;
     if (bounded) {
+        // float rounding of the squared sums and of sqrt: < 4e-7 relative; taken off lo and added to hi
+        // before the extra whole unit below
         const double u = (double)g.unit;
-        const double lo = sqrt(lo2) / u, hi = sqrt(hi2) / u;
-        // round lo down and hi up by one extra unit: the double sqrt / divide may be an ulp off
+        const double lo = sqrt((double)lo2) * (1.0 - 1e-6) / u, hi = sqrt((double)hi2) * (1.0 + 1e-6) / u;
+        // round lo down and hi up by one extra unit
         lq = lo >= 65535.0 ? 65535u : (uint32_t)fmax(floor(lo) - 1.0, 0.0);
         hq = hi + 1.0 < 65535.0 ? (uint32_t)ceil(hi) + 1u : 0xFFFFu;
     }
@@ -124,6 +159,7 @@ extern "C" hipError_t vgpu_launch_capt_grid(float* base, const vgpu::CaptGridArg
     const uint64_t n = (uint64_t)g->nx * g->ny * g->nz;
     if (n == 0) return hipSuccess;
     if (n >= ((uint64_t)1 << 31)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(vgpu::capt_grid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, base, *g);
+    hipLaunchKernelGGL(vgpu::capt_grid_kernel, dim3((unsigned)((n + vgpu::kGridBlock - 1) / vgpu::kGridBlock)),
+                       dim3(vgpu::kGridBlock), 0, st, base, *g);
     return hipGetLastError();
 }

@@ -23,6 +23,34 @@
 
 #define VGPU_CONST __attribute__((address_space(4)))
 
+// ---- debug bounds checks (make DEBUG=1 -> -DVGPU_DEBUG; SURVEY §5 "race detection / sanitizers") ----
+// Data-dependent indices (staged item lists, CAPT nodes / leaves / affordance ranges / grid cells, kNN
+// tiles and candidates) are checked against their ranges.  A failed check adds 1 to dbg[0] and leaves its
+// site id in dbg[1] (the first one); the kernel goes on with the index clamped, so a violation is counted
+// and reported (vgpu_debug_violations) instead of faulting the GPU.  dbg: the environment blob's first
+// two words (EnvView::base) or the kNN pool's.  Release builds compile the checks out.
+enum : uint32_t {
+    DBG_QUEUE_SLOT = 1, DBG_CHILD_GROUP, DBG_CHILD_ITEM, DBG_CAPT_CELL, DBG_CAPT_NODE, DBG_CAPT_LEAF,
+    DBG_CAPT_AFF, DBG_DEFER_SLOT, DBG_DEFER_CLOUD, DBG_KNN_TILE, DBG_KNN_SUPER, DBG_KNN_VERTEX, DBG_KNN_QUERY
+};
+#ifdef VGPU_DEBUG
+__device__ __forceinline__ uint32_t vgpu_dcheck(const void* dbg, bool ok, uint32_t site, uint32_t v, uint32_t hi)
+{
+    if (!ok && dbg) {
+        uint32_t* w = (uint32_t*)dbg;
+        atomicAdd(w, 1u);
+        atomicCAS(w + 1, 0u, site);
+    }
+    return ok ? v : (hi ? hi - 1u : 0u);
+}
+#define VGPU_DCHECK(dbg, cond, site) (void)vgpu_dcheck((dbg), (cond), (site), 0u, 0u)
+#define VGPU_DCLAMP(dbg, v, hi, site) vgpu_dcheck((dbg), (uint32_t)(v) < (uint32_t)(hi), (site), (uint32_t)(v), (uint32_t)(hi))
+#else
+#define VGPU_DCHECK(dbg, cond, site) ((void)0)
+#define VGPU_DCLAMP(dbg, v, hi, site) (v)
+#endif
+constexpr int kDbgWords = 16;  // floats reserved at the start of an environment blob (debug words + padding)
+
 // ---- group reductions -----------------------------------------------------------------
 // A rake group is G consecutive lanes of a wave64 (G = 8 -> one DPP half-row).  The
 // reductions are VALU DPP shuffles (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror), so the
@@ -415,8 +443,8 @@ __device__ __forceinline__ int capt_decide(const VGPU_CONST float* h, float x, f
         const float fy = (y - h[PC_GY]) * h[PC_GINVH];
         const float fz = (z - h[PC_GZ]) * h[PC_GINVH];
         if (fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < h[PC_GNXF] && fy < h[PC_GNYF] && fz < h[PC_GNZF]) {
-            const uint32_t cell =
-                ((uint32_t)fz * hdr_u(h, PC_GNY) + (uint32_t)fy) * hdr_u(h, PC_GNX) + (uint32_t)fx;
+            uint32_t cell = ((uint32_t)fz * hdr_u(h, PC_GNY) + (uint32_t)fy) * hdr_u(h, PC_GNX) + (uint32_t)fx;
+            cell = VGPU_DCLAMP(base, cell, hdr_u(h, PC_GNX) * hdr_u(h, PC_GNY) * hdr_u(h, PC_GNZ), DBG_CAPT_CELL);
             const uint2 rec = ((const uint2*)(base + goff))[cell];
             const float rr = r + h[PC_RPOINT];
             const float rc = rr * rr;
@@ -440,7 +468,7 @@ __device__ __forceinline__ bool capt_resolve(const VGPU_CONST float* h, const fl
     const float* __restrict__ tests = base + hdr_u(h, PC_TESTS);
     const float rr = r + h[PC_RPOINT];
     const float rc = rr * rr;
-    uint32_t idx = node;
+    uint32_t idx = nlog2 ? VGPU_DCLAMP(base, node, (1u << nlog2) - 1u, DBG_CAPT_NODE) : node;
     int i = 31 - __builtin_clz(idx + 1u);  // the node's level; the axis of level i is i % 3
     const int rot = i % 3;
     float a = rot == 0 ? x : (rot == 1 ? y : z);
@@ -463,7 +491,8 @@ __device__ __forceinline__ bool capt_resolve(const VGPU_CONST float* h, const fl
         b = c;
         c = t;
     }
-    const uint32_t leaf = nlog2 ? idx - ((1u << nlog2) - 1u) : 0u;
+    uint32_t leaf = nlog2 ? idx - ((1u << nlog2) - 1u) : 0u;
+    leaf = VGPU_DCLAMP(base, leaf, 1u << nlog2, DBG_CAPT_LEAF);
     const float* __restrict__ box = base + hdr_u(h, PC_AABBS) + 6u * leaf;
     const float d0 = x - mm_min(mm_max(x, box[0]), box[3]);
     const float d1 = y - mm_min(mm_max(y, box[1]), box[4]);
@@ -471,6 +500,7 @@ __device__ __forceinline__ bool capt_resolve(const VGPU_CONST float* h, const fl
     if (!(__builtin_fmaf(d0, d0, __builtin_fmaf(d2, d2, d1 * d1)) <= rc)) return false;
     const uint32_t* __restrict__ starts = (const uint32_t*)(base + hdr_u(h, PC_STARTS));
     const uint32_t s = starts[leaf], e = starts[leaf + 1];
+    VGPU_DCHECK(base, s <= e && e <= starts[1u << nlog2], DBG_CAPT_AFF);
     const float4* __restrict__ aff = (const float4*)(base + hdr_u(h, PC_AFF));
     for (uint32_t i = s; i < e; ++i) {
         const float4* v = aff + 6u * i;
@@ -568,8 +598,9 @@ __device__ __forceinline__ bool capt_defer_push(bool pend, int tag, int cloud, f
     if (c0 + np > (uint32_t)kDeferCap)
         return pend && capt_resolve(pc + kExtHdr * cloud, base, x, y, z, r, node, cloud == 0 ? lds_levels : 0);
     if (pend) {
-        const uint32_t pos = c0 + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
-                                                                     __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+        uint32_t pos = c0 + (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(pm >> 32),
+                                                               __builtin_amdgcn_mbcnt_lo((uint32_t)pm, 0u));
+        pos = VGPU_DCLAMP(base, pos, (uint32_t)kDeferCap, DBG_DEFER_SLOT);
         DeferQ& q = defer_q()[w];
         q.x[pos] = x;
         q.y[pos] = y;

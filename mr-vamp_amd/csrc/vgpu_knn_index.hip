@@ -403,7 +403,7 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
                                                         uint32_t q_count, const uint32_t* __restrict__ kq,
                                                         const float* __restrict__ rq, uint32_t kmax,
                                                         uint32_t* __restrict__ nbr, float* __restrict__ dist,
-                                                        uint32_t* __restrict__ cnt)
+                                                        uint32_t* __restrict__ cnt, uint32_t* __restrict__ dbg)
 {
     const uint32_t wave = blockIdx.x * (kQBlock / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
@@ -421,9 +421,9 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
     for (int q = 0; q < QG; ++q) {
         const uint32_t qo = g0 + q;
         const bool inq = qo < q_count;
-        const uint32_t p = uni(inq ? (qlist ? qlist[qo] : qo) : 0u);
+        const uint32_t p = uni(VGPU_DCLAMP(dbg, inq ? (qlist ? qlist[qo] : qo) : 0u, n, DBG_KNN_QUERY));
         if (q == 0) p0 = p;
-        qi[q] = uni(inq ? perm[p] : 0xFFFFFFFFu);
+        qi[q] = uni(inq ? VGPU_DCLAMP(dbg, perm[p], n, DBG_KNN_VERTEX) : 0xFFFFFFFFu);
         const bool live = inq && qi[q] >= 2;  // vertices 0, 1 (start, goal) query nothing (prm.hh:228-233)
 #pragma unroll
         for (int d = 0; d < D; ++d) me[q][d] = unf(inq ? Vs[(size_t)p * D + d] : 0.0f);
@@ -446,6 +446,7 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
         uint32_t j;
     };
     auto load = [&](uint32_t t, Cand& cd) {
+        t = VGPU_DCLAMP(dbg, t, T, DBG_KNN_TILE);
         const uint32_t cp = t * kTile + lane;
         const bool ok = cp < n;
 #pragma unroll
@@ -496,6 +497,7 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
     // all needed tiles of super-tile sp except `skip`, the next tile's candidates loaded while the
     // current one is tested
     auto visit_super = [&](uint32_t sp, uint32_t skip) {
+        sp = VGPU_DCLAMP(dbg, sp, S, DBG_KNN_SUPER);
         const uint32_t t = sp * kSuper + lane;
         const bool need = t < T && t != skip && need_box(tbox + (size_t)t * 2 * D, tmin[t]);
         uint64_t m = __builtin_amdgcn_ballot_w64(need);
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
         if (g0 + q >= q_count) break;
-        const size_t o = (size_t)(qi[q] - q_first);
+        const size_t o = VGPU_DCLAMP(dbg, qi[q] - q_first, q_count, DBG_KNN_QUERY);
         if (lane == 0) cnt[o] = c[q];
         if (lane < c[q]) {
             nbr[o * kmax + lane] = bi[q];
@@ -591,7 +593,7 @@ hipError_t layout(uint32_t n, uint32_t q_count, Layout& L)
 template <int D, int K>
 hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, const uint32_t* k, const float* r,
                uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, char* pool, size_t pool_bytes, int group,
-               hipStream_t st)
+               uint32_t* dbg, hipStream_t st)
 {
     Layout L;
     hipError_t e = layout<D>(n, q_count, L);
@@ -651,7 +653,7 @@ hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, c
     const unsigned grid = (unsigned)((waves + kQBlock / 64 - 1) / (kQBlock / 64));
 #define VGPU_KNN_GROUP_LAUNCH(Q)                                                                                      \
     hipLaunchKernelGGL((group_kernel<D, Q>), dim3(grid), dim3(kQBlock), 0, st, Vs, perm, n, T, S, tbox, tmin, sbox, \
-                       smin, ql, q_first, q_count, k, r, kmax, nbr, dist, cnt)
+                       smin, ql, q_first, q_count, k, r, kmax, nbr, dist, cnt, dbg)
     switch (QG) {
     case 1: VGPU_KNN_GROUP_LAUNCH(1); break;
     case 2: VGPU_KNN_GROUP_LAUNCH(2); break;
@@ -665,13 +667,13 @@ hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, c
 template <int D>
 hipError_t run_dim(const float* V, uint32_t n, uint32_t qf, uint32_t qc, const uint32_t* k, const float* r,
                    uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt, char* pool, size_t pb, int g,
-                   hipStream_t st)
+                   uint32_t* dbg, hipStream_t st)
 {
-    if (g > 0) return run<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);  // K unused
-    if (kmax <= 16) return run<D, 16>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);
-    if (kmax <= 32) return run<D, 32>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);
-    if (kmax <= 48) return run<D, 48>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);
-    return run<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, st);
+    if (g > 0) return run<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, dbg, st);  // K unused
+    if (kmax <= 16) return run<D, 16>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, dbg, st);
+    if (kmax <= 32) return run<D, 32>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, dbg, st);
+    if (kmax <= 48) return run<D, 48>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, dbg, st);
+    return run<D, 64>(V, n, qf, qc, k, r, kmax, nbr, dist, cnt, pool, pb, g, dbg, st);
 }
 
 }  // namespace knnidx
@@ -698,7 +700,7 @@ size_t vgpu_knn_index_bytes(int dim, uint32_t n, uint32_t q_count)
 // kmax <= 64, dim in {6, 7, 8, 14}, n >= 1, q_count >= 1 (checked by the caller)
 hipError_t vgpu_launch_knn_index(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
                                  const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr, float* dist,
-                                 uint32_t* cnt, void* pool, size_t pool_bytes, hipStream_t st)
+                                 uint32_t* cnt, void* pool, size_t pool_bytes, uint32_t* dbg, hipStream_t st)
 {
     using namespace vgpu::knnidx;
     char* p = (char*)pool;
@@ -708,10 +710,10 @@ hipError_t vgpu_launch_knn_index(int dim, const float* V, uint32_t n, uint32_t q
         return s ? std::atoi(s) : 4;
     }();
     switch (dim) {
-    case 6: return run_dim<6>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, st);
-    case 7: return run_dim<7>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, st);
-    case 8: return run_dim<8>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, st);
-    case 14: return run_dim<14>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, st);
+    case 6: return run_dim<6>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, dbg, st);
+    case 7: return run_dim<7>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, dbg, st);
+    case 8: return run_dim<8>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, dbg, st);
+    case 14: return run_dim<14>(V, n, q_first, q_count, k, r, kmax, nbr, dist, cnt, p, pool_bytes, g, dbg, st);
     default: return hipErrorInvalidValue;
     }
 }

@@ -46,6 +46,7 @@ struct StagedPlan {
     uint32_t start[kPlanMaxChecks], end[kPlanMaxChecks], fill[kPlanMaxChecks];
     uint32_t lo[kPlanMaxClasses], hi[kPlanMaxClasses];
     uint32_t total;
+    uint32_t n_groups;  // groups of the pass (debug bounds checks)
 };
 
 // Children register classes.  A children kernel's VGPR budget is the maximum over the checks it can
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(kStagedBlock) void count_kernel(Src src, const type
 // class-major.  One lane per check computes its fired count, lane 0 lays them out.
 template <class R>
 __global__ __launch_bounds__(64) void plan_kernel(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t W,
-                                                  uint64_t set, StagedPlan* __restrict__ plan)
+                                                  uint64_t set, uint32_t n_groups, StagedPlan* __restrict__ plan)
 {
     using CC = ChildClasses<R>;
     __shared__ uint32_t fired[R::kChecks];
@@ -333,6 +334,7 @@ __global__ __launch_bounds__(64) void plan_kernel(const uint32_t* __restrict__ o
         plan->hi[cls] = total;
     }
     plan->total = total;
+    plan->n_groups = n_groups;
 }
 
 // Position of group g in check c's segment:
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
                                                              const StagedPlan* __restrict__ plan,
                                                              const uint8_t* __restrict__ valid,
                                                              const uint32_t* __restrict__ offs,
-                                                             uint32_t* __restrict__ items)
+                                                             uint32_t* __restrict__ items, const void* dbg)
 {
     using M = typename R::Mask;
     const uint32_t g = blockIdx.x * kStagedBlock + threadIdx.x;
@@ -367,7 +369,11 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
         const uint64_t b = __builtin_amdgcn_ballot_w64((m >> c) & 1u);
         uint32_t base = plan->start[c] + (offs[(size_t)c * nb + blockIdx.x] - offs[(size_t)c * nb]);
         for (int i = 0; i < w; ++i) base += wcnt[i][c];
-        if ((m >> c) & 1u) items[base + (uint32_t)__builtin_popcountll(b & below)] = g;
+        if ((m >> c) & 1u) {
+            const uint32_t slot = base + (uint32_t)__builtin_popcountll(b & below);
+            VGPU_DCHECK(dbg, slot >= plan->start[c] && slot < plan->fill[c], DBG_QUEUE_SLOT);
+            if (slot < plan->total) items[slot] = g;
+        }
     }
 }
 
@@ -413,7 +419,7 @@ __global__ __launch_bounds__(kStagedBlock, (ChildWaves<R, K, EXT>::v)) void chil
     for (int k = 0; k < R::kChecks; ++k)
         if (ChildClasses<R>::of(k) == K && item0 >= plan->start[k] && item0 < plan->end[k]) fill = plan->fill[k];
     if (item >= fill) return;  // segment padding (group-uniform)
-    const uint32_t g = items[item];
+    const uint32_t g = VGPU_DCLAMP(env.base, items[item], plan->n_groups, DBG_CHILD_GROUP);
     float v[R::D];
     src.load(g, lane, v);
     bool hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bs) > 0;
@@ -460,10 +466,11 @@ struct StagedHost {
 
     template <class Src>
     static hipError_t queue(const Src& src, const M* mask, uint32_t n_groups, M set, const StagedPlan* plan,
-                            const uint8_t* valid, const uint32_t* offs, uint32_t* items, hipStream_t st)
+                            const uint8_t* valid, const uint32_t* offs, uint32_t* items, const void* dbg,
+                            hipStream_t st)
     {
         hipLaunchKernelGGL((queue_kernel<R, Src>), dim3(group_blocks(n_groups)), dim3(kStagedBlock), 0, st, src, mask,
-                           n_groups, set, plan, valid, offs, items);
+                           n_groups, set, plan, valid, offs, items, dbg);
         return hipGetLastError();
     }
 
@@ -497,9 +504,10 @@ struct StagedHost {
         return children_classes<Src, false>(src, plan, ub, items, env, bs, valid, st);
     }
 
-    static hipError_t plan(const uint32_t* offs, uint32_t nb, uint32_t W, M set, StagedPlan* plan, hipStream_t st)
+    static hipError_t plan(const uint32_t* offs, uint32_t nb, uint32_t W, M set, uint32_t n_groups, StagedPlan* plan,
+                           hipStream_t st)
     {
-        hipLaunchKernelGGL((plan_kernel<R>), dim3(1), dim3(64), 0, st, offs, nb, W, (uint64_t)set, plan);
+        hipLaunchKernelGGL((plan_kernel<R>), dim3(1), dim3(64), 0, st, offs, nb, W, (uint64_t)set, n_groups, plan);
         return hipGetLastError();
     }
 
@@ -569,21 +577,21 @@ struct StagedHost {
             return H::count(src, (const typename R::Mask*)mask, n_groups, (typename R::Mask)set, valid, counts, st); \
         });                                                                                                          \
     }                                                                                                                \
-    hipError_t vgpu_##NAME##_staged_plan(const uint32_t* offs, uint32_t nb, uint32_t W, uint64_t set, void* plan,    \
-                                         hipStream_t st)                                                             \
+    hipError_t vgpu_##NAME##_staged_plan(const uint32_t* offs, uint32_t nb, uint32_t W, uint64_t set,                \
+                                         uint32_t n_groups, void* plan, hipStream_t st)                              \
     {                                                                                                                \
-        return vgpu::StagedHost<R>::plan(offs, nb, W, (typename R::Mask)set, (vgpu::StagedPlan*)plan, st);           \
+        return vgpu::StagedHost<R>::plan(offs, nb, W, (typename R::Mask)set, n_groups, (vgpu::StagedPlan*)plan, st); \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           const void* mask, uint32_t n_groups, uint64_t set, const void* plan,       \
                                           const uint8_t* valid, const uint32_t* offs, uint32_t* items,               \
-                                          hipStream_t st)                                                            \
+                                          const void* dbg, hipStream_t st)                                           \
     {                                                                                                                \
         using H = vgpu::StagedHost<R>;                                                                               \
         if (n_groups == 0) return hipSuccess;                                                                        \
         return H::with_source(kind, s0, s1, s2, s3, 0, [&](auto src) {                                              \
             return H::queue(src, (const typename R::Mask*)mask, n_groups, (typename R::Mask)set,                     \
-                            (const vgpu::StagedPlan*)plan, valid, offs, items, st);                                  \
+                            (const vgpu::StagedPlan*)plan, valid, offs, items, dbg, st);                             \
         });                                                                                                          \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_children(int kind, const void* s0, const void* s1, const void* s2,               \

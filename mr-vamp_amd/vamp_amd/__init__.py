@@ -15,6 +15,7 @@ plus the batch entry points the GPU path exists for.  Every call goes through th
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -231,10 +232,14 @@ class Attachment:
         return np.array([list(s.center) + [s.r] for s in self.spheres], np.float32).reshape(-1, 4)
 
 
+_ENVS = weakref.WeakSet()  # live environments (the debug build's bounds-check fixture reads their copies)
+
+
 class Environment:
     """collision::Environment<float> (environment.hh:12-82) realised lazily per Context."""
 
     def __init__(self):
+        _ENVS.add(self)
         self._ops: List[Tuple[str, object]] = []
         self._handles: Dict[int, C.c_void_p] = {}
         self._host: Optional[C.c_void_p] = None  # host-only twin holding the built CAPTs

@@ -71,3 +71,40 @@ def oracle():
     import oracle_py
     oracle_py.build()
     return oracle_py
+
+
+# Debug builds (make -C mr-vamp_amd DEBUG=1, selected with VAMP_AMD_LIB=.../libvampgpu_debug.so): after
+# every GPU test, the bounds-check counters of the default context and of every live environment copy
+# must be zero (vgpu_debug_violations; SURVEY §5 "race detection / sanitizers").
+DEBUG_CHECKED = []
+
+
+@pytest.fixture(autouse=True)
+def _debug_bounds(request):
+    yield
+    if "gpu" not in request.keywords:
+        return
+    import ctypes as C
+    try:
+        from vamp_amd._lib import load
+        lib = load()
+        if not lib.vgpu_debug_build():
+            return
+        import vamp_amd
+    except Exception:
+        return
+    ctx = vamp_amd.context(0)
+    out = (C.c_uint32 * 2)()
+    found = []
+    assert lib.vgpu_debug_violations(ctx.h, None, out) == 0
+    if out[0]:
+        found.append(("context", out[0], out[1]))
+    for env in list(vamp_amd._ENVS):
+        for key, h in list(env._handles.items()):
+            if key != ctx.h.value:  # copies on other (possibly closed) contexts are skipped
+                continue
+            assert lib.vgpu_debug_violations(C.c_void_p(key), h, out) == 0
+            if out[0]:
+                found.append(("environment", out[0], out[1]))
+    DEBUG_CHECKED.append(request.node.nodeid)
+    assert not found, f"debug bounds violations (where, count, first site): {found}"

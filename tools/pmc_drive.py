@@ -3,12 +3,12 @@
 kernel trace or PMC pass over this process holds only that step's dispatches (development tool,
 not the contract bench).
 
-    python tools/pmc_drive.py prep --workload W          # inputs -> gpurun_out/pmc_inputs/W.npz (unprofiled)
+    python tools/pmc_drive.py prep --workload W          # inputs -> $TMPDIR/vamp_pmc_inputs/W.npz (unprofiled)
     rocprofv3 --pmc ... -- python3 tools/pmc_drive.py run --workload W [--calls C]
 
 `run` loads the inputs, builds the environment (its upload kernels -- the CAPT cell grid -- are
 excluded from the summaries by kernel name), runs one warm-up call and C measured calls of the
-workload's step, and writes gpurun_out/pmc_inputs/W.meta.json (units per call, calls) for
+workload's step, and writes $TMPDIR/vamp_pmc_inputs/W.meta.json (units per call, calls) for
 tools/pmc_report.py.  Workloads: validate (configs[1] set B, 2^20 edges), validate_setA, capt
 (configs[2], 2^20 configurations), fetch_prm (configs[3] vertex stage, 4M draws: the fused
 sample+fkcc and the compaction), prm_edges (configs[3] edge stage: kNN + gather + validation +
@@ -30,7 +30,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import bench  # noqa: E402
 
-OUT = os.path.join(ROOT, "gpurun_out", "pmc_inputs")
+OUT = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamp_pmc_inputs")  # large inputs: outside gpurun_out
 WORKLOADS = ("validate", "validate_setA", "capt", "fetch_prm", "prm_edges", "prm_edges_full", "pair")
 
 

@@ -21,5 +21,8 @@ for W in "$@"; do
         python3 tools/pmc_drive.py run --workload $W --calls 2 > $D/pmc_$i.log 2>&1 || { echo "pmc $W pass $i failed"; tail -5 $D/pmc_$i.log; exit 1; }
   done
   python3 tools/pmc_report.py $W $D gpurun_out/prof4/$W.json || exit 1
+  # keep the summaries only (gpurun copies back <= 64 MiB): the kernel stats CSV and the record
+  cp $(find $D/trace -name "*kernel_stats.csv" | head -1) gpurun_out/prof4/${W}_kernel_stats.csv 2>/dev/null
+  rm -rf $D/trace $D/pmc_*/
 done
 echo prof done
