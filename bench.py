@@ -399,7 +399,7 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         "cpu_baseline": cpu,
         "parity": parity,
     }
-    print(json.dumps(line))
+    emit(line)
 
 
 def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
@@ -597,7 +597,7 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         "cpu_baseline": cpu,
         "phases": phases,
     }
-    print(json.dumps(line), flush=True)
+    emit(line)
     if not (index_equals_brute is not False and step_equal):
         print("PARITY FAILURE (kNN index vs brute force, or the C edge stage vs the host assembly)", file=sys.stderr)
         sys.exit(3)
@@ -794,7 +794,7 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     line["counting"] = "rake_early_exit (8 x rake blocks the reference evaluates)"
     line["value_full_mask_count"] = units_full_all * a.steps / wall_max
     line["parity"] = parity
-    print(json.dumps(line))
+    emit(line)
 
 
 def run_rrtc(a, torch, dist, rank, world, dev, stream, ctx, vamp):
@@ -871,7 +871,7 @@ def run_rrtc(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                           "gpu_vs_cpu_rake_mismatches": int((gpu_ok != cpu_ok).sum())},
         "cpu_baseline": None, "cpu_model": cpu_model(),
     }
-    print(json.dumps(line))
+    emit(line)
 
 
 def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
@@ -1015,11 +1015,26 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                                      "incremental_grid_builds": st1["grids"] - st0["grids"],
                                      "incremental_note": "Environment.attach or detach + vgpu_env_upload (tail only, "
                                                          "in place), mean of 20, host wall clock"}
-    print(json.dumps(line))
+    emit(line)
+
+
+_OUT = None  # the process's real stdout (fd 1 is pointed at stderr while the bench runs)
+
+
+def emit(line):
+    """The contract's one JSON line, on the real stdout.  Everything else -- including banners that native
+    libraries printf to fd 1 (RCCL prints its version at communicator creation) -- goes to stderr."""
+    out = _OUT or sys.stdout
+    out.write(json.dumps(line) + "\n")
+    out.flush()
 
 
 def main():
+    global _OUT
     a = parse()
+    sys.stdout.flush()
+    _OUT = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     import torch
     import torch.distributed as dist
 
@@ -1255,7 +1270,7 @@ def main():
             "cpu_baseline": cpu,
             "parity": parity,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
         if parity_failed:
             print(f"PARITY FAILURE ({', '.join(parity_failed)}): {parity}", file=sys.stderr)
             sys.exit(3)

@@ -9,6 +9,11 @@
 #ifndef VGPU_FETCH_STAGED_WAVES_PER_EU
 #define VGPU_FETCH_STAGED_WAVES_PER_EU 6
 #endif
+// bound kernels of the validate head / tail (8-lane groups): at 6 waves/EU they spilled (r04 PMC of the
+// configs[3] edge stage: 0.5 TB of scratch writes per 2.68M-vertex step)
+#ifndef VGPU_FETCH_BOUND8_WAVES
+#define VGPU_FETCH_BOUND8_WAVES 4
+#endif
 // children register classes (ChildClasses, vgpu_staged.hh): VGPRs per check compiled alone
 // (gfx950, Grp8 and Grp1 alike): <= 62 except checks 8, 17, 27, 48, 51, 56, 59 (65-70) and 23 (89);
 // one kernel over all 63 at 6 waves/EU (80 VGPRs) spilled 84-116 B/lane
@@ -29,6 +34,7 @@ struct FetchR {
     static constexpr int kRes = 32;  // robots/fetch.hh:13
     static constexpr int kChecks = fetch_n_checks;
     static constexpr int kWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
+    static constexpr int kBoundWaves8 = VGPU_FETCH_BOUND8_WAVES;
     static constexpr int kChildWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
     using Mask = fetch_mask_t;
     static constexpr Mask kEnvChecks = fetch_env_check_bits;

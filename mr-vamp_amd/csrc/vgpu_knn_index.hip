@@ -392,6 +392,16 @@ __device__ __forceinline__ float box_lb(const float* __restrict__ bx, const floa
 __device__ __forceinline__ float shfl_up1(float v) { return __shfl_up(v, 1, 64); }
 __device__ __forceinline__ uint32_t shfl_up1(uint32_t v) { return (uint32_t)__shfl_up((int)v, 1, 64); }
 
+// XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs (blocks b and b + 8 share one,
+// MI355X_MICROARCH.md "Workgroup dispatch"), so consecutive blocks -- neighbouring Morton-sorted query groups,
+// which visit the same candidate tiles -- would pull the same tiles into 8 different L2s.  Renumbered, the
+// blocks of one XCD take one contiguous run of query groups (a bijection of [0, nb) for any nb).
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
+{
+    const uint32_t x = b & 7u, q = nb >> 3, r = nb & 7u;
+    return x * q + (x < r ? x : r) + (b >> 3);
+}
+
 template <int D, int QG>
 __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict__ Vs, const uint32_t* __restrict__ perm,
                                                         uint32_t n, uint32_t T, uint32_t S,
@@ -405,7 +415,7 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
                                                         uint32_t* __restrict__ nbr, float* __restrict__ dist,
                                                         uint32_t* __restrict__ cnt, uint32_t* __restrict__ dbg)
 {
-    const uint32_t wave = blockIdx.x * (kQBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t wave = xcd_block(blockIdx.x, gridDim.x) * (kQBlock / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t g0 = wave * QG;
     if (g0 >= q_count) return;  // wave-uniform; the kernel has no block barrier

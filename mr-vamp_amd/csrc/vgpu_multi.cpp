@@ -15,11 +15,13 @@
 //     Every rank-local failure (argument, allocation, kernel) still enters exchange 1 with a failure word in
 //     place of its count, so all ranks return the same error and none is left inside an all-gather.
 #include <dlfcn.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -262,6 +264,28 @@ extern "C" int vgpu_comm_unique_id(uint8_t id[128])
     return VGPU_OK;
 }
 
+// RCCL prints its version banner on stdout when a communicator is created; the caller's stdout (bench.py's
+// one JSON line, a planner's output) stays clean: the banner goes to stderr
+namespace {
+struct StdoutToStderr {
+    int saved = -1;
+    StdoutToStderr()
+    {
+        std::fflush(stdout);
+        saved = dup(1);
+        if (saved >= 0) dup2(2, 1);
+    }
+    ~StdoutToStderr()
+    {
+        std::fflush(stdout);
+        if (saved >= 0) {
+            dup2(saved, 1);
+            close(saved);
+        }
+    }
+};
+}  // namespace
+
 extern "C" int vgpu_comm_init(vgpu_ctx* ctx, int rank, int world, const uint8_t id[128], vgpu_comm** out)
 {
     if (!ctx || !id || !out || world < 1 || rank < 0 || rank >= world) return VGPU_ERR_INVALID_ARG;
@@ -278,7 +302,12 @@ extern "C" int vgpu_comm_init(vgpu_ctx* ctx, int rank, int world, const uint8_t 
     }
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
-    if (R.init(&c->comm, world, u, rank) != ncclSuccess) {
+    ncclResult_t ir;
+    {
+        StdoutToStderr quiet;
+        ir = R.init(&c->comm, world, u, rank);
+    }
+    if (ir != ncclSuccess) {
         (void)hipStreamDestroy(c->st);
         delete c;
         return VGPU_ERR_HIP;

@@ -17,6 +17,11 @@
 #ifndef VGPU_PAIR_BOUND_WAVES
 #define VGPU_PAIR_BOUND_WAVES 5
 #endif
+// the inter-arm passes' bound kernels over 8-lane rake groups (validate head / tail): both arms' link
+// frames are live at once -- 176 B/lane of scratch at 5 waves/EU, none at 3 (132 VGPRs)
+#ifndef VGPU_PAIR_INTER_BOUND8_WAVES
+#define VGPU_PAIR_INTER_BOUND8_WAVES 3
+#endif
 #ifndef VGPU_PAIR_INTER_WAVES
 #define VGPU_PAIR_INTER_WAVES 6
 #endif
@@ -88,6 +93,7 @@ struct PairInterR : PairRakeR {
     static constexpr int kChecks = (panda_pair_n_checks - kFirst) < panda_pair_chunk ? (panda_pair_n_checks - kFirst)
                                                                                       : panda_pair_chunk;
     static constexpr int kWavesPerEU = VGPU_PAIR_BOUND_WAVES;
+    static constexpr int kBoundWaves8 = VGPU_PAIR_INTER_BOUND8_WAVES;
     static constexpr int kChildWavesPerEU = VGPU_PAIR_INTER_WAVES;
     using Mask = uint64_t;
     static constexpr Mask kEnvChecks = 0u;

@@ -242,9 +242,22 @@ __device__ __forceinline__ void block_counts(typename R::Mask m, uint32_t* __res
     for (int i = threadIdx.x; i < R::kChecks; i += kStagedBlock) counts[(size_t)i * gridDim.x + blockIdx.x] = cnt[i];
 }
 
+// waves/EU of a bound kernel: R::kWavesPerEU, or R::kBoundWaves8 for the 8-lane rake sources (validate head
+// and tail) when the robot sets it -- their rake loaders and group reductions add live registers, which
+// at the sampler's occupancy spilled hundreds of bytes per lane (Fetch, the composite's inter-arm passes:
+// r04 PMC, GB of scratch writes per call)
+template <class R, class Src, class = void>
+struct BoundWaves {
+    static constexpr int v = R::kWavesPerEU;
+};
+template <class R, class Src>
+struct BoundWaves<R, Src, std::void_t<decltype(R::kBoundWaves8)>> {
+    static constexpr int v = Src::G > 1 ? R::kBoundWaves8 : R::kWavesPerEU;
+};
+
 // ---- stage 1: bounding masks ---------------------------------------------------------------
 template <class R, class Src, bool EXT>
-__global__ __launch_bounds__(kStagedBlock, R::kWavesPerEU) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
+__global__ __launch_bounds__(kStagedBlock, (BoundWaves<R, Src>::v)) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
                                                                              Bases bs, int chain,
                                                                              typename R::Mask* __restrict__ mask,
                                                                              uint8_t* __restrict__ valid)
