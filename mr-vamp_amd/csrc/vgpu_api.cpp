@@ -821,29 +821,37 @@ static bool grid_cells(size_t& cells)
 // obstacle sections, heightfields, the attachment -- small, rewritten in place on add_sphere / attach /
 // detach ... without touching the clouds or relaunching their grid builds (environment.cc:107-163 mutate
 // the reference's environment in place just as cheaply).
-static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& blob, bool device)
+// The cell grids are written by the device (vgpu_launch_capt_grid), so they are holes in the host copy of the
+// prefix: `holes` receives (host position, device floats skipped) per grid, and every offset the prefix records
+// is a device position (host position + the holes before it).  An upload then sends the host runs between
+// the holes -- no zero-filled grid crosses PCIe (16 MB for the 10k-point cloud's 2M cells).
+static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& blob, bool device,
+                         std::vector<std::pair<size_t, size_t>>* holes = nullptr)
 {
     blob.assign(kDbgWords, 0.0f);  // the debug-check words (vgpu_device.hh VGPU_DCHECK), zero at every full upload
     if (device) e->pc_grid.clear();
+    if (holes) holes->clear();
+    size_t shift = 0;  // device floats of the holes so far (multiples of 16: host and device alignment agree)
+    auto dpos = [&]() { return blob.size() + shift; };
     auto hdr_u = [](uint32_t u) { return u2f(u); };
     auto align16 = [&]() { while (blob.size() % 4) blob.push_back(0.0f); };
-    L.pc_off = blob.size();
+    L.pc_off = dpos();
     blob.resize(blob.size() + (size_t)kExtHdr * e->pointclouds.size(), 0.0f);
     for (size_t i = 0; i < e->pointclouds.size(); ++i) {
         const auto& t = e->pointclouds[i];
         align16();
-        const size_t o_tests = blob.size();
+        const size_t o_tests = dpos();
         blob.insert(blob.end(), t.tests.begin(), t.tests.end());
         align16();
-        const size_t o_aabbs = blob.size();
+        const size_t o_aabbs = dpos();
         blob.insert(blob.end(), t.aabbs.begin(), t.aabbs.end());
         align16();
-        const size_t o_starts = blob.size();
+        const size_t o_starts = dpos();
         for (uint32_t v : t.aff_starts) blob.push_back(u2f(v));
         align16();
-        const size_t o_aff = blob.size();
+        const size_t o_aff = dpos();
         blob.insert(blob.end(), t.aff.begin(), t.aff.end());
-        float* hd = &blob[L.pc_off + kExtHdr * i];
+        float* hd = &blob[L.pc_off + kExtHdr * i];  // headers precede every hole: host == device position
         std::copy(t.top, t.top + 6, hd);
         hd[PC_RPOINT] = t.r_point;
         hd[PC_NLOG2] = hdr_u((uint32_t)t.nlog2);
@@ -851,17 +859,18 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
         hd[PC_AABBS] = hdr_u((uint32_t)o_aabbs);
         hd[PC_STARTS] = hdr_u((uint32_t)o_starts);
         hd[PC_AFF] = hdr_u((uint32_t)o_aff);
-        // device copies: room for the cell grid, filled by vgpu_launch_capt_grid after the upload
+        // device copies: the cell grid, a hole filled by vgpu_launch_capt_grid after the upload
         vgpu::CaptGridArgs g{};
         size_t cells = 0;
         if (device && grid_cells(cells) && vgpu::capt_grid_plan(t, cells, g)) {
-            align16();
+            while (blob.size() % 16) blob.push_back(0.0f);
             g.tests_off = (uint32_t)o_tests;
             g.starts_off = (uint32_t)o_starts;
             g.aff_off = (uint32_t)o_aff;
-            g.cells_off = (uint32_t)blob.size();
-            blob.resize(blob.size() + 2 * (size_t)g.nx * g.ny * g.nz, 0.0f);
-            hd = &blob[L.pc_off + kExtHdr * i];
+            g.cells_off = (uint32_t)dpos();
+            const size_t hole = (2 * (size_t)g.nx * g.ny * g.nz + 15) & ~(size_t)15;
+            if (holes) holes->push_back({blob.size(), hole});
+            shift += hole;
             const float gv[] = {g.x0, g.y0, g.z0, g.inv_h};
             std::copy(gv, gv + 4, hd + PC_GX);
             hd[PC_GNX] = hdr_u(g.nx);
@@ -934,16 +943,24 @@ static void build_tail(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& tai
     for (const auto& sp : e->att_spheres) tail.insert(tail.end(), sp.begin(), sp.end());
 }
 
-static int build_blob(vgpu_env* e, std::vector<float>& blob, bool device = false)
+// host: the whole blob; device (holes != NULL): the blob minus the grid holes, *dev_floats = its device size
+static int build_blob(vgpu_env* e, std::vector<float>& blob, std::vector<std::pair<size_t, size_t>>* holes = nullptr,
+                      size_t* dev_floats = nullptr)
 {
+    const bool device = holes != nullptr;
     vgpu_env::Layout& L = device ? e->dev_lay : e->host_lay;
-    build_prefix(e, L, blob, device);
+    build_prefix(e, L, blob, device, holes);
+    size_t shift = 0;
+    if (holes)
+        for (const auto& h : *holes) shift += h.second;
     std::vector<float> tail;
-    const size_t base = blob.size();
+    const size_t base = blob.size() + shift;  // device position of the tail
     build_tail(e, L, tail, base);
     blob.insert(blob.end(), tail.begin(), tail.end());
     if (device) e->tail_off = base;
-    if (blob.size() >= ((size_t)1 << 32)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "environment larger than 16 GiB");
+    if (dev_floats) *dev_floats = blob.size() + shift;
+    if (blob.size() + shift >= ((size_t)1 << 32))
+        return fail(e->ctx, VGPU_ERR_INVALID_ARG, "environment larger than 16 GiB");
     return VGPU_OK;
 }
 
@@ -968,10 +985,12 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
         }
     }
     std::vector<float> blob;
-    if (int rc = build_blob(e, blob, true)) return rc;
+    std::vector<std::pair<size_t, size_t>> holes;
+    size_t total = 0;
+    if (int rc = build_blob(e, blob, &holes, &total)) return rc;
     // room for the tail to grow in place (obstacles added later, an attachment)
-    const size_t want = blob.size() + std::max<size_t>(blob.size() - e->tail_off, 4096);
-    if (blob.size() > e->dev_floats) {
+    const size_t want = total + std::max<size_t>(total - e->tail_off, 4096);
+    if (total > e->dev_floats) {
         if (e->dev) {
             HIPCHK(c, hipStreamSynchronize(c->cur));
             HIPCHK(c, hipFree(e->dev));
@@ -981,7 +1000,17 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
         HIPCHK(c, hipMalloc(&e->dev, want * sizeof(float)));
         e->dev_floats = want;
     }
-    HIPCHK(c, hipMemcpyAsync(e->dev, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice, c->cur));
+    // the host runs between the grid holes
+    size_t hpos = 0, dpos = 0;
+    for (size_t k = 0; k <= holes.size(); ++k) {
+        const size_t hend = k < holes.size() ? holes[k].first : blob.size();
+        if (hend > hpos)
+            HIPCHK(c, hipMemcpyAsync(e->dev + dpos, blob.data() + hpos, (hend - hpos) * sizeof(float),
+                                     hipMemcpyHostToDevice, c->cur));
+        dpos += hend - hpos;
+        hpos = hend;
+        if (k < holes.size()) dpos += holes[k].second;
+    }
     for (const auto& g : e->pc_grid)
         if (g.cells_off) {
             HIPCHK(c, vgpu_launch_capt_grid(e->dev, &g, c->cur));
@@ -1166,21 +1195,26 @@ struct StagedOps {
                         const void*, const uint8_t*, const uint32_t*, uint32_t*, const void*, hipStream_t);
     hipError_t (*children)(int, const void*, const void*, const void*, const void*, uint64_t, const void*,
                            const uint32_t*, const uint32_t*, const EnvView*, const float*, uint8_t*, hipStream_t);
+    // source kinds (bit k = kind k) run as ONE round of every check: there the rounds' bookkeeping costs
+    // more than their early exit saves (A/B on MI355X, profiles/r04e_ab.log, r04f_rounds_ab.log: the Fetch
+    // sampler 1.09 -> 1.02 ms per 4M draws, the composite 10.69-10.73 -> 10.53-10.55 ms per 2^20 edges;
+    // the Panda keeps its rounds: set B 2.53 vs 2.85 ms, set A 1.61 vs 2.95, CAPT 0.52 vs 0.64)
+    unsigned one_round_kinds;
 };
-#define VGPU_STAGED_OPS(NAME)                                                                                        \
+#define VGPU_STAGED_OPS(NAME, ONE_ROUND)                                                                             \
     StagedOps                                                                                                        \
     {                                                                                                                \
         vgpu_##NAME##_staged_checks, vgpu_##NAME##_staged_env_checks, vgpu_##NAME##_staged_mask_bytes,               \
             vgpu_##NAME##_staged_class, vgpu_##NAME##_staged_plan_bytes, vgpu_##NAME##_staged_blocks,                \
             vgpu_##NAME##_staged_bound, vgpu_##NAME##_staged_count, vgpu_##NAME##_staged_plan,                       \
-            vgpu_##NAME##_staged_queue, vgpu_##NAME##_staged_children                                                \
+            vgpu_##NAME##_staged_queue, vgpu_##NAME##_staged_children, ONE_ROUND                                     \
     }
-static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda);
-static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch);
-static const StagedOps kUr5Staged = VGPU_STAGED_OPS(ur5);
+static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda, 0u);
+static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch, 1u << 1);  // the sampler
+static const StagedOps kUr5Staged = VGPU_STAGED_OPS(ur5, 0u);
 // the two-Panda composite: four chained passes (vgpu_pair_staged.hip) -- arm A, arm B, inter-arm chunks
-static const StagedOps kPairStaged[4] = {VGPU_STAGED_OPS(pair_a), VGPU_STAGED_OPS(pair_b), VGPU_STAGED_OPS(pair_i0),
-                                         VGPU_STAGED_OPS(pair_i1)};
+static const StagedOps kPairStaged[4] = {VGPU_STAGED_OPS(pair_a, 0x1Fu), VGPU_STAGED_OPS(pair_b, 0x1Fu),
+                                         VGPU_STAGED_OPS(pair_i0, 0x1Fu), VGPU_STAGED_OPS(pair_i1, 0x1Fu)};
 
 // robots built from vgpu_robot.hh (one TU each): their launch table, or NULL
 static const RobotOps* generic_ops(int32_t kind)
@@ -1192,10 +1226,10 @@ static const RobotOps* generic_ops(int32_t kind)
     }
 }
 // the Baxter: its 388 checks in 7 chained chunks of <= 64 (vgpu_baxter_staged.hip)
-static const StagedOps kBaxterStaged[7] = {VGPU_STAGED_OPS(baxter_c0), VGPU_STAGED_OPS(baxter_c1),
-                                           VGPU_STAGED_OPS(baxter_c2), VGPU_STAGED_OPS(baxter_c3),
-                                           VGPU_STAGED_OPS(baxter_c4), VGPU_STAGED_OPS(baxter_c5),
-                                           VGPU_STAGED_OPS(baxter_c6)};
+static const StagedOps kBaxterStaged[7] = {VGPU_STAGED_OPS(baxter_c0, 0u), VGPU_STAGED_OPS(baxter_c1, 0u),
+                                           VGPU_STAGED_OPS(baxter_c2, 0u), VGPU_STAGED_OPS(baxter_c3, 0u),
+                                           VGPU_STAGED_OPS(baxter_c4, 0u), VGPU_STAGED_OPS(baxter_c5, 0u),
+                                           VGPU_STAGED_OPS(baxter_c6, 0u)};
 // A robot's staged pipeline: one pass, or several chained passes over the same groups (check lists
 // beyond one 64-bit mask, the composite's arms and inter-arm checks)
 struct StagedChain {
@@ -1257,6 +1291,7 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
         std::fprintf(stderr, "\n");
     }
     std::vector<uint64_t> rounds(c->rounds.begin(), c->rounds.end());
+    if (rounds.empty() && ((ops.one_round_kinds >> kind) & 1u)) rounds = {all};
     if (rounds.empty()) {
         // Rounds from this batch's bounding statistics: (1) the first three environment checks
         // that fire at all (the links that leave the base region -- they invalidate most groups

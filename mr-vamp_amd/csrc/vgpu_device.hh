@@ -468,7 +468,8 @@ __device__ __forceinline__ bool capt_resolve(const VGPU_CONST float* h, const fl
     const float* __restrict__ tests = base + hdr_u(h, PC_TESTS);
     const float rr = r + h[PC_RPOINT];
     const float rc = rr * rr;
-    uint32_t idx = nlog2 ? VGPU_DCLAMP(base, node, (1u << nlog2) - 1u, DBG_CAPT_NODE) : node;
+    // node: a split node or, when the whole grid cell lies in one leaf's region, that leaf
+    uint32_t idx = VGPU_DCLAMP(base, node, (2u << nlog2) - 1u, DBG_CAPT_NODE);
     int i = 31 - __builtin_clz(idx + 1u);  // the node's level; the axis of level i is i % 3
     const int rot = i % 3;
     float a = rot == 0 ? x : (rot == 1 ? y : z);

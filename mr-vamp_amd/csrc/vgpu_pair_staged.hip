@@ -18,9 +18,11 @@
 #define VGPU_PAIR_BOUND_WAVES 5
 #endif
 // the inter-arm passes' bound kernels over 8-lane rake groups (validate head / tail): both arms' link
-// frames are live at once -- 176 B/lane of scratch at 5 waves/EU, none at 3 (132 VGPRs)
+// frames are live at once -- 176 B/lane of scratch at 5 waves/EU, 12 B at 4 (128 VGPRs), none at 3
+// (132); A/B on MI355X (2^20 composite edges, 2 x 2 alternating): 4 waves 10.58-10.68 ms, 3 waves
+// 10.72-10.77 (profiles/r04d_pair_ab.log)
 #ifndef VGPU_PAIR_INTER_BOUND8_WAVES
-#define VGPU_PAIR_INTER_BOUND8_WAVES 3
+#define VGPU_PAIR_INTER_BOUND8_WAVES 4
 #endif
 #ifndef VGPU_PAIR_INTER_WAVES
 #define VGPU_PAIR_INTER_WAVES 6
