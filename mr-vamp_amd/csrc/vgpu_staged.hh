@@ -391,6 +391,15 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
 }
 
 // ---- stage 2: children, one check per wave ------------------------------------------------------
+#ifdef VGPU_HITSTATS
+__device__ unsigned int vgpu_hitstats[5][64][2];
+template <class Src> struct SrcKindOf;
+template <class R> struct SrcKindOf<SrcConfigsT<R>> { static constexpr int v = 0; };
+template <class R> struct SrcKindOf<SrcSamplesT<R>> { static constexpr int v = 1; };
+template <class R> struct SrcKindOf<SrcHeadT<R>> { static constexpr int v = 2; };
+template <class R> struct SrcKindOf<SrcTailT<R>> { static constexpr int v = 3; };
+template <class R> struct SrcKindOf<SrcTailMaskT<R>> { static constexpr int v = 4; };
+#endif
 // A class's kernel covers the class's item range [lo, hi) of the plan; its grid is sized by the
 // host from an upper bound (the first round's counts), so waves past hi exit at once.  The check of
 // a wave is found by scanning the class's checks (compile-time list, scalar compares against the
@@ -438,6 +447,18 @@ __global__ __launch_bounds__(kStagedBlock, (ChildWaves<R, K, EXT>::v)) void chil
     bool hit = children_of_class<R, K, Grp, EXT>(item0, plan, v, env, bs) > 0;
     if constexpr (EXT) hit = Grp::any(capt_defer_finish(env.pc, env.base, env.pc_lds_levels) != 0ull) || hit;
     if (hit && lane == 0) valid[src.out(g)] = 0;  // every writer stores 0: the race is benign
+#ifdef VGPU_HITSTATS
+    // development statistics (variant builds only): items run and items whose children hit, per
+    // (source kind, check) -- how much of the children work verifies a bounding hit that is no collision
+    if (lane == 0) {
+        int chk = 0;
+#pragma unroll
+        for (int k = 0; k < R::kChecks; ++k)
+            if (item0 >= plan->start[k] && item0 < plan->end[k]) chk = k;
+        atomicAdd(&vgpu_hitstats[SrcKindOf<Src>::v][chk][0], 1u);
+        if (hit) atomicAdd(&vgpu_hitstats[SrcKindOf<Src>::v][chk][1], 1u);
+    }
+#endif
 }
 
 // ---- host-side launch helpers ------------------------------------------------------------------

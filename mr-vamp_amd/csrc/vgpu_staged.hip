@@ -118,3 +118,17 @@ extern "C" hipError_t vgpu_launch_tail_counts(const float* starts, const float* 
                        n_blocks, cnt);
     return hipGetLastError();
 }
+
+#ifdef VGPU_HITSTATS
+// development statistics of the VGPU_HITSTATS variant: out[5][64][2] (items, items with a children hit)
+// per (source kind, check) since the last call; reset = 1 zeroes them
+extern "C" int vgpu_panda_hitstats(unsigned int* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vgpu::vgpu_hitstats), sizeof(vgpu::vgpu_hitstats)) != hipSuccess) return -2;
+    if (reset) {
+        static const unsigned int zero[5][64][2] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vgpu::vgpu_hitstats), zero, sizeof(zero)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
