@@ -163,6 +163,8 @@ int vgpu_env_detach(vgpu_env *env);
 int vgpu_env_upload(vgpu_env *env);
 /* out[0] whole-blob uploads, out[1] tail-only uploads, out[2] cell-grid builds of this environment */
 int vgpu_env_upload_stats(const vgpu_env *env, uint64_t out[3]);
+/* point cloud `index`'s cell grid as the uploaded device header records it: {nx, ny, nz, cells_off} */
+int vgpu_env_pointcloud_grid(vgpu_env *env, int index, uint32_t out[4]);
 
 /* ---- batched hot path (device pointers, asynchronous) ------------------------------------ */
 /* Robot::sphere_fk for n configurations q[n][dim] -> xyz[3][n_spheres][ld] (SoA, world frame,

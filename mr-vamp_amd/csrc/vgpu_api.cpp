@@ -864,6 +864,7 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
         size_t cells = 0;
         if (device && grid_cells(cells) && vgpu::capt_grid_plan(t, cells, g)) {
             while (blob.size() % 16) blob.push_back(0.0f);
+            hd = &blob[L.pc_off + kExtHdr * i];  // the push_backs may have moved the blob
             g.tests_off = (uint32_t)o_tests;
             g.starts_off = (uint32_t)o_starts;
             g.aff_off = (uint32_t)o_aff;
@@ -1019,6 +1020,22 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     HIPCHK(c, hipStreamSynchronize(c->cur));  // blob is a host temporary
     e->dirty = e->pc_dirty = false;
     ++e->n_full;
+    return VGPU_OK;
+}
+
+// The cell grid of point cloud `index` as its DEVICE header records it: out = {nx, ny, nz, cells_off} (all 0:
+// no grid).  Reads the uploaded header back, so a layout slip that drops the grid shows up in a test.
+extern "C" int vgpu_env_pointcloud_grid(vgpu_env* e, int index, uint32_t out[4])
+{
+    if (!e || !out || !e->ctx || index < 0 || (size_t)index >= e->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
+    if (int rc = vgpu_env_upload(e)) return rc;
+    vgpu_ctx* c = e->ctx;
+    float hd[kExtHdr];
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->cur));
+    HIPCHK(c, hipMemcpy(hd, e->dev + e->dev_lay.pc_off + (size_t)kExtHdr * index, sizeof(hd), hipMemcpyDeviceToHost));
+    const int f[4] = {PC_GNX, PC_GNY, PC_GNZ, PC_GCELLS};
+    for (int k = 0; k < 4; ++k) std::memcpy(&out[k], &hd[f[k]], 4);
     return VGPU_OK;
 }
 

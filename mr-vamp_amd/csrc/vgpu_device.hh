@@ -630,6 +630,64 @@ __device__ __forceinline__ uint32_t scan_env_type(const EnvView& env, float emax
     return scan_type<TYPE>(env.obs[TYPE], emax, acc, test);
 }
 
+// Conservative environment test of a mid-level sphere (tools/gen_kernels.py --mids): sign bit set when the
+// sphere may touch an obstacle.  Its cull extent, (sqrt(|c|^2) + r) * 1.001, bounds from above the
+// approximate extent the reference culls a contained child sphere with (|c_child| + r_child <= |c| + r - 1e-4,
+// and v * rsqrt_host(v) is within 2^-11 relative of sqrt v), so no obstacle a child could be tested against
+// is culled here; the predicates are the reference's, on a sphere that contains the child with a 0.1 mm
+// margin (float rounding of the test values is far below it).  Primitive obstacles only (no EXT).
+template <class Grp>
+__device__ __forceinline__ uint32_t mid_env_bits(const EnvView& env, float x, float y, float z, float r,
+                                                 uint32_t acc = 0u)
+{
+    const float d = dot3(x, y, z, x, y, z);
+    float me = (__builtin_sqrtf(d) + r) * 1.001f + 1e-5f;
+    if (me != me) me = __builtin_inff();
+    const float emax = Grp::max(me);
+    const float rsq = r * r;
+    if (env.n[OBS_SPHERE])
+        acc = scan_env_type<OBS_SPHERE>(env, emax, acc, [&](const auto* o) {
+            return sphere_sphere(o[1], o[2], o[3], o[4], x, y, z, r);
+        });
+    if (env.n[OBS_CAPSULE])
+        acc = scan_env_type<OBS_CAPSULE>(env, emax, acc, [&](const auto* o) {
+            const float dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
+            const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
+            const float px = __builtin_fmaf(o[4], cdf, o[1]);
+            const float py = __builtin_fmaf(o[5], cdf, o[2]);
+            const float pz = __builtin_fmaf(o[6], cdf, o[3]);
+            const float xs = x - px, ys = y - py, zs = z - pz;
+            const float rs = r + o[7];
+            return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
+        });
+    if (env.n[OBS_ZCAPSULE])
+        acc = scan_env_type<OBS_ZCAPSULE>(env, emax, acc, [&](const auto* o) {
+            const float dot = (z - o[3]) * o[6];
+            const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
+            const float pz = __builtin_fmaf(o[6], cdf, o[3]);
+            const float xs = x - o[1], ys = y - o[2], zs = z - pz;
+            const float rs = r + o[7];
+            return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
+        });
+    if (env.n[OBS_CUBOID])
+        acc = scan_env_type<OBS_CUBOID>(env, emax, acc, [&](const auto* o) {
+            const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
+            const float a1 = max0(__builtin_fabsf(dot3(o[4], o[5], o[6], xs, ys, zs)) - o[13]);
+            const float a2 = max0(__builtin_fabsf(dot3(o[7], o[8], o[9], xs, ys, zs)) - o[14]);
+            const float a3 = max0(__builtin_fabsf(dot3(o[10], o[11], o[12], xs, ys, zs)) - o[15]);
+            return dot3(a1, a2, a3, a1, a2, a3) - rsq;
+        });
+    if (env.n[OBS_ZCUBOID])
+        acc = scan_env_type<OBS_ZCUBOID>(env, emax, acc, [&](const auto* o) {
+            const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
+            const float a1 = max0(__builtin_fabsf(dot2(o[4], o[5], xs, ys)) - o[13]);
+            const float a2 = max0(__builtin_fabsf(dot2(o[7], o[8], xs, ys)) - o[14]);
+            const float a3 = max0(__builtin_fabsf(zs) - o[15]);
+            return dot3(a1, a2, a3, a1, a2, a3) - rsq;
+        });
+    return acc;
+}
+
 // Returns acc with this lane's hits OR-ed into the sign bit.  A lane entering with its sign
 // bit already set (an earlier child hit) does not keep any obstacle loop alive.
 // tag: the deferred-query tag (kTagDefault: the group type's; bound kernels pass the check's bit)

@@ -255,6 +255,28 @@ struct BoundWaves<R, Src, std::void_t<decltype(R::kBoundWaves8)>> {
     static constexpr int v = Src::G > 1 ? R::kBoundWaves8 : R::kWavesPerEU;
 };
 
+// source kinds, numbered (the MidBound selection and the VGPU_HITSTATS counters)
+template <class Src> struct SrcKindOf;
+template <class R> struct SrcKindOf<SrcConfigsT<R>> { static constexpr int v = 0; };
+template <class R> struct SrcKindOf<SrcSamplesT<R>> { static constexpr int v = 1; };
+template <class R> struct SrcKindOf<SrcHeadT<R>> { static constexpr int v = 2; };
+template <class R> struct SrcKindOf<SrcTailT<R>> { static constexpr int v = 3; };
+template <class R> struct SrcKindOf<SrcTailMaskT<R>> { static constexpr int v = 4; };
+
+// R::kMidKinds (optional, default none): bit k set = sources of kind k evaluate the bound stage with the
+// model's mid-sphere tests, R::bound<Grp, EXT, true> (tools/gen_kernels.py MIDS).  They cut the children
+// queued where bounding hits rarely confirm (a validate tail's back-steps) and cost time where they do.
+template <class R, class = void>
+struct MidKinds {
+    static constexpr uint32_t v = 0u;
+};
+template <class R>
+struct MidKinds<R, std::void_t<decltype(R::kMidKinds)>> {
+    static constexpr uint32_t v = R::kMidKinds;
+};
+template <class R, class Src>
+inline constexpr bool kMidBound = ((MidKinds<R>::v >> SrcKindOf<Src>::v) & 1u) != 0u;
+
 // ---- stage 1: bounding masks ---------------------------------------------------------------
 template <class R, class Src, bool EXT>
 __global__ __launch_bounds__(kStagedBlock, (BoundWaves<R, Src>::v)) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
@@ -285,7 +307,9 @@ __global__ __launch_bounds__(kStagedBlock, (BoundWaves<R, Src>::v)) void bound_k
             for (int j = 0; j < R::D; ++j) src.q_out[R::D * (size_t)g + j] = v[j];
         }
     }
-    typename R::Mask m = R::template bound<Grp, EXT>(v, env, bs);
+    typename R::Mask m;
+    if constexpr (kMidBound<R, Src>) m = R::template bound<Grp, EXT, true>(v, env, bs);
+    else m = R::template bound<Grp, EXT>(v, env, bs);
     if constexpr (EXT) m |= (typename R::Mask)group_or64<Grp>(capt_defer_finish(env.pc, env.base, env.pc_lds_levels));
     if (lane == 0) {
         mask[g] = m;
@@ -393,12 +417,6 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
 // ---- stage 2: children, one check per wave ------------------------------------------------------
 #ifdef VGPU_HITSTATS
 __device__ unsigned int vgpu_hitstats[5][64][2];
-template <class Src> struct SrcKindOf;
-template <class R> struct SrcKindOf<SrcConfigsT<R>> { static constexpr int v = 0; };
-template <class R> struct SrcKindOf<SrcSamplesT<R>> { static constexpr int v = 1; };
-template <class R> struct SrcKindOf<SrcHeadT<R>> { static constexpr int v = 2; };
-template <class R> struct SrcKindOf<SrcTailT<R>> { static constexpr int v = 3; };
-template <class R> struct SrcKindOf<SrcTailMaskT<R>> { static constexpr int v = 4; };
 #endif
 // A class's kernel covers the class's item range [lo, hi) of the plan; its grid is sized by the
 // host from an upper bound (the first round's counts), so waves past hi exit at once.  The check of

@@ -13,6 +13,11 @@
 // children classes (A/B on MI355X, 2^20 cage edges): class 0 at 8 waves/EU 1.5-3 % faster than 7;
 // class 2 (checks 15, 21) at 6: 79 VGPRs since their children hold the link5 centres and stream the other
 // link's (tools/gen_kernels.py HOLD; 105 VGPRs at 4 waves/EU before, A/B 3.50 -> 3.44 ms)
+// bound stages that run the mid-sphere tests (vgpu_staged.hh MidBound, bit = SrcKindOf): the validate
+// tails' (3, 4), whose bounding hits almost never confirm (tools/hitstats.py)
+#ifndef VGPU_PANDA_MID_KINDS
+#define VGPU_PANDA_MID_KINDS ((1u << 3) | (1u << 4))
+#endif
 #ifndef VGPU_PANDA_CLASS0_WAVES
 #define VGPU_PANDA_CLASS0_WAVES 8
 #endif
@@ -54,10 +59,12 @@ struct PandaR {
         const Rake rk = rake_setup(s, g);
         rake_block(s, rk, lane, k, v);
     }
-    template <class Grp, bool EXT>
+    // validate tails (SrcTailT, SrcTailMaskT) run the mid-sphere tests in their bound stage
+    static constexpr uint32_t kMidKinds = VGPU_PANDA_MID_KINDS;
+    template <class Grp, bool EXT, bool MID = false>
     __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, const Bases& b)
     {
-        return panda_bound_mask<Grp, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, b.x, b.y, b.z);
+        return panda_bound_mask<Grp, EXT, MID>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, b.x, b.y, b.z);
     }
     template <class Grp, bool EXT>
     __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, const Bases& b)

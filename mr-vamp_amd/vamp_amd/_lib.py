@@ -137,6 +137,7 @@ SIGNATURES = {
     "vgpu_comm_destroy": (None, [VP]),
     "vgpu_comm_last_error": (C.c_char_p, [VP]),
     "vgpu_env_upload_stats": (C.c_int, [VP, C.POINTER(C.c_uint64)]),
+    "vgpu_env_pointcloud_grid": (C.c_int, [VP, C.c_int, C.POINTER(C.c_uint32)]),
     "vgpu_debug_build": (C.c_int, []),
     "vgpu_debug_violations": (C.c_int, [VP, VP, C.POINTER(C.c_uint32)]),
     "vgpu_ctx_device": (C.c_int, [VP, C.POINTER(C.c_int)]),

@@ -82,3 +82,25 @@ def test_many_tail_updates_grow_in_place_or_rebuild(vamp, oracle):
         oenv.add_sphere(c, F(r))
         if k % 50 == 49:
             assert np.array_equal(robot.fkcc_batch(q, env), oracle.fkcc_threads(oenv, q))
+
+
+def test_uploaded_grid_header_is_complete(vamp):
+    """The device copy's point-cloud header carries its cell grid (dims and offset) after a full upload, after
+    in-place tail uploads and with two clouds -- a layout slip that loses the grid changes no answer (the
+    traversal decides alone) but costs ~3x in CAPT time, so it is checked here directly."""
+    import ctypes as Cc
+
+    from vamp_amd._lib import check, load
+    lib = load()
+    ctx = vamp.context(0)
+    env = vamp.Environment()
+    env.add_pointcloud(scenes.cage_points(10000, seed=1), scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    env.add_sphere(vamp.Sphere((0.5, 0.0, 0.4), 0.1))
+    env.add_pointcloud(scenes.cage_points(3000, seed=7), scenes.R_MIN, scenes.R_MAX, scenes.R_POINT)
+    out = (Cc.c_uint32 * 4)()
+    for _ in range(2):
+        for i in range(2):
+            check(lib.vgpu_env_pointcloud_grid(env.handle(ctx), i, out), ctx.h)
+            nx, ny, nz, off = list(out)
+            assert nx > 1 and ny > 1 and nz > 1 and off > 0, (i, list(out))
+        env.add_sphere(vamp.Sphere((-0.5, 0.1, 0.4), 0.1))  # a tail upload in between

@@ -27,6 +27,19 @@ F = np.float32
 REMAT = False  # rebuild rotation matrices per check (A/B on MI355X: 5.80 -> 6.81 ms, off)
 HOLD = True    # GPU self-pair children: hold the smaller side's centres, stream the other (--no-hold: chunks)
 GATE = True    # GPU staged bound stage: the wrist checks' (q5, q6) gate table when the model has one (--no-gate)
+# GPU staged bound stage (--mids): mid-level spheres between a link-bounding sphere and its children.  A check
+# whose bounding test fires gets its bit only if one of a few spheres, each enclosing a cluster of the
+# check's children with a 0.1 mm margin, passes a CONSERVATIVE test (environment: a cull extent that bounds
+# the reference's approximate one from above; self: a plain overlap).  A child the reference reports hit
+# lies inside some mid sphere, so that sphere's test fires: results are unchanged, and bounding hits that no
+# child confirms (most of a validate tail's) queue no children.  {link: clusters} / {(link_a, link_b): ...}
+# The mid tests sit behind the bound function's MID template flag: the staged kernels turn it on per source
+# kind (R::kMidKinds, vgpu_staged.hh MidBound), since they pay only where bounding hits rarely confirm.
+MIDS = None
+MID_ENV = {"panda_link5": 4, "panda_hand": 4, "panda_link7": 3}
+MID_SELF_LINKS = {"panda_link1": 2, "panda_link2": 2, "panda_link5": 4}
+MID_SELF_CHECKS = [("panda_link1", "panda_link5"), ("panda_link2", "panda_link5")]
+MID_MARGIN = 1e-4
 
 # Emitted types.  The HIP kernels compute one configuration per lane in `float` with the
 # per-lane check bits in `uint32_t`; the CPU restatement (--cpu, mr-vamp_amd/csrc/cpu/) emits
@@ -210,6 +223,31 @@ def joint(E: Emitter, fr: dict, A, R_A, P, qoff: int = 0):
     E.flops += 2 * 16
     comp = [SV.zero() if a == 0 else (sn if a > 0 else E.neg(sn)) for a in ax]
     return qmul(E, A, (c, comp[0], comp[1], comp[2])), P
+
+
+def mid_spheres(offsets, radii, k):
+    """k spheres enclosing the given child spheres (offsets in one frame): children sorted along the
+    principal axis of their offsets and cut into k runs of near-equal size; each run's sphere is centred on
+    its box and reaches every member's far side plus MID_MARGIN (radius rounded up to float)."""
+    P = np.asarray(offsets, np.float64)
+    r = np.asarray(radii, np.float64)
+    k = max(1, min(k, len(P)))
+    if len(P) > 1:
+        _, _, vt = np.linalg.svd(P - P.mean(0))
+        order = np.argsort(P @ vt[0], kind="stable")
+    else:
+        order = np.arange(len(P))
+    out = []
+    for run in np.array_split(order, k):
+        lo = (P[run] - r[run, None]).min(0)
+        hi = (P[run] + r[run, None]).max(0)
+        c = (lo + hi) / 2
+        R = max(np.linalg.norm(P[i] - c) + r[i] for i in run) + MID_MARGIN
+        Rf = np.float32(R)
+        if float(Rf) < R:
+            Rf = np.nextafter(Rf, np.float32(np.inf))
+        out.append(([float(np.float32(v)) for v in c], float(Rf)))
+    return out
 
 
 class RobotGen:
@@ -647,9 +685,9 @@ class RobotGen:
                ["    default:", "        return false;", "    }", "}", ""]
         return "\n".join(out)
 
-    def signature(self, ret, fname, extra=""):
+    def signature(self, ret, fname, extra="", mid=False):
         dim = self.m["dimension"]
-        return [f"template <class Grp, bool EXT>",
+        return [f"template <class Grp, bool EXT, bool MID = false>" if mid else f"template <class Grp, bool EXT>",
                 f"{TY['qual']} {ret} {self.name}_{fname}(",
                 f"    {extra}" + ", ".join(f"{TY['f']} q{i}" for i in range(dim)) + ",",
                 "    const EnvView& env, float bx, float by, float bz)",
@@ -776,7 +814,10 @@ class RobotGen:
             gated = {c: b for b, c in enumerate(gate["checks"])}
         for c, o in enumerate(order):
             kind, test, ck = self.bound_test(fr, o)
-            if kind == "env":  # the check's bit is its deferred-query tag (vgpu_device.hh capt_defer_*)
+            mids = self.mids_of(ck, kind) if (MIDS and c not in gated) else None
+            if mids:
+                self.emit_mid_check(E, fr, kind, test, ck, mids, c, one)
+            elif kind == "env":  # the check's bit is its deferred-query tag (vgpu_device.hh capt_defer_*)
                 E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c}))) mask |= {one} << {c};")
             elif c in gated:
                 E.raw(f"if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c};")
@@ -790,9 +831,78 @@ class RobotGen:
                f"constexpr {mt} {self.name}_env_check_bits = {env_bits:#x}{'ull' if wide else 'u'};  // environment checks"]
         if gate is not None:
             out += self.gate_function(gate)
-        out += self.signature(mt, "bound_mask") + E.lines + ["}", ""]
+        out += self.signature(mt, "bound_mask", mid=bool(MIDS)) + E.lines + ["}", ""]
         out += self.staged_children(order)
         return "\n".join(out)
+
+    def side_spheres(self, ck, side):
+        """sphere indices of one side of a self check's child pairs"""
+        return sorted(set(p[side] for p in ck["children"]))
+
+    def mids_of(self, ck, kind):
+        """the mid spheres of a check ((frame, base flag, [(offset, radius)]) per side), or None"""
+        S = self.m["spheres"]
+        if kind == "env":
+            if ck.get("leaf") or ck["link"] not in MID_ENV:
+                return None
+            kids = [k["sphere"] for k in ck["children"]]
+            frames = {S[i]["frame"] for i in kids}
+            bases = {k["base"] for k in ck["children"]}
+            if len(frames) != 1 or len(bases) != 1:
+                return None
+            ms = mid_spheres([S[i]["offset"] for i in kids], [S[i]["radius"] for i in kids], MID_ENV[ck["link"]])
+            return [(frames.pop(), bases.pop(), ms)]
+        if tuple(ck["links"]) not in MID_SELF_CHECKS or ck.get("unreachable"):
+            return None
+        sides = []
+        for side in (0, 1):
+            ids = self.side_spheres(ck, side)
+            frames = {S[i]["frame"] for i in ids}
+            if len(frames) != 1:
+                return None
+            ms = mid_spheres([S[i]["offset"] for i in ids], [S[i]["radius"] for i in ids],
+                             MID_SELF_LINKS.get(ck["links"][side], 1))
+            sides.append((frames.pop(), False, ms))
+        return sides
+
+    def emit_mid_check(self, E, fr, kind, test, ck, mids, c, one):
+        """bound test, then (MID instantiations: non-EXT environments / every self test) the mid spheres'
+        conservative tests"""
+        if kind == "env":
+            E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c}))) {{")
+        else:
+            E.raw(f"if (Grp::any({test})) {{")
+        E.indent += 1
+        if kind == "env":
+            E.raw(f"if constexpr (EXT || !MID) {{ mask |= {one} << {c}; }} else {{")
+            E.indent += 1
+            frame, base, ms = mids[0]
+            E.raw(bdecl("hm", "sign bit: a mid sphere may touch an obstacle"))
+            for off, R in ms:
+                w = self.world(fr.center(frame, off), base)
+                E.raw(f"hm = mid_env_bits<Grp>(env, {w[0]}, {w[1]}, {w[2]}, {flit(R)}, hm);")
+            E.raw(f"if (Grp::any_bits(hm)) mask |= {one} << {c};")
+            E.indent -= 1
+            E.raw("}")
+        else:
+            (fa, _, ma), (fb, _, mb) = mids
+            ca = [fr.center(fa, off) for off, _ in ma]
+            cb = [fr.center(fb, off) for off, _ in mb]
+            terms = []
+            for (oa, ra), xa in zip(ma, ca):
+                for (ob, rb), xb in zip(mb, cb):
+                    terms.append(f"self_lane({xa[0].expr()}, {xa[1].expr()}, {xa[2].expr()}, {flit(ra)}, "
+                                 f"{xb[0].expr()}, {xb[1].expr()}, {xb[2].expr()}, {flit(rb)})")
+            E.raw(f"if constexpr (!MID) {{ mask |= {one} << {c}; }} else {{")
+            E.indent += 1
+            E.raw("uint32_t hm = 0u;  // some mid pair overlaps")
+            for t in terms:
+                E.raw(f"hm |= (uint32_t){t};")
+            E.raw(f"if (Grp::any(hm != 0u)) mask |= {one} << {c};")
+            E.indent -= 1
+            E.raw("}")
+        E.indent -= 1
+        E.raw("}")
 
     def staged_children(self, order):
         """<robot>_children(check, q..., env, base): check c's children, frames recomputed"""
@@ -870,7 +980,7 @@ def gen_radii(paths) -> str:
 
 
 def main():
-    global REMAT, TY, HOLD, GATE
+    global REMAT, TY, HOLD, GATE, MIDS
     if "--radii" in sys.argv:  # tools/gen_kernels.py --radii OUT model/a.json model/b.json ...
         args = [a for a in sys.argv[1:] if a != "--radii"]
         open(args[0], "w").write(gen_radii(args[1:]))
@@ -887,6 +997,9 @@ def main():
     if "--no-gate" in sys.argv:
         GATE = False
         sys.argv.remove("--no-gate")
+    if "--mids" in sys.argv:
+        MIDS = True
+        sys.argv.remove("--mids")
     argv = [a for a in sys.argv if not a.startswith("--")]
     sys.argv[1:3] = argv[1:3]
     model = json.load(open(sys.argv[1]))
