@@ -245,6 +245,7 @@ struct vgpu_ctx {
     bool staged = true;
     bool stats = false;  // print each staged pass's per-check bounding counts (VAMP_AMD_STAGED_STATS)
     std::vector<uint64_t> rounds;  // check sets run in order (staged); empty = chosen per batch
+    long one_round = -1;           // A/B: source kinds run as one round (VAMP_AMD_ONE_ROUND), -1 = the robot's
     uint32_t* st_mask = nullptr;
     size_t st_mask_cap = 0;
     uint32_t* st_q = nullptr;  // staged sampling without a caller buffer: the drawn configurations
@@ -338,6 +339,7 @@ extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
     if (const char* s = std::getenv("VAMP_AMD_STAGED")) c->staged = std::strcmp(s, "0") != 0;
     if (const char* s = std::getenv("VAMP_AMD_KNN")) c->knn_mode = std::atoi(s);
     if (const char* s = std::getenv("VAMP_AMD_STAGED_STATS")) c->stats = std::strcmp(s, "0") != 0;
+    if (const char* s = std::getenv("VAMP_AMD_ONE_ROUND")) c->one_round = std::strtol(s, nullptr, 0);
     if (const char* s = std::getenv("VAMP_AMD_ROUNDS")) {  // A/B: comma-separated check bit masks
         for (const char* p = s; *p;) {
             char* end = nullptr;
@@ -1308,16 +1310,20 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
         std::fprintf(stderr, "\n");
     }
     std::vector<uint64_t> rounds(c->rounds.begin(), c->rounds.end());
-    if (rounds.empty() && ((ops.one_round_kinds >> kind) & 1u)) rounds = {all};
+    const unsigned one_round = c->one_round >= 0 ? (unsigned)c->one_round : ops.one_round_kinds;
+    if (rounds.empty() && ((one_round >> kind) & 1u)) rounds = {all};
     if (rounds.empty()) {
-        // Rounds from this batch's bounding statistics: (1) the first three environment checks
-        // that fire at all (the links that leave the base region -- they invalidate most groups
-        // cheaply), (3) self checks whose bounding spheres overlap for ~every group (adjacent
-        // links: many children, rarely a hit), (2) everything else.  Later rounds only see the
-        // groups still valid: the reference's early exit, recovered at round granularity.
+        // Rounds from this batch's bounding statistics: (1) the environment check that fires for
+        // the most groups, alone (the Panda's link-5 sphere: it fires for ~every group of an
+        // invalid-heavy batch and its children confirm 97 % of them there, so later rounds see few
+        // groups), (3) self checks whose bounding spheres overlap for ~every group (adjacent links:
+        // many children, rarely a hit), (2) everything else.  Later rounds only see the groups still
+        // valid: the reference's early exit, recovered at round granularity.  A/B on MI355X
+        // (profiles/r04k_rounds_ab.log) against round 1 = the first three environment checks that
+        // fire: set A 1.61 -> 1.45 ms, set B 2.41 -> 2.36-2.39, fkcc 0.85 -> 0.855.
         uint64_t r1 = 0, r3 = 0;
-        for (int k = 0, taken = 0; k < checks && taken < 3; ++k)
-            if (((env_bits >> k) & 1u) && fired[k]) r1 |= 1ull << k, ++taken;
+        for (int k = 0, best = -1; k < checks; ++k)
+            if (((env_bits >> k) & 1u) && fired[k] && (best < 0 || fired[k] > fired[best])) r1 = 1ull << k, best = k;
         for (int k = 0; k < checks; ++k)
             if (!((env_bits >> k) & 1u) && fired[k] >= n - n / 100) r3 |= 1ull << k;
         rounds = {r1, all & ~r1 & ~r3, r3};

@@ -14,7 +14,9 @@
 // class 2 (checks 15, 21) at 6: 79 VGPRs since their children hold the link5 centres and stream the other
 // link's (tools/gen_kernels.py HOLD; 105 VGPRs at 4 waves/EU before, A/B 3.50 -> 3.44 ms)
 // bound stages that run the mid-sphere tests (vgpu_staged.hh MidBound, bit = SrcKindOf): the validate
-// tails' (3, 4), whose bounding hits almost never confirm (tools/hitstats.py)
+// tails' (3, 4), whose bounding hits almost never confirm (tools/hitstats.py).  A/B on MI355X, two
+// alternating runs (profiles/r04k_mid_ab.log): tails set B 2.40-2.42 ms vs none 2.57, set A and fkcc equal;
+// head + tails: set A 1.94-1.96 vs 1.61-1.64 (head hits mostly confirm, so the mid tests are pure cost)
 #ifndef VGPU_PANDA_MID_KINDS
 #define VGPU_PANDA_MID_KINDS ((1u << 3) | (1u << 4))
 #endif

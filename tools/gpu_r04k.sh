@@ -19,3 +19,5 @@ done
 grep -v amdgpu.ids gpurun_out/r04k_ab.log
 timeout -k 10 300 python bench.py --steps 10 --warmup 2 > gpurun_out/bench_r04k_validate.json 2> gpurun_out/bench_r04k_validate.err || { tail -20 gpurun_out/bench_r04k_validate.err; exit 1; }
 python3 -c "import json; d=json.load(open('gpurun_out/bench_r04k_validate.json')); r=d['roofline']; print('validate', d['value'], 'ms', d['ms_per_step'], 'kernel_ms', r.get('kernel_ms'), 'parity', d.get('parity'))"
+# rounds led by check 8 alone (the link-5 environment check: fires for ~every set A head group, 97 % confirm)
+SETS="default 0x100,0x18,0xfffffee7 0x100,0xfffffeff 0x100,0x18,0x80430800,0x7fbcf6e0" timeout -k 10 600 bash tools/rounds_ab.sh r04k || exit 1
