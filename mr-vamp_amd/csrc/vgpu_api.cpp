@@ -65,7 +65,11 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
     hipError_t vgpu_##NAME##_staged_children(int kind, const void* s0, const void* s1, const void* s2,               \
                                              const void* s3, uint64_t first, const void* plan, const uint32_t* ub,   \
                                              const uint32_t* items, const EnvView* env, const float* bases,          \
-                                             uint8_t* valid, hipStream_t st);
+                                             uint8_t* valid, hipStream_t st);                                         \
+    int vgpu_##NAME##_staged_lead_check(void);                                                                       \
+    hipError_t vgpu_##NAME##_staged_lead(int kind, const void* s0, const void* s1, const void* s2, const void* s3,   \
+                                         uint64_t first, uint32_t n_groups, const EnvView* env, const float* bases,  \
+                                         uint8_t* valid, hipStream_t st);
 VGPU_STAGED_DECL(panda)
 VGPU_STAGED_DECL(fetch)
 VGPU_STAGED_DECL(ur5)
@@ -246,6 +250,7 @@ struct vgpu_ctx {
     bool stats = false;  // print each staged pass's per-check bounding counts (VAMP_AMD_STAGED_STATS)
     std::vector<uint64_t> rounds;  // check sets run in order (staged); empty = chosen per batch
     long one_round = -1;           // A/B: source kinds run as one round (VAMP_AMD_ONE_ROUND), -1 = the robot's
+    long lead = -1;                // A/B: source kinds that run the lead pass (VAMP_AMD_LEAD), -1 = the robot's
     uint32_t* st_mask = nullptr;
     size_t st_mask_cap = 0;
     uint32_t* st_q = nullptr;  // staged sampling without a caller buffer: the drawn configurations
@@ -340,6 +345,7 @@ extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
     if (const char* s = std::getenv("VAMP_AMD_KNN")) c->knn_mode = std::atoi(s);
     if (const char* s = std::getenv("VAMP_AMD_STAGED_STATS")) c->stats = std::strcmp(s, "0") != 0;
     if (const char* s = std::getenv("VAMP_AMD_ONE_ROUND")) c->one_round = std::strtol(s, nullptr, 0);
+    if (const char* s = std::getenv("VAMP_AMD_LEAD")) c->lead = std::strtol(s, nullptr, 0);
     if (const char* s = std::getenv("VAMP_AMD_ROUNDS")) {  // A/B: comma-separated check bit masks
         for (const char* p = s; *p;) {
             char* end = nullptr;
@@ -870,6 +876,7 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
             g.tests_off = (uint32_t)o_tests;
             g.starts_off = (uint32_t)o_starts;
             g.aff_off = (uint32_t)o_aff;
+            g.aabbs_off = (uint32_t)o_aabbs;
             g.cells_off = (uint32_t)dpos();
             const size_t hole = (2 * (size_t)g.nx * g.ny * g.nz + 15) & ~(size_t)15;
             if (holes) holes->push_back({blob.size(), hole});
@@ -1217,23 +1224,32 @@ struct StagedOps {
     // source kinds (bit k = kind k) run as ONE round of every check: there the rounds' bookkeeping costs
     // more than their early exit saves (A/B on MI355X, profiles/r04e_ab.log, r04f_rounds_ab.log: the Fetch
     // sampler 1.09 -> 1.02 ms per 4M draws, the composite 10.69-10.73 -> 10.53-10.55 ms per 2^20 edges;
-    // the Panda keeps its rounds: set B 2.53 vs 2.85 ms, set A 1.61 vs 2.95, CAPT 0.52 vs 0.64)
+    // the Panda keeps its rounds for heads and configurations: set B 2.53 vs 2.85 ms, set A 1.61 vs 2.95, CAPT
+    // 0.52 vs 0.64; its validate tails, whose bound stage runs the mid-sphere tests, take one round: set B
+    // 2.33-2.37 -> 2.32, set A 1.41-1.45 -> 1.40, profiles/r04l_ab.log)
     unsigned one_round_kinds;
+    int (*lead_check)(void);  // the robot's lead check (vgpu_staged.hh lead_kernel), -1: none
+    hipError_t (*lead)(int, const void*, const void*, const void*, const void*, uint64_t, uint32_t, const EnvView*,
+                       const float*, uint8_t*, hipStream_t);
+    // source kinds (bit k = kind k) that run the lead pass first: where its check invalidates most
+    // groups, the chained bound stage skips them (the Panda's validate heads, A/B in DESIGN.md §5d)
+    unsigned lead_kinds;
 };
-#define VGPU_STAGED_OPS(NAME, ONE_ROUND)                                                                             \
+#define VGPU_STAGED_OPS(NAME, ONE_ROUND, LEAD)                                                                           \
     StagedOps                                                                                                        \
     {                                                                                                                \
         vgpu_##NAME##_staged_checks, vgpu_##NAME##_staged_env_checks, vgpu_##NAME##_staged_mask_bytes,               \
             vgpu_##NAME##_staged_class, vgpu_##NAME##_staged_plan_bytes, vgpu_##NAME##_staged_blocks,                \
             vgpu_##NAME##_staged_bound, vgpu_##NAME##_staged_count, vgpu_##NAME##_staged_plan,                       \
-            vgpu_##NAME##_staged_queue, vgpu_##NAME##_staged_children, ONE_ROUND                                     \
+            vgpu_##NAME##_staged_queue, vgpu_##NAME##_staged_children, ONE_ROUND, vgpu_##NAME##_staged_lead_check,   \
+            vgpu_##NAME##_staged_lead, LEAD                                                                          \
     }
-static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda, 0u);
-static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch, 1u << 1);  // the sampler
-static const StagedOps kUr5Staged = VGPU_STAGED_OPS(ur5, 0u);
+static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda, (1u << 3) | (1u << 4), 1u << 2);
+static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch, 1u << 1, 0u);  // the sampler
+static const StagedOps kUr5Staged = VGPU_STAGED_OPS(ur5, 0u, 0u);
 // the two-Panda composite: four chained passes (vgpu_pair_staged.hip) -- arm A, arm B, inter-arm chunks
-static const StagedOps kPairStaged[4] = {VGPU_STAGED_OPS(pair_a, 0x1Fu), VGPU_STAGED_OPS(pair_b, 0x1Fu),
-                                         VGPU_STAGED_OPS(pair_i0, 0x1Fu), VGPU_STAGED_OPS(pair_i1, 0x1Fu)};
+static const StagedOps kPairStaged[4] = {VGPU_STAGED_OPS(pair_a, 0x1Fu, 0u), VGPU_STAGED_OPS(pair_b, 0x1Fu, 0u),
+                                         VGPU_STAGED_OPS(pair_i0, 0x1Fu, 0u), VGPU_STAGED_OPS(pair_i1, 0x1Fu, 0u)};
 
 // robots built from vgpu_robot.hh (one TU each): their launch table, or NULL
 static const RobotOps* generic_ops(int32_t kind)
@@ -1245,10 +1261,10 @@ static const RobotOps* generic_ops(int32_t kind)
     }
 }
 // the Baxter: its 388 checks in 7 chained chunks of <= 64 (vgpu_baxter_staged.hip)
-static const StagedOps kBaxterStaged[7] = {VGPU_STAGED_OPS(baxter_c0, 0u), VGPU_STAGED_OPS(baxter_c1, 0u),
-                                           VGPU_STAGED_OPS(baxter_c2, 0u), VGPU_STAGED_OPS(baxter_c3, 0u),
-                                           VGPU_STAGED_OPS(baxter_c4, 0u), VGPU_STAGED_OPS(baxter_c5, 0u),
-                                           VGPU_STAGED_OPS(baxter_c6, 0u)};
+static const StagedOps kBaxterStaged[7] = {VGPU_STAGED_OPS(baxter_c0, 0u, 0u), VGPU_STAGED_OPS(baxter_c1, 0u, 0u),
+                                           VGPU_STAGED_OPS(baxter_c2, 0u, 0u), VGPU_STAGED_OPS(baxter_c3, 0u, 0u),
+                                           VGPU_STAGED_OPS(baxter_c4, 0u, 0u), VGPU_STAGED_OPS(baxter_c5, 0u, 0u),
+                                           VGPU_STAGED_OPS(baxter_c6, 0u, 0u)};
 // A robot's staged pipeline: one pass, or several chained passes over the same groups (check lists
 // beyond one 64-bit mask, the composite's arms and inter-arm checks)
 struct StagedChain {
@@ -1293,10 +1309,19 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* 
     void* plan = c->st_cnt + 2 * cells_al;
     void* tmp = c->st_cnt + 2 * cells_al + plan_words;
     HIPCHK(c, hipMemsetAsync(counts + cells, 0, sizeof(uint32_t), c->cur));
+    // the lead pass: one check for every group first (it initialises the flags), the rest chained
+    const int lead = ops.lead_check();
+    const unsigned lead_kinds = c->lead >= 0 ? (unsigned)c->lead : ops.lead_kinds;
+    const bool use_lead = lead >= 0 && !chain && ((lead_kinds >> kind) & 1u) && v->n_hf == 0 && v->n_pc == 0;
+    if (use_lead) {
+        HIPCHK(c, ops.lead(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, valid, c->cur));
+        chain = 1;
+    }
     HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, chain, c->st_mask, valid, c->cur));
-    const uint64_t all = checks >= 64 ? ~0ull : ((1ull << checks) - 1ull);
+    uint64_t all = checks >= 64 ? ~0ull : ((1ull << checks) - 1ull);
+    if (use_lead) all &= ~(1ull << lead);  // decided by the lead pass
     const uint64_t env_bits = ops.env_checks();
-    // every check's fired groups (all groups valid here): segment boundaries offs[k * nb], k = 0..checks
+    // every check's fired groups (groups still valid): segment boundaries offs[k * nb], k = 0..checks
     HIPCHK(c, ops.count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, all, valid, counts, c->cur));
     HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
     HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t), checks + 1,

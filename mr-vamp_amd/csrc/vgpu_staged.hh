@@ -319,6 +319,36 @@ __global__ __launch_bounds__(kStagedBlock, (BoundWaves<R, Src>::v)) void bound_k
     }
 }
 
+// ---- lead pass (optional, R::kLeadCheck): one check, monolithic, before the bound stage ----------
+// R::lead<Grp>(v, env, bases) evaluates check kLeadCheck alone -- bounding test, then its children when
+// the group's bounding test fires -- and is true when the group passes it.  The pass initialises the
+// flags; the bound stage then runs chained (a group the lead check invalidated skips it) and the
+// rounds leave the lead check out.  Primitive environments only (no point clouds or heightfields).
+template <class R, class = void>
+struct LeadCheck {
+    static constexpr int v = -1;
+};
+template <class R>
+struct LeadCheck<R, std::void_t<decltype(R::kLeadCheck)>> {
+    static constexpr int v = R::kLeadCheck;
+};
+
+template <class R, class Src>
+__global__ __launch_bounds__(kStagedBlock, (BoundWaves<R, Src>::v)) void lead_kernel(Src src, uint32_t n_groups,
+                                                                                EnvView env, Bases bs,
+                                                                                uint8_t* __restrict__ valid)
+{
+    using Grp = typename GrpOf<Src::G>::T;
+    const size_t tid = (size_t)blockIdx.x * kStagedBlock + threadIdx.x;
+    const uint32_t g = (uint32_t)(tid / Src::G);
+    const int lane = (int)(tid % Src::G);
+    if (g >= n_groups) return;  // group-uniform
+    float v[R::D];
+    src.load(g, lane, v);
+    const bool ok = R::template lead<Grp>(v, env, bs);
+    if (lane == 0) valid[src.out(g)] = ok ? 1 : 0;
+}
+
 // ---- rounds: the fired (group, check) pairs of a set of checks, for groups still valid ----------
 // Checks run in rounds (e.g. the environment checks, then the self checks): a group invalidated by
 // an earlier round contributes no work to later ones, which recovers the reference's early exit.
@@ -389,8 +419,14 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
     const uint32_t g = blockIdx.x * kStagedBlock + threadIdx.x;
     const M m = round_bits<R>(src, mask, n_groups, set, valid, g);
     const int w = threadIdx.x >> 6;
-    __shared__ uint32_t wcnt[kStagedBlock / 64][R::kChecks];
-    for (int i = threadIdx.x; i < (kStagedBlock / 64) * R::kChecks; i += kStagedBlock) (&wcnt[0][0])[i] = 0u;
+    constexpr int kW = kStagedBlock / 64;
+    __shared__ uint32_t wcnt[kW][R::kChecks];
+    __shared__ uint32_t cbase[R::kChecks];
+    const size_t nb = gridDim.x;
+    for (int i = threadIdx.x; i < kW * R::kChecks; i += kStagedBlock) (&wcnt[0][0])[i] = 0u;
+    // the block's first slot in every check's segment: all loads issued at once, not one per set bit
+    for (int c = threadIdx.x; c < R::kChecks; c += kStagedBlock)
+        cbase[c] = plan->start[c] + (offs[(size_t)c * nb + blockIdx.x] - offs[(size_t)c * nb]);
     __syncthreads();
     const M any = wave_or(m);
     for (M a = any; a; a &= a - 1) {
@@ -400,11 +436,10 @@ __global__ __launch_bounds__(kStagedBlock) void queue_kernel(Src src, const type
     }
     __syncthreads();
     const uint64_t below = (__lane_id() == 0) ? 0ull : (~0ull >> (64 - __lane_id()));
-    const size_t nb = gridDim.x;
     for (M a = any; a; a &= a - 1) {
         const int c = mask_ctz(a);
         const uint64_t b = __builtin_amdgcn_ballot_w64((m >> c) & 1u);
-        uint32_t base = plan->start[c] + (offs[(size_t)c * nb + blockIdx.x] - offs[(size_t)c * nb]);
+        uint32_t base = cbase[c];
         for (int i = 0; i < w; ++i) base += wcnt[i][c];
         if ((m >> c) & 1u) {
             const uint32_t slot = base + (uint32_t)__builtin_popcountll(b & below);
@@ -505,6 +540,21 @@ struct StagedHost {
             hipLaunchKernelGGL((bound_kernel<R, Src, false>), dim3(grid), dim3(kStagedBlock), 0, st, src, n_groups,
                                *env, bs, chain, mask, valid);
         return hipGetLastError();
+    }
+
+    template <class Src>
+    static hipError_t lead(const Src& src, uint32_t n_groups, const EnvView* env, const Bases& bs, uint8_t* valid,
+                           hipStream_t st)
+    {
+        if constexpr (LeadCheck<R>::v < 0 || !Src::kInit) {
+            return hipErrorInvalidValue;
+        } else {
+            if (env->n_hf > 0 || env->n_pc > 0) return hipErrorInvalidValue;
+            if (n_groups == 0) return hipSuccess;
+            hipLaunchKernelGGL((lead_kernel<R, Src>), dim3(grid_of<Src>(n_groups)), dim3(kStagedBlock), 0, st, src,
+                               n_groups, *env, bs, valid);
+            return hipGetLastError();
+        }
     }
 
     template <class Src>
@@ -618,6 +668,16 @@ struct StagedHost {
         return H::with_source(kind, s0, s1, s2, s3, first, [&](auto src) {                                          \
             return H::bound(src, n_groups, env, bs, chain, (typename R::Mask*)mask, valid, st);                      \
         });                                                                                                          \
+    }                                                                                                                \
+    int vgpu_##NAME##_staged_lead_check(void) { return vgpu::LeadCheck<R>::v; }                                   \
+    hipError_t vgpu_##NAME##_staged_lead(int kind, const void* s0, const void* s1, const void* s2, const void* s3,   \
+                                         uint64_t first, uint32_t n_groups, const EnvView* env, const float* bases,  \
+                                         uint8_t* valid, hipStream_t st)                                             \
+    {                                                                                                                \
+        using H = vgpu::StagedHost<R>;                                                                               \
+        const Bases bs{bases[0], bases[1], bases[2], bases[3], bases[4], bases[5]};                            \
+        return H::with_source(kind, s0, s1, s2, s3, first,                                                           \
+                              [&](auto src) { return H::lead(src, n_groups, env, bs, valid, st); });                \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_count(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \

@@ -68,6 +68,13 @@ struct PandaR {
     {
         return panda_bound_mask<Grp, EXT, MID>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, b.x, b.y, b.z);
     }
+    // the lead pass (vgpu_staged.hh lead_kernel): check 8, the link-5 environment check
+    static constexpr int kLeadCheck = panda_lead_check;
+    template <class Grp>
+    __device__ static __forceinline__ bool lead(const float* v, const EnvView& env, const Bases& b)
+    {
+        return panda_lead<Grp, false>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], env, b.x, b.y, b.z);
+    }
     template <class Grp, bool EXT>
     __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, const Bases& b)
     {

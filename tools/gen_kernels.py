@@ -36,6 +36,11 @@ GATE = True    # GPU staged bound stage: the wrist checks' (q5, q6) gate table w
 # The mid tests sit behind the bound function's MID template flag: the staged kernels turn it on per source
 # kind (R::kMidKinds, vgpu_staged.hh MidBound), since they pay only where bounding hits rarely confirm.
 MIDS = None
+# GPU staged lead pass: {robot: link} -- that link's environment check, bounding test and children in one
+# monolithic pass before the bound stage (vgpu_staged.hh lead_kernel), so that the groups it invalidates
+# skip the bound stage.  The Panda's link 5: it fires for ~every group of an invalid-heavy batch and
+# its children confirm 97 % of them there (tools/hitstats.py).
+LEAD = {"panda": "panda_link5"}
 MID_ENV = {"panda_link5": 4, "panda_hand": 4, "panda_link7": 3}
 MID_SELF_LINKS = {"panda_link1": 2, "panda_link2": 2, "panda_link5": 4}
 MID_SELF_CHECKS = [("panda_link1", "panda_link5"), ("panda_link2", "panda_link5")]
@@ -693,14 +698,15 @@ class RobotGen:
                 "    const EnvView& env, float bx, float by, float bz)",
                 "{"]
 
-    def gen_fkcc(self) -> str:
+    def gen_fkcc(self, order=None, fname="fkcc", note=None) -> str:
         """Monolithic fkcc: FK emitted lazily in check order; per check the bounding test, and
-        the children only when any lane of the group fires (Grp::any), early return."""
+        the children only when any lane of the group fires (Grp::any), early return.  `order`: a
+        subset of the checks (the staged lead pass, `fname` "lead")."""
         E = Emitter()
         fr = self.Frames(self, E)
         m = self.m
         posed = False
-        for o in m["check_order"]:
+        for o in (m["check_order"] if order is None else order):
             if REMAT:
                 fr.R.clear()
             if o["kind"] in ("att", "attenv"):
@@ -737,7 +743,8 @@ class RobotGen:
         E.raw("return true;")
         hdr = [f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
                "// Monolithic fkcc: checks follow the reference hierarchy (link-bounding sphere first,",
-               "// children only when the group's bounding test fires)."] + self.signature("bool", "fkcc")
+               "// children only when the group's bounding test fires)."] if note is None else note
+        hdr = hdr + self.signature("bool", fname)
         return "\n".join(hdr + E.lines + ["}", ""])
 
     def emit_att_check(self, E, fr, o):
@@ -833,6 +840,14 @@ class RobotGen:
             out += self.gate_function(gate)
         out += self.signature(mt, "bound_mask", mid=bool(MIDS)) + E.lines + ["}", ""]
         out += self.staged_children(order)
+        lead = [c for c, o in enumerate(order) if o["kind"] == "env" and
+                m["env_checks"][o["index"]]["link"] == LEAD.get(self.name)]
+        if lead:
+            c = lead[0]
+            out += ["", f"constexpr int {self.name}_lead_check = {c};",
+                    self.gen_fkcc([order[c]], "lead",
+                                  [f"// staged lead pass: check {c} ({LEAD[self.name]} vs the environment) alone, "
+                                   "monolithic -- true when it passes"])]
         return "\n".join(out)
 
     def side_spheres(self, ck, side):
