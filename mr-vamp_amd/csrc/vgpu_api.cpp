@@ -876,7 +876,6 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
             g.tests_off = (uint32_t)o_tests;
             g.starts_off = (uint32_t)o_starts;
             g.aff_off = (uint32_t)o_aff;
-            g.aabbs_off = (uint32_t)o_aabbs;
             g.cells_off = (uint32_t)dpos();
             const size_t hole = (2 * (size_t)g.nx * g.ny * g.nz + 15) & ~(size_t)15;
             if (holes) holes->push_back({blob.size(), hole});

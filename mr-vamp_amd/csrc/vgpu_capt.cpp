@@ -196,9 +196,7 @@ bool capt_grid_plan(const CaptTree& t, size_t cells, CaptGridArgs& g)
     g.nz = n[2];
     g.unit = (float)(1.0 / (double)g.inv_h / 256.0);
     g.nlog2 = t.nlog2;
-    const double reach = m * 1.01;
-    g.reach2 = (float)(reach * reach);
-    return g.unit > 0.0f && std::isfinite(g.unit) && std::isfinite(g.reach2);
+    return g.unit > 0.0f && std::isfinite(g.unit);
 }
 
 }  // namespace vgpu

@@ -29,8 +29,7 @@ void capt_build(const float* points, size_t n, float r_min, float r_max, float r
 
 // Cell grid of a device copy (vgpu_capt_grid.hip); offsets in floats into the environment blob.
 struct CaptGridArgs {
-    uint32_t tests_off, starts_off, aff_off, aabbs_off;
-    float reach2;  // ((r_max + r_point) * 1.01)^2: bounds beyond it decide nothing for radii <= r_max
+    uint32_t tests_off, starts_off, aff_off;
     int nlog2;
     float x0, y0, z0, inv_h;
     uint32_t nx, ny, nz;

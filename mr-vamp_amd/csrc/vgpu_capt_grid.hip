@@ -22,13 +22,6 @@
 // (r + r_point)^2 < (lo)^2 * 0.9999 -> miss and > (hi)^2 * 1.0001 -> hit: the reference's
 // fma sum-of-squares differs from the exact squared distance by < 1e-6 relative (all terms
 // non-negative), and the float products of the bound by < 1e-6.
-// Leaves are pruned with their point boxes (the CAPT's aabbs: each leaf's representative and
-// affordances): a leaf's affordances are scanned only if the box's least distance to the cell is
-// below min(lo^2 so far, reach^2) or, while hi is still live, its largest farthest-corner distance is
-// above hi^2 so far (both bounds use the scan's own float operations, so they bound every point's
-// value from below / above).  lo is stored as min(lo, reach): exact below reach and still a lower
-// bound above it, where every radius <= r_max is a miss either way; hi above reach is stored as "no
-// bound" (hi only decides hits, and a radius <= r_max never exceeds it there).
 #include "vgpu_capt.hh"
 #include "vgpu_device.hh"
 
@@ -85,7 +78,6 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
     const float* __restrict__ tests = base + g.tests_off;
     const uint32_t* __restrict__ starts = (const uint32_t*)(base + g.starts_off);
     const float* __restrict__ aff = base + g.aff_off;
-    const float* __restrict__ boxes = base + g.aabbs_off;
     const int nlog2 = g.nlog2;
 
     // the deepest node containing the whole expanded cell
@@ -99,7 +91,6 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
     }
     // the leaves reachable from it, depth first
     float lo2 = __builtin_inff(), hi2 = 0.0f;
-    bool hi_live = true;  // false: hi above reach (or unbounded) -- stored as no bound
     int leaves = 0;
     bool bounded = nlog2 < kStackDepth;
     int sp = 0;
@@ -114,34 +105,8 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
                 break;
             }
             const uint32_t leaf = n - first_leaf;
-            const uint32_t j0 = starts[leaf], j1 = starts[leaf + 1];
-            if (j0 == j1) {  // an empty leaf: no lo, and no hit bound
-                hi_live = false;
-                continue;
-            }
-            {
-                const float* bx = boxes + 6u * leaf;
-                float nb = 0.0f, fb = 0.0f, fl = 0.0f;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float bl = bx[k], bu = bx[3 + k];
-                    const float near = fmaxf(fmaxf(Lf[k] - bu, bl - Uf[k]), 0.0f);
-                    const float far = fmaxf(fmaxf(fabsf(bl - Lf[k]), fabsf(bu - Lf[k])),
-                                            fmaxf(fabsf(bl - Uf[k]), fabsf(bu - Uf[k])));
-                    // farthest-corner distance of the box's nearest point to the cell centre, from below
-                    const float mid = 0.5f * (Lf[k] + Uf[k]);
-                    const float fmin = 0.5f * (Uf[k] - Lf[k]) + fmaxf(fmaxf(bl - mid, mid - bu), 0.0f);
-                    nb = __builtin_fmaf(near, near, nb);
-                    fb = __builtin_fmaf(far, far, fb);
-                    fl = __builtin_fmaf(fmin, fmin, fl);
-                }
-                if (fl * 0.999f > g.reach2) hi_live = false;  // every affordance's hmin is beyond reach
-                const bool need_lo = nb < fminf(lo2, g.reach2);
-                const bool need_hi = hi_live && fb > hi2;
-                if (!need_lo && !need_hi) continue;
-            }
             float lmin = __builtin_inff(), hmin = __builtin_inff();
-            for (uint32_t j = j0; j < j1; ++j) {
+            for (uint32_t j = starts[leaf], e = starts[leaf + 1]; j < e; ++j) {
                 const float* v = aff + 24u * j;
 #pragma unroll
                 for (int l = 0; l < 8; ++l) {
@@ -161,8 +126,7 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
                 }
             }
             lo2 = fminf(lo2, lmin);
-            hi2 = fmaxf(hi2, hmin);
-            if (hi2 > g.reach2) hi_live = false;
+            hi2 = fmaxf(hi2, hmin);  // an empty leaf: +inf, no hit bound
             continue;
         }
         const int lv = 31 - __builtin_clz(n + 1u);
@@ -176,8 +140,6 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
         if (L[ax] < (double)t || t != t) stk[sp++][tx] = 2u * n + 1u;    // some a < t (or NaN t)
     }
     uint32_t lq = 0u, hq = 0xFFFFu;
-    lo2 = fminf(lo2, g.reach2);
-    if (!hi_live) hi2 = __builtin_inff();
     if (bounded) {
         // float rounding of the squared sums and of sqrt: < 4e-7 relative; taken off lo and added to hi
         // before the extra whole unit below

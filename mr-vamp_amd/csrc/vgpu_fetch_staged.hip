@@ -85,6 +85,20 @@ __global__ __launch_bounds__(kStagedBlock) void fetch_tail_counts_kernel(const f
 
 VGPU_STAGED_EXPORTS(vgpu::FetchR, fetch)
 
+#ifdef VGPU_HITSTATS
+// development statistics of the VGPU_HITSTATS variant (this translation unit's counters: the Fetch passes),
+// laid out as vgpu_panda_hitstats's
+extern "C" int vgpu_fetch_hitstats(unsigned int* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vgpu::vgpu_hitstats), sizeof(vgpu::vgpu_hitstats)) != hipSuccess) return -2;
+    if (reset) {
+        static const unsigned int zero[5][64][2] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vgpu::vgpu_hitstats), zero, sizeof(zero)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
+
 extern "C" hipError_t vgpu_launch_fetch_tail_counts(const float* starts, const float* goals, size_t n_edges,
                                                     const uint8_t* ok, int32_t* n_blocks, uint32_t* cnt,
                                                     hipStream_t st)

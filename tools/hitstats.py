@@ -5,6 +5,8 @@ one CAPT fkcc call: per (source kind, check) the children items run and how many
 children work that only confirms a bounding hit that is no collision.
 
     VAMP_AMD_LIB=mr-vamp_amd/vamp_amd/libvampgpu_hs.so python tools/hitstats.py > gpurun_out/hitstats.json
+    VAMP_AMD_LIB=... python tools/hitstats.py --fetch   # the Fetch: configs[3]'s sampler (4M draws) and the
+                                                        # edge stage at 100k vertices
 """
 import ctypes as C
 import json
@@ -21,7 +23,48 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import bench  # noqa: E402
 
 
+def fetch_main():
+    import torch
+
+    import vamp_amd as vamp
+    from vamp_amd import roadmap
+    from vamp_amd._lib import load
+    lib = load()
+    fn = lib.vgpu_fetch_hitstats
+    fn.restype = C.c_int
+    fn.argtypes = [C.POINTER(C.c_uint32), C.c_int]
+    buf = (C.c_uint32 * (5 * 64 * 2))()
+    dev = torch.device("cuda", 0)
+    ctx = vamp.context(0)
+    st = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(st)
+    ctx.set_stream(st.cuda_stream)
+    env, _ = bench.fetch_scene(vamp)
+    env.handle(ctx)
+    out = {}
+
+    def grab(tag):
+        torch.cuda.synchronize(dev)
+        assert fn(buf, 1) == 0
+        a = np.frombuffer(buf, np.uint32).reshape(5, 64, 2).copy()
+        out[tag] = {f"kind{k}_check{c}": {"items": int(a[k, c, 0]), "hits": int(a[k, c, 1]),
+                                          "hit_rate": int(a[k, c, 1]) / int(a[k, c, 0])}
+                    for k in range(5) for c in range(64) if a[k, c, 0]}
+
+    fn(buf, 1)
+    rows, _, cnt = roadmap.sample_valid_shard(torch, vamp.fetch, env, 1, 4_000_000, ctx, dev)
+    grab("fetch_sampler_4M")
+    V = rows[:min(100_000, cnt)].contiguous()
+    comm = roadmap.Comm(ctx, 0, 1, roadmap.Comm.unique_id())
+    fn(buf, 1)
+    roadmap.build_roadmap_edges_comm(torch, vamp.fetch, env, V, comm)
+    grab("fetch_edges_100k")
+    print(json.dumps(out))
+
+
 def main():
+    if "--fetch" in sys.argv:
+        return fetch_main()
     import torch
 
     import vamp_amd as vamp
