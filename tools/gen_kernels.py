@@ -41,6 +41,10 @@ MIDS = None
 # skip the bound stage.  The Panda's link 5: it fires for ~every group of an invalid-heavy batch and
 # its children confirm 97 % of them there (tools/hitstats.py).
 LEAD = {"panda": "panda_link5"}
+# GPU staged children: robots whose environment children leave at the group's first hit (primitive
+# environments).  Off: for the Panda it changed nothing measurable (set B 2.33-2.36 vs 2.33-2.34 ms, pair
+# 10.49 vs 10.43-10.50; profiles/r04q_early_ab.log) -- unlike the lead pass, where it took set A 1.06 -> 0.81
+EARLY_CHILDREN = set()
 MID_ENV = {"panda_link5": 4, "panda_hand": 4, "panda_link7": 3}
 MID_SELF_LINKS = {"panda_link1": 2, "panda_link2": 2, "panda_link5": 4}
 MID_SELF_CHECKS = [("panda_link1", "panda_link5"), ("panda_link2", "panda_link5")]
@@ -393,15 +397,23 @@ class RobotGen:
         bi = links.index(e["bound"])
         return fr.bound_center(bi), m["bounding"][bi]["radius"]
 
-    def emit_children(self, E, fr, kind, ck, on_hit):
-        """Children of a fired check; `on_hit` is the statement run when any lane's child fires."""
+    def emit_children(self, E, fr, kind, ck, on_hit, early=False):
+        """Children of a fired check; `on_hit` is the statement run when any lane's child fires.
+        early: environment children leave as soon as one fires for the group (a group whose
+        answer is known stops; the wave stops when all its groups have); "primitive": only in
+        instantiations without point clouds (EXT false)."""
         spheres = self.m["spheres"]
         if kind == "env":
             E.raw(bdecl("h", "sign bit: this lane hit (a hit lane keeps no obstacle loop alive)"))
-            for kid in ck["children"]:
+            kids = ck["children"]
+            for i, kid in enumerate(kids):
                 sp = spheres[kid["sphere"]]
                 cw = self.world(fr.center(sp["frame"], sp["offset"]), kid["base"])
                 E.raw(f"h = env_bits<Grp, EXT>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])}, h);")
+                if early == "primitive" and i + 1 < len(kids):  # staged: point-cloud queries may be deferred
+                    E.raw(f"if constexpr (!EXT) {{ if (Grp::any_bits(h)) {on_hit} }}")
+                elif early and i + 1 < len(kids):
+                    E.raw(f"if (Grp::any_bits(h)) {on_hit}")
             E.raw(f"if (Grp::any_bits(h)) {on_hit}")
             return
         pairs = ck["children"]
@@ -698,7 +710,7 @@ class RobotGen:
                 "    const EnvView& env, float bx, float by, float bz)",
                 "{"]
 
-    def gen_fkcc(self, order=None, fname="fkcc", note=None) -> str:
+    def gen_fkcc(self, order=None, fname="fkcc", note=None, early=False) -> str:
         """Monolithic fkcc: FK emitted lazily in check order; per check the bounding test, and
         the children only when any lane of the group fires (Grp::any), early return.  `order`: a
         subset of the checks (the staged lead pass, `fname` "lead")."""
@@ -737,7 +749,7 @@ class RobotGen:
             else:
                 E.raw(f"if (Grp::any({test})) {{")
             E.indent += 1
-            self.emit_children(E, fr, kind, ck, "return false;")
+            self.emit_children(E, fr, kind, ck, "return false;", early)
             E.indent -= 1
             E.raw("}")
         E.raw("return true;")
@@ -847,7 +859,8 @@ class RobotGen:
             out += ["", f"constexpr int {self.name}_lead_check = {c};",
                     self.gen_fkcc([order[c]], "lead",
                                   [f"// staged lead pass: check {c} ({LEAD[self.name]} vs the environment) alone, "
-                                   "monolithic -- true when it passes"])]
+                                   "monolithic -- true when it passes; a group leaves at its first child hit"],
+                                  early=True)]
         return "\n".join(out)
 
     def side_spheres(self, ck, side):
@@ -941,7 +954,7 @@ class RobotGen:
                 for sa, sb in ck["children"]:
                     fr.rot(m["spheres"][sa]["frame"])
                     fr.rot(m["spheres"][sb]["frame"])
-            self.emit_children(E, fr, kind, ck, "return true;")
+            self.emit_children(E, fr, kind, ck, "return true;", "primitive" if self.name in EARLY_CHILDREN else False)
             body += [f"    case {c}: {{  // {kind}: {label} ({len(ck['children'])} children)"] + E.lines + \
                     ["        return false;", "    }"]
         out = self.signature("bool", "children", "int check, ")
