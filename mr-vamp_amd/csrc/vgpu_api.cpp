@@ -1244,7 +1244,9 @@ struct StagedOps {
             vgpu_##NAME##_staged_lead, LEAD                                                                          \
     }
 static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda, (1u << 3) | (1u << 4), 1u << 2);
-static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch, 1u << 1, 0u);  // the sampler
+// the Fetch: the sampler and the validate tails as one round (edge stage at 100k vertices 26.12-26.14 ->
+// 25.81-25.97 ms per step, profiles/r04t_fetch_rounds_ab.log)
+static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch, (1u << 1) | (1u << 3) | (1u << 4), 0u);
 static const StagedOps kUr5Staged = VGPU_STAGED_OPS(ur5, 0u, 0u);
 // the two-Panda composite: four chained passes (vgpu_pair_staged.hip) -- arm A, arm B, inter-arm chunks
 static const StagedOps kPairStaged[4] = {VGPU_STAGED_OPS(pair_a, 0x1Fu, 0u), VGPU_STAGED_OPS(pair_b, 0x1Fu, 0u),
