@@ -56,7 +56,6 @@ def parse():
     ap.add_argument("--oracle-edges", type=int, default=1 << 18,
                     help="edges checked against the scalar oracle (the CPU rake checks every edge)")
     ap.add_argument("--no-fk-leg", dest="fk_leg", action="store_false")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
     ap.add_argument("--workload", default="validate",
                     choices=["validate", "capt", "fetch_prm", "prm_edges", "pair", "rrtc"],
                     help="validate: BASELINE configs[1] (the headline); capt: configs[2]; fetch_prm: configs[3] "
@@ -211,14 +210,38 @@ def algorithmic_flops(oenv, starts, goals, base, n=65536):
     return float(h.mean()), float(t.mean()), int(len(h))
 
 
-def traffic_record(path):
-    """HBM bytes per head-kernel launch from a rocprofv3 --pmc pass of this code (written by
-    tools/profile_round.sh); None when that file is absent."""
-    try:
-        with open(path) as f:
-            return json.load(f)
-    except (OSError, ValueError):
-        return None
+def prof_record(workload):
+    """The newest committed step profile of a workload (tools/prof_step.sh -> profiles/rNN_prof_<workload>.json,
+    the highest round NN): kernel trace + PMC of exactly one timed step of this build's code.  (path, record) or
+    (None, None)."""
+    import glob
+    import re
+    best = None
+    for path in glob.glob(os.path.join(ROOT, "profiles", f"r*_prof_{workload}.json")):
+        m = re.match(r"r(\d+)_prof_", os.path.basename(path))
+        if m and (best is None or int(m.group(1)) > best[0]):
+            best = (int(m.group(1)), path)
+    if best is None:
+        return None, None
+    with open(best[1]) as f:
+        return os.path.relpath(best[1], ROOT), json.load(f)
+
+
+def traffic_fields(workload, units):
+    """`traffic` of a roofline from the workload's committed profile: its HBM bytes per call ((2 x FETCH_SIZE +
+    WRITE_SIZE) x 1 KiB over the step's kernels, MI355X_MICROARCH.md's gfx950 correction) scaled to this run's
+    units, plus the per-kernel L2 hit rates when the profile has them"""
+    path, rec = prof_record(workload)
+    if not rec or not rec.get("hbm_bytes_per_call"):
+        return {"traffic": None, "traffic_source": None}
+    out = {"traffic": rec["hbm_bytes_per_call"] * units / rec["units_per_call"],
+           "traffic_source": f"{path}: PMC of one timed step of this workload (not measured in this run), "
+                             f"{rec['hbm_bytes_per_call'] / rec['units_per_call']:.1f} B per {rec.get('unit', 'unit')}"}
+    l2 = {k: v["L2_hit_rate"] for k, v in (rec.get("kernels") or {}).items()
+          if v.get("L2_hit_rate") is not None and v.get("ms_per_call", 0) > 0.01}
+    if l2:
+        out["l2_hit_rate"] = l2
+    return out
 
 
 def c_ok_head_items(n_blocks, n_evaluated):
@@ -389,9 +412,10 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                                f"{world} GPU(s), all-gather of valid vertices",
                    "robot": "Fetch", "draws_total": a.draws, "vertices": int(n_vertices),
                    "parallelism": f"dp{world} (contiguous draw ranges, one all-gather)"},
-        "roofline": {"kernel": "fetch_sample_fkcc_kernel", "bound": "valu", "achieved": achieved,
+        "roofline": {"kernel": "vgpu_sample_fkcc: staged Halton + scale + fkcc (bound / queue / children kernels)",
+                     "bound": "valu", "achieved": achieved,
                      "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-                     "traffic": None, "kernel_ms": kern_ms, "algorithmic_flops_per_sample": f_sample,
+                     **traffic_fields("fetch_prm", n), "kernel_ms": kern_ms, "algorithmic_flops_per_sample": f_sample,
                      "algorithmic_bytes_per_sample": 8 * 4 + 1, "step_ms_events": step_ev_ms,
                      "frac_meaning": FRAC_MEANING,
                      "executed": executed_record("fetch_prm", n, step_ev_ms) if world == 1 else None,
@@ -519,11 +543,15 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     torch.cuda.synchronize(dev)
     gather_ms, validate_ms = e0.elapsed_time(e1), e1.elapsed_time(e2)
     cand_interp = float(8 * nbc[:candidates].long().sum().item())
+    # a strided sample of the candidate edges for the algorithmic flop count (rank 0, below)
+    stride = max(1, candidates // 8192)
+    cand_sample = (starts[:candidates:stride][:8192].cpu().numpy(), goals[:candidates:stride][:8192].cpu().numpy())
     del starts, goals, okc, nbc, nb_i, cc_i, offs
     phases = {"knn_index_ms": knn["index"], "gather_ms": gather_ms, "validate_ms": validate_ms,
               "validate_candidates": candidates, "validate_interpolants_full_mask_count": cand_interp,
               "validate_interpolants_per_s_full_mask_count": cand_interp / (validate_ms * 1e-3),
-              "rest_of_step_ms (selection, exchange, assembly, D2H)": step_ev_ms - knn["index"] - gather_ms - validate_ms,
+              "rest_of_step_ms (selection, exchange, assembly, D2H)":
+                  step_ev_ms - knn["index" if n >= 65536 else "brute"] - gather_ms - validate_ms,
               "torch_path_gpu_knn_gather_validate_ms": (t1 - t0) * 1e3, "torch_path_exchange_ms": (t2 - t1) * 1e3,
               "torch_path_device_assembly_ms": (t3 - t2) * 1e3,
               "step_roadmap_equals_host_assembly_of_torch_path_pairs": step_equal,
@@ -534,9 +562,38 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     # algorithmic work of the brute-force query kernel: one Space<8>::distance per (vertex, earlier
     # vertex) pair = 8 sub + 8 mul + 7 add + 1 sqrt (nn.hh:53-57)
     pairs_scanned = sum(range(qf, qf + qc))
-    flops = 24.0 * pairs_scanned
     knn_ms = knn.get("brute")
-    achieved = flops / (knn_ms * 1e-3) / 1e12 if knn_ms else None
+    knn_brute_tflops = 24.0 * pairs_scanned / (knn_ms * 1e-3) / 1e12 if knn_ms else None
+    # the step's dominant work: validate_motion of every candidate edge (the Fetch's staged bound / queue /
+    # children kernels), priced in the float ops the reference executes for those edges (early exit
+    # included), counted by the instrumented restatement on a strided sample of this run's candidates
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_py as op
+    from test_oracle_fetch import fetch_env
+
+    oenv = fetch_env(op, fx)
+    f_cand = float(op.robot_validate_flops("fetch", oenv, *cand_sample, threads=host_threads()).mean())
+    val_tflops = f_cand * candidates / (validate_ms * 1e-3) / 1e12
+    # the spatial-index kNN: its bytes past L2 (PMC of the committed step profile at this size) over its time
+    prof_w = "prm_edges" if n <= 200_000 else "prm_edges_full"
+    ppath, prec = prof_record(prof_w)
+    knn_bytes = None
+    if prec and int(prec.get("units_per_call", 0)) == n:
+        for kname, kv in (prec.get("kernels") or {}).items():
+            if kname.startswith("knnidx::group_kernel") and kv.get("FETCH_SIZE") is not None:
+                knn_bytes = (2 * kv["FETCH_SIZE"] + kv.get("WRITE_SIZE", 0.0)) * 1024.0
+    knn_roof = {"kernel": "knnidx::group_kernel<8, 4> (causal neighbour queries through the spatial index)",
+                "bound": "hbm", "ms": knn["index"], "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                "traffic": knn_bytes,
+                "achieved_traffic_rate": knn_bytes / (knn["index"] * 1e-3) / 1e9 if knn_bytes else None,
+                "frac_traffic_rate": knn_bytes / (knn["index"] * 1e-3) / 1e9 / HBM_PEAK_GBS if knn_bytes else None,
+                "algorithmic_bytes": int(n * dim * 4 + qc * (4 + 8 * kmax)),
+                "traffic_source": f"{ppath}: (2 x FETCH_SIZE + WRITE_SIZE) of the kernel in one timed step"
+                if knn_bytes else None,
+                "note": "algorithmic bytes = the vertex set once + the lists; the kernel re-reads candidate tiles "
+                        "(traffic past L2, served mostly by the 256 MB Infinity Cache): its rate against the HBM peak "
+                        "is the measure of how close it runs to the memory system's limit"}
+    parity = None
     cpu = None
     if not a.no_cpu and world == 1:
         # the reference's host path for the stage: an exact k-d tree neighbour query (nigh's role,
@@ -554,11 +611,13 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
             qm = (np.arange(len(qi)) - np.repeat(np.cumsum(cn_.astype(np.int64)) - cn_, cn_.astype(np.int64)))
             qj = nb_[qi, qm].astype(np.int64)
             t_nn = time.perf_counter() - t
-            robot.cpu_validate_batch(Vh[qj], Vh[qi], env, threads=threads)
+            ok_c = robot.cpu_validate_batch(Vh[qj], Vh[qi], env, threads=threads)[0]
             dt = time.perf_counter() - t
             if dt >= a.cpu_seconds / 3 or m >= n:
                 break
             m = min(n, int(m * min(4.0, max(1.3, (a.cpu_seconds / max(dt, 1e-3)) ** 0.5))))
+        parity = graph_parity(n, m, qi[ok_c], qj[ok_c], off_h.numpy(), adj_h[:info["n_adj"]].numpy(),
+                              comp_h[:n].numpy(), roadmap)
         cpu = {"value": m / dt, "unit": "vertices/s", "cores": threads, "kind": "port",
                "sample": f"the first {m} vertices of the same sequence: exact k-d tree neighbour queries "
                          f"(vgpu_cpu_roadmap_knn, {t_nn:.2f} s) + validate_motion of the {len(qi)} candidates on the "
@@ -584,23 +643,65 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                    "robot": "Fetch", "vertices": n, "kmax": kmax, "candidate_edges_rank0": candidates,
                    "valid_edges": info.get("pairs"), "components": info.get("components"),
                    "parallelism": f"dp{world} (query ranges of equal prefix work, one all-gather)"},
-        "roofline": {"kernel": "knn_kernel<8, K> (causal neighbour queries, brute force)", "bound": "valu",
-                     "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP32_PEAK_TFLOPS if achieved else None,
-                     "traffic": None, "kernel_ms": knn_ms, "step_kernel_ms_events": step_ev_ms,
-                     "algorithmic_flops_per_vertex_pair": 24, "vertex_pairs_rank0": pairs_scanned,
+        "roofline": {"kernel": "validate_motion of the step's candidate edges: the Fetch staged bound / queue / "
+                               "children kernels (rank 0's candidates)", "bound": "valu",
+                     "achieved": val_tflops, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": val_tflops / FP32_PEAK_TFLOPS, "kernel_ms": validate_ms,
+                     "algorithmic_flops_per_candidate_edge": f_cand, "candidate_edges": candidates,
+                     "algorithmic_bytes_per_candidate_edge": 2 * dim * 4 + 1, **traffic_fields(prof_w, n),
+                     "traffic_note": "traffic = HBM bytes of the whole step (all its kernels) from the committed profile",
+                     "step_kernel_ms_events": step_ev_ms, "frac_meaning": FRAC_MEANING,
+                     "knn_index": knn_roof,
+                     "knn_brute": {"ms": knn_ms, "achieved_tflops": knn_brute_tflops,
+                                   "algorithmic_flops_per_vertex_pair": 24, "vertex_pairs_rank0": pairs_scanned,
+                                   "note": "the brute-force kernel (not run by the step: auto mode uses the index "
+                                           "from 65536 vertices), timed for the index == brute force check"},
                      "knn_ms": knn, "knn_mode_in_step": "index" if n >= 65536 else "brute",
                      "index_equals_brute": index_equals_brute,
-                     "executed": executed_record("prm_edges" if n <= 200_000 else "prm_edges_full", n, step_ev_ms),
-                     "note": "roofline of the brute-force kernel (every pair evaluated); the index kernel's time is "
-                             "beside it, not priced in flops (it skips pairs); `executed` is over the whole step"},
+                     "executed": executed_record(prof_w, n, step_ev_ms),
+                     "executed_note": "over the whole step"},
         "cpu_baseline": cpu,
+        "parity": parity,
         "phases": phases,
     }
     emit(line)
-    if not (index_equals_brute is not False and step_equal):
-        print("PARITY FAILURE (kNN index vs brute force, or the C edge stage vs the host assembly)", file=sys.stderr)
+    graph_ok = parity is None or (parity["query_lists_mismatched"] == 0 and parity.get("graph_equal") is not False)
+    if not (index_equals_brute is not False and step_equal and graph_ok):
+        print("PARITY FAILURE (kNN index vs brute force, the C edge stage vs the host assembly, or the roadmap vs the "
+              f"CPU path): {parity}", file=sys.stderr)
         sys.exit(3)
+
+
+def graph_parity(n, m, qi, qj, off, adj, comp, roadmap):
+    """The step's roadmap (GPU) against the CPU path's graph (exact k-d tree neighbour queries + the AVX2 rake,
+    build_roadmap's append order) on the queries 0 .. m-1 the CPU leg ran: vertex i's own list -- the leading
+    entries < i of its adjacency list, appended when i was inserted (prm.hh:267-276) -- must equal i's valid
+    CPU neighbours in order; with m = n also the whole Roadmap (offsets, adjacency, components) of the host
+    assembly of the CPU pairs."""
+    off = np.asarray(off, np.int64)
+    adj = np.asarray(adj).view(np.uint32).astype(np.int64)
+    owner = np.repeat(np.arange(n, dtype=np.int64), np.diff(off))
+    own = adj < owner
+    g_i, g_j = owner[own], adj[own]
+    keep = g_i < m
+    g_i, g_j = g_i[keep], g_j[keep]
+    c_i, c_j = np.asarray(qi, np.int64), np.asarray(qj, np.int64)
+    if len(g_i) == len(c_i) and np.array_equal(g_i, c_i) and np.array_equal(g_j, c_j):
+        bad = 0
+    else:  # per query: which lists differ
+        gs = np.searchsorted(g_i, np.arange(m + 1))
+        cs = np.searchsorted(c_i, np.arange(m + 1))
+        bad = sum(1 for i in range(m) if not np.array_equal(g_j[gs[i]:gs[i + 1]], c_j[cs[i]:cs[i + 1]]))
+    rec = {"queries_compared": int(m), "query_lists_mismatched": int(bad), "valid_pairs_gpu": int(len(g_i)),
+           "valid_pairs_cpu": int(len(c_i)),
+           "checker": "CPU path on the same vertices: vgpu_cpu_roadmap_knn (exact k-d tree) + the AVX2 rake "
+                      "(mr-vamp_amd/csrc/cpu), valid pairs in query order"}
+    if m == n:
+        o2, a2, c2 = roadmap.assemble(n, np.stack([c_i, c_j], 1).astype(np.uint32))
+        rec["graph_equal"] = bool(np.array_equal(off, o2) and np.array_equal(adj, a2.astype(np.int64)) and
+                                  np.array_equal(np.asarray(comp).view(np.uint32), c2))
+        rec["graph_checker"] = "vgpu_roadmap_assemble (host) of the CPU pairs: offsets, adjacency, components"
+    return rec
 
 
 def timed_steps(a, torch, dist, dev, world, step, events=None):
@@ -633,15 +734,13 @@ VALU_ISSUE_PER_S = 256 * 4 * 2.4e9 / 2  # 1024 SIMDs x one wave64 VALU instructi
 
 def executed_record(workload, units, kernel_ms):
     """Hardware utilisation beside the reference-work `frac`: the executed VALU instructions and FP32
-    operations per unit from the committed PMC record of the same workload (profiles/r04_prof_<w>.json:
+    operations per unit from the newest committed PMC record of the same workload (profiles/rNN_prof_<w>.json:
     tools/pmc_drive.py under rocprofv3, tools/pmc_report.py), times this run's units, over this run's
     kernel time.  valu_issue_frac = SQ_INSTS_VALU / (time x 1.2288e12 wave-instructions/s);
     fp32_exec_frac = 64 x (ADD + MUL + 2 FMA) / time / peak."""
-    path = os.path.join(ROOT, "profiles", f"r04_prof_{workload}.json")
-    if not os.path.exists(path) or not kernel_ms:
+    path, rec = prof_record(workload)
+    if not rec or not kernel_ms:
         return None
-    with open(path) as f:
-        rec = json.load(f)
     pu = rec.get("per_unit") or {}
     if not pu.get("valu_insts"):
         return None
@@ -654,8 +753,8 @@ def executed_record(workload, units, kernel_ms):
             "valu_insts_per_unit": pu["valu_insts"], "fp32_ops_per_unit": pu["fp32_ops"],
             "hbm_bytes_per_call_pmc": hbm * units / rec["units_per_call"] if hbm else None,
             "pmc_kernel_ms_per_call": rec.get("kernel_ms_per_call"), "pmc_units_per_call": rec.get("units_per_call"),
-            "source": os.path.relpath(path, ROOT) + " (committed PMC of the same workload's step; per-unit counts x "
-                                                   "this run's units / this run's kernel time)"}
+            "source": path + " (committed PMC of the same workload's step; per-unit counts x this run's units / "
+                             "this run's kernel time)"}
 
 
 FRAC_MEANING = ("reference-work throughput: the float ops the reference executes for these inputs (its early exits "
@@ -787,7 +886,7 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "parallelism": f"dp{world} (independent edge shards, no collective)"},
         {"kernel": "pair_validate_head/tail kernels (one validate_motions call)", "bound": "valu",
          "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-         "traffic": None, "algorithmic_flops_per_edge": f_edge, "kernel_ms": kern_ms,
+         **traffic_fields("pair", E), "algorithmic_flops_per_edge": f_edge, "kernel_ms": kern_ms,
          "step_ms_wall": wall / a.steps * 1e3, "frac_meaning": FRAC_MEANING,
          "executed": executed_record("pair", E, kern_ms) if not strong else None},
         cpu)
@@ -974,17 +1073,7 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                "sample": f"{m} configurations of the same workload, mr-vamp_amd/csrc/cpu AVX2 rake fkcc (broadcast "
                          f"block per configuration, CAPT collides_simd), {threads} threads, {dt:.1f} s",
                "cpu_model": cpu_model()}
-    # HBM bytes per fkcc call from the committed PMC passes of the same workload (tools/gpu_capt_pmc.sh):
-    # (2 * FETCH_SIZE + WRITE_SIZE) KB of the bound + children kernels (FETCH_SIZE doubled per
-    # MI355X_MICROARCH.md; gathers are narrower than the streaming reads it was calibrated on, so
-    # this is an upper estimate), plus their L2 hit rates
-    pmc = traffic_record(os.path.join(ROOT, "profiles", "r03_capt_pmc.json"))
-    traffic, l2 = None, None
-    if pmc:
-        ks = [v for k, v in pmc["kernels"].items() if k.startswith(("bound_kernel", "children_kernel"))]
-        if ks and all("FETCH_SIZE" in v and "WRITE_SIZE" in v for v in ks):
-            traffic = sum(2 * v["FETCH_SIZE"] + v["WRITE_SIZE"] for v in ks) * 1024.0
-        l2 = {k.split("<")[0]: v.get("L2_hit_rate") for k, v in pmc["kernels"].items()}
+    tf = traffic_fields("capt", N)
     line = contract_line(
         a, world, wall_max, units_all, "CAPT point-cloud collision queries/sec (Panda 7-DOF fkcc vs 10k-point cloud)",
         "configs/s", "weak", "synthetic (10k points on the cage spheres, seed 1; uniform Panda configurations)",
@@ -992,11 +1081,10 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "robot": "PandaBase<0,0,0>", "configs_per_gpu": N, "valid_fraction": float(ok.float().mean().item()),
          "parallelism": f"dp{world} (independent shards, no collective)"},
         {"kernel": "fkcc (staged, point-cloud ext path)", "bound": "valu", "achieved": achieved,
-         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, "traffic": traffic,
-         "algorithmic_flops_per_config": f_cfg, "kernel_ms": kern_ms, "step_ms_wall": wall / a.steps * 1e3,
-         "l2_hit_rate": l2, "frac_meaning": FRAC_MEANING, "executed": executed_record("capt", N, kern_ms),
-         "traffic_source": "profiles/r03_capt_pmc.json (tools/gpu_capt_pmc.sh: rocprofv3 --pmc FETCH_SIZE, "
-                           "WRITE_SIZE, TCC_HIT_sum/TCC_MISS_sum in separate passes)",
+         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, **tf,
+         "algorithmic_bytes_per_config": 7 * 4 + 1, "algorithmic_flops_per_config": f_cfg, "kernel_ms": kern_ms,
+         "step_ms_wall": wall / a.steps * 1e3, "frac_meaning": FRAC_MEANING,
+         "executed": executed_record("capt", N, kern_ms),
          "note": "latency-bound gathers, not FLOPs: the cell grid (vgpu_capt_grid.hip) decides most sphere queries "
                  "with one dependent 8-B load after the sphere's FK; undecided ones are queued per wave in LDS and "
                  "resolved a full wave at a time (descent from the cell's node, leaf box, affordance scan: "
@@ -1192,7 +1280,9 @@ def main():
         backstep_ops = 56.0 * float((tail_items * (tail_items + 1) // 2).sum()) / max(1, len(c_nb))  # 7 rows x 8 lanes
         achieved = f_head * E / (head_ms * 1e-3) / 1e12
         achieved_step = (f_head + f_tail) * E / (kern_ms * 1e-3) / 1e12
-        tr = traffic_record(a.traffic_json) if (a.edge_set, a.base, a.scene) == ("B", "000", "cage") else None
+        prof_w = {("B", "000", "cage"): "validate", ("A", "000", "cage"): "validate_setA"}.get((a.edge_set, a.base,
+                                                                                                a.scene))
+        tf = traffic_fields(prof_w, E) if prof_w and not strong else {"traffic": None, "traffic_source": None}
         cpu = None
         parity = None
         parity_failed = []
@@ -1245,15 +1335,13 @@ def main():
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
                 "frac": achieved_step / FP32_PEAK_TFLOPS,
-                "traffic": (tr or {}).get("step_bytes_per_call"),
+                **tf,
                 "traffic_measured_in_run": False,
                 "algorithmic_flops_per_launch": (f_head + f_tail) * E,
                 "algorithmic_flops_per_edge": f_head + f_tail,
                 "kernel_ms": kern_ms,
                 "algorithmic_bytes_per_launch": EDGE_BYTES * E,
                 "hbm_frac": EDGE_BYTES * E / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                "traffic_source": ("committed PMC record of this workload, not measured in this run: " + a.traffic_json +
-                                   " (" + str((tr or {}).get("source")) + ")") if tr else None,
                 "algorithmic_flops_sample_edges": f_edges,
                 "backstep_subtract_flops_per_edge": backstep_ops,
                 "backstep_frac_of_tail": backstep_ops / max(f_tail, 1e-9),
@@ -1261,9 +1349,7 @@ def main():
                 "phase_frac": {"head": achieved / FP32_PEAK_TFLOPS,
                                "tail": f_tail * E / (max(tail_ms, 1e-9) * 1e-3) / 1e12 / FP32_PEAK_TFLOPS},
                 "frac_meaning": FRAC_MEANING,
-                "executed": executed_record({("B", "000", "cage"): "validate", ("A", "000", "cage"): "validate_setA"}
-                                            .get((a.edge_set, a.base, a.scene), "none"), E, kern_ms)
-                            if not strong else None,
+                "executed": executed_record(prof_w, E, kern_ms) if prof_w and not strong else None,
             },
             "roofline_hbm_fk": fk_leg,
             "full_mask": full_mask,

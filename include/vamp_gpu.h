@@ -419,11 +419,24 @@ int vgpu_comm_init(vgpu_ctx *ctx, int rank, int world, const uint8_t id[128], vg
 void vgpu_comm_destroy(vgpu_comm *comm);
 /* message of the communicator's last failed call (which rank failed, or what failed here) */
 const char *vgpu_comm_last_error(const vgpu_comm *comm);
-/* Collective calls below are failure-safe: a rank whose arguments, allocations or kernels fail still enters
- * the first exchange, with a failure word in place of its count; then EVERY rank returns that rank's error
- * code (the first failing rank's) and nobody blocks in the next all-gather.  Buffers and the exchange
- * stream belong to the communicator (grown on demand, freed by vgpu_comm_destroy); ctx must live on the
- * communicator's device (else VGPU_ERR_INVALID_ARG, reported to every rank). */
+/* In-process loopback communicators: `world` ranks as host threads of ONE process, each with
+ * its own context (on one device or several); the stages' all-gathers become a barrier plus device copies
+ * from every peer.  Same stage semantics as RCCL -- it runs the multi-rank logic (rank-order concatenation,
+ * count padding, failure words) at world size > 1 without a multi-GPU job.  A rank that does not arrive
+ * within VGPU_LOOPBACK_TIMEOUT_S seconds (default 120) makes its peers' exchange fail instead of hang.
+ * vgpu_loopback_destroy fails (VGPU_ERR_INVALID_ARG) while communicators still use the hub. */
+typedef struct vgpu_loopback vgpu_loopback;
+int vgpu_loopback_create(int world, vgpu_loopback **out);
+int vgpu_loopback_destroy(vgpu_loopback *hub);
+int vgpu_comm_init_loopback(vgpu_ctx *ctx, int rank, vgpu_loopback *hub, vgpu_comm **out);
+/* Collective calls below are failure-safe: a rank whose arguments (other than a null comm), allocations or
+ * kernels fail still enters the first exchange -- its word buffer is allocated with the communicator --
+ * with a failure word in place of its count; then EVERY rank returns the lowest failing rank's error code
+ * and nobody blocks in the next all-gather.  Buffers and the exchange stream belong to the communicator
+ * (grown on demand, freed by vgpu_comm_destroy); ctx must live on the communicator's device (else
+ * VGPU_ERR_INVALID_ARG, reported to every rank).  Fault injection for tests: VGPU_FAULT_INJECT=<site>[@rank]
+ * with site prm_vertices|prm_edges followed by ":args" (argument error), ":alloc" (first allocation) or
+ * nothing (after every allocation). */
 /* The PRM vertex stage of BASELINE configs[3] sharded over the ranks with ONE exchange: this rank's
  * contiguous share of draws first .. first + n_draws_total - 1 through the fused sampler + fkcc +
  * compaction, then an all-gather of the counts and of the count-padded rows and draw indices.  rows[cap][dim]

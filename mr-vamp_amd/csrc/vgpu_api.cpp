@@ -71,7 +71,10 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
                                          uint64_t first, uint32_t n_groups, const EnvView* env, const float* bases,  \
                                          uint8_t* valid, hipStream_t st);
 VGPU_STAGED_DECL(panda)
-VGPU_STAGED_DECL(fetch)
+VGPU_STAGED_DECL(fetch_p0)
+VGPU_STAGED_DECL(fetch_p1)
+VGPU_STAGED_DECL(fetch_p2)
+VGPU_STAGED_DECL(fetch_p3)
 VGPU_STAGED_DECL(ur5)
 VGPU_STAGED_DECL(pair_a)
 VGPU_STAGED_DECL(pair_b)
@@ -1233,6 +1236,9 @@ struct StagedOps {
     // source kinds (bit k = kind k) that run the lead pass first: where its check invalidates most
     // groups, the chained bound stage skips them (the Panda's validate heads, A/B in DESIGN.md §5d)
     unsigned lead_kinds;
+    // a robot compiled as several translation units by source kind (vgpu_fetch_staged.hip VGPU_FETCH_PART):
+    // by_kind[k] = the part whose exports run kind k (NULL: this table runs every kind)
+    const struct StagedOps* const* by_kind = nullptr;
 };
 #define VGPU_STAGED_OPS(NAME, ONE_ROUND, LEAD)                                                                           \
     StagedOps                                                                                                        \
@@ -1246,7 +1252,17 @@ struct StagedOps {
 static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda, (1u << 3) | (1u << 4), 1u << 2);
 // the Fetch: the sampler and the validate tails as one round (edge stage at 100k vertices 26.12-26.14 ->
 // 25.81-25.97 ms per step, profiles/r04t_fetch_rounds_ab.log)
-static const StagedOps kFetchStaged = VGPU_STAGED_OPS(fetch, (1u << 1) | (1u << 3) | (1u << 4), 0u);
+static const StagedOps kFetchParts[4] = {VGPU_STAGED_OPS(fetch_p0, (1u << 1) | (1u << 3) | (1u << 4), 0u),
+                                         VGPU_STAGED_OPS(fetch_p1, (1u << 1) | (1u << 3) | (1u << 4), 0u),
+                                         VGPU_STAGED_OPS(fetch_p2, (1u << 1) | (1u << 3) | (1u << 4), 0u),
+                                         VGPU_STAGED_OPS(fetch_p3, (1u << 1) | (1u << 3) | (1u << 4), 0u)};
+static const StagedOps* const kFetchByKind[5] = {&kFetchParts[0], &kFetchParts[0], &kFetchParts[1], &kFetchParts[2],
+                                                 &kFetchParts[3]};
+static const StagedOps kFetchStaged = [] {
+    StagedOps o = kFetchParts[0];
+    o.by_kind = kFetchByKind;
+    return o;
+}();
 static const StagedOps kUr5Staged = VGPU_STAGED_OPS(ur5, 0u, 0u);
 // the two-Panda composite: four chained passes (vgpu_pair_staged.hip) -- arm A, arm B, inter-arm chunks
 static const StagedOps kPairStaged[4] = {VGPU_STAGED_OPS(pair_a, 0x1Fu, 0u), VGPU_STAGED_OPS(pair_b, 0x1Fu, 0u),
@@ -1287,10 +1303,12 @@ static StagedChain generic_chain(int32_t kind)
 // device (plan_kernel) and read there by queue and children.
 // b: the robot base (b[0..2]) -- and the composite's second arm (b[3..5]); chain != 0: a later pass
 // over the same groups (the flags are ANDed into, groups already invalid skip every stage)
-static int staged_pass(vgpu_ctx* c, const StagedOps& ops, int kind, const void* s0, const void* s1, const void* s2,
+static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const void* s0, const void* s1, const void* s2,
                        const void* s3, uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid,
                        int chain = 0, const float* b2 = nullptr)
 {
+    if (kind < 0 || kind > 4) return fail(c, VGPU_ERR_INVALID_ARG, "staged pass: source kind");
+    const StagedOps& ops = ops_in.by_kind ? *ops_in.by_kind[kind] : ops_in;
     const float bases[6] = {b[0], b[1], b[2], b2 ? b2[0] : 0.0f, b2 ? b2[1] : 0.0f, b2 ? b2[2] : 0.0f};
     if (n == 0) return VGPU_OK;
     if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many groups in one call (< 2^31)");

@@ -6,6 +6,15 @@
 
 #include "gen/fetch_fk.inc"
 
+// One translation unit per part of the source kinds (VGPU_FETCH_PART, compiled in parallel: one TU with every
+// kind took 12.5 min): part 0 = configurations + Halton samples (+ the tail counts), 1 = validate heads,
+// 2 = validate tails, 3 = full-mask tails.  vgpu_api.cpp dispatches a kind to its part's exports.
+#ifndef VGPU_FETCH_PART
+#define VGPU_FETCH_PART 0
+#endif
+#define VGPU_CAT_(a, b) a##b
+#define VGPU_CAT(a, b) VGPU_CAT_(a, b)
+
 #ifndef VGPU_FETCH_STAGED_WAVES_PER_EU
 #define VGPU_FETCH_STAGED_WAVES_PER_EU 6
 #endif
@@ -38,6 +47,7 @@ struct FetchR {
     static constexpr int kChildWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
     using Mask = fetch_mask_t;
     static constexpr Mask kEnvChecks = fetch_env_check_bits;
+    static constexpr unsigned kSourceKinds = VGPU_FETCH_PART == 0 ? 0x3u : (0x4u << (VGPU_FETCH_PART - 1));
     static constexpr int kClasses = 3;
     static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0,
                                               0, 0, 2, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
@@ -67,6 +77,7 @@ struct FetchR {
     }
 };
 
+#if VGPU_FETCH_PART == 0
 __global__ __launch_bounds__(kStagedBlock) void fetch_tail_counts_kernel(const float* __restrict__ starts,
                                                                          const float* __restrict__ goals,
                                                                          size_t n_edges,
@@ -81,19 +92,43 @@ __global__ __launch_bounds__(kStagedBlock) void fetch_tail_counts_kernel(const f
     cnt[e] = (ok[e] && rk.n > 1) ? (uint32_t)(rk.n - 1) : 0u;
 }
 
+#endif
+
 }  // namespace vgpu
 
-VGPU_STAGED_EXPORTS(vgpu::FetchR, fetch)
+#define VGPU_STAGED_EXPORTS_X(R, NAME) VGPU_STAGED_EXPORTS(R, NAME)  // expands NAME before the pasting
+VGPU_STAGED_EXPORTS_X(vgpu::FetchR, VGPU_CAT(fetch_p, VGPU_FETCH_PART))
 
 #ifdef VGPU_HITSTATS
-// development statistics of the VGPU_HITSTATS variant (this translation unit's counters: the Fetch passes),
-// laid out as vgpu_panda_hitstats's
-extern "C" int vgpu_fetch_hitstats(unsigned int* out, int reset)
+// development statistics of the VGPU_HITSTATS variant: this part's counters (each part has its own copy of
+// vgpu_hitstats; its kinds' rows are the only ones it writes)
+extern "C" int VGPU_CAT(VGPU_CAT(vgpu_fetch_p, VGPU_FETCH_PART), _hitstats)(unsigned int* out, int reset)
 {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vgpu::vgpu_hitstats), sizeof(vgpu::vgpu_hitstats)) != hipSuccess) return -2;
     if (reset) {
         static const unsigned int zero[5][64][2] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(vgpu::vgpu_hitstats), zero, sizeof(zero)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
+
+#if VGPU_FETCH_PART == 0
+
+#ifdef VGPU_HITSTATS
+extern "C" int vgpu_fetch_p1_hitstats(unsigned int*, int);
+extern "C" int vgpu_fetch_p2_hitstats(unsigned int*, int);
+extern "C" int vgpu_fetch_p3_hitstats(unsigned int*, int);
+// the Fetch passes' counters, laid out as vgpu_panda_hitstats's: the sum over the parts
+extern "C" int vgpu_fetch_hitstats(unsigned int* out, int reset)
+{
+    static unsigned int part[5][64][2];
+    int (*fn[4])(unsigned int*, int) = {vgpu_fetch_p0_hitstats, vgpu_fetch_p1_hitstats, vgpu_fetch_p2_hitstats,
+                                        vgpu_fetch_p3_hitstats};
+    for (int i = 0; i < 5 * 64 * 2; ++i) out[i] = 0;
+    for (auto f : fn) {
+        if (int rc = f(&part[0][0][0], reset)) return rc;
+        for (int i = 0; i < 5 * 64 * 2; ++i) out[i] += (&part[0][0][0])[i];
     }
     return 0;
 }
@@ -110,3 +145,4 @@ extern "C" hipError_t vgpu_launch_fetch_tail_counts(const float* starts, const f
                        n_edges, ok, n_blocks, cnt);
     return hipGetLastError();
 }
+#endif

@@ -20,10 +20,13 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -204,7 +207,14 @@ extern "C" int vgpu_multi_sample_fkcc_host(vgpu_multi* m, const vgpu_robot* r, v
     return VGPU_OK;
 }
 
-// ---- one process per GPU: RCCL, loaded at run time ----------------------------------------------------
+// ---- one process per GPU: the exchange a communicator runs its all-gathers over -----------------------
+// The sharded stages below need exactly one collective: an all-gather of equal-sized device blocks in rank
+// order.  Two implementations sit behind it:
+//   * RCCL (librccl.so.1 loaded at run time, no torch): ncclAllGather over xGMI -- the product path;
+//   * a loopback hub: the ranks are host threads of ONE process (each with its own context, on one device
+//     or several), the all-gather is a barrier plus device copies from every peer's send block.  It runs the
+//     stages' multi-rank logic -- rank-order concatenation, count padding, failure words -- at world sizes
+//     above one on a single GPU (an in-process loopback communicator for tests).
 namespace {
 struct Rccl {
     void* h = nullptr;
@@ -235,6 +245,96 @@ Rccl& rccl()
     return R;
 }
 
+// every rank's `bytes` of send (device) into recv[k * bytes] (device), in rank order; enqueued on st or
+// completed before returning -- the caller synchronises st before reading recv
+struct Exchange {
+    virtual ~Exchange() = default;
+    virtual bool allgather(const void* send, void* recv, size_t bytes, hipStream_t st) = 0;
+};
+
+struct RcclExchange final : Exchange {
+    ncclComm_t comm = nullptr;
+    ~RcclExchange() override
+    {
+        if (comm && rccl().ok) rccl().destroy(comm);
+    }
+    bool allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override
+    {
+        return rccl().allgather(send, recv, bytes, ncclUint8, comm, st) == ncclSuccess;
+    }
+};
+}  // namespace
+
+// The loopback hub: `world` ranks as threads of this process.  A generation barrier with a timeout (a rank
+// that never arrives makes the others fail instead of hang).
+struct vgpu_loopback {
+    int world = 1;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t gen = 0;
+    int arrived = 0;
+    std::vector<const void*> send;
+    std::vector<size_t> bytes;
+    int members = 0;  // communicators created on the hub and not yet destroyed
+    int timeout_s = 120;
+
+    bool barrier()
+    {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        if (!cv.wait_for(lk, std::chrono::seconds(timeout_s), [&] { return gen != g; })) {
+            --arrived;  // leave: the peers that did arrive time out as well
+            return false;
+        }
+        return true;
+    }
+};
+
+namespace {
+struct LoopbackExchange final : Exchange {
+    vgpu_loopback* hub = nullptr;
+    int rank = 0;
+    ~LoopbackExchange() override
+    {
+        std::lock_guard<std::mutex> lk(hub->mu);
+        --hub->members;
+    }
+    bool allgather(const void* send, void* recv, size_t bytes, hipStream_t st) override
+    {
+        // the send block must be complete before a peer copies it
+        bool ok = hipStreamSynchronize(st) == hipSuccess;
+        {
+            std::lock_guard<std::mutex> lk(hub->mu);
+            hub->send[rank] = ok ? send : nullptr;
+            hub->bytes[rank] = bytes;
+        }
+        if (!hub->barrier()) return false;
+        for (int k = 0; k < hub->world; ++k) {
+            const void* src;
+            size_t b;
+            {
+                std::lock_guard<std::mutex> lk(hub->mu);
+                src = hub->send[k];
+                b = hub->bytes[k];
+            }
+            if (b != bytes || (bytes && !src)) ok = false;  // mismatched sizes or a peer's failed sync
+            if (ok && bytes &&
+                hipMemcpyAsync((char*)recv + (size_t)k * bytes, src, bytes, hipMemcpyDefault, st) != hipSuccess)
+                ok = false;
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) ok = false;
+        // the peers' send blocks stay untouched until every rank has copied them
+        if (!hub->barrier()) return false;
+        return ok;
+    }
+};
+
 // grow-only device buffers of a communicator, one per slot (the stages below name their slots)
 struct DevBuf {
     void* p = nullptr;
@@ -244,9 +344,13 @@ constexpr int kSlots = 16;
 }  // namespace
 
 struct vgpu_comm {
-    ncclComm_t comm = nullptr;
+    std::unique_ptr<Exchange> x;
     int rank = 0, world = 1, device = 0;
     hipStream_t st = nullptr;  // the exchanges' stream (the kernels run on the context's)
+    // exchange 1's word buffer (2 * world + 2 u64: the gathered words, this rank's word, the selection
+    // count), allocated with the communicator: a stage whose own allocations or arguments fail still has
+    // it, so it always enters exchange 1
+    uint64_t* words = nullptr;
     DevBuf buf[kSlots];
     std::string err;
 };
@@ -264,27 +368,45 @@ extern "C" int vgpu_comm_unique_id(uint8_t id[128])
     return VGPU_OK;
 }
 
-// RCCL prints its version banner on stdout when a communicator is created; the caller's stdout (bench.py's
-// one JSON line, a planner's output) stays clean: the banner goes to stderr
+// RCCL may print a version banner on stdout while a communicator is created.  With VGPU_RCCL_QUIET=1 the
+// caller's stdout (bench.py's one JSON line) stays clean: fd 1 is pointed at stderr for the duration of
+// ncclCommInitRank.  The redirect is process-global (other threads' stdout writes in that window go to
+// stderr too), hence opt-in.
 namespace {
 struct StdoutToStderr {
     int saved = -1;
     StdoutToStderr()
     {
+        const char* q = std::getenv("VGPU_RCCL_QUIET");
+        if (!q || std::strcmp(q, "1") != 0) return;
         std::fflush(stdout);
         saved = dup(1);
         if (saved >= 0) dup2(2, 1);
     }
     ~StdoutToStderr()
     {
+        if (saved < 0) return;
         std::fflush(stdout);
-        if (saved >= 0) {
-            dup2(saved, 1);
-            close(saved);
-        }
+        dup2(saved, 1);
+        close(saved);
     }
 };
+
+// the communicator's stream and word buffer on its device (before the exchange itself exists)
+int comm_alloc(vgpu_comm* c, int dev, int world)
+{
+    c->device = dev;
+    c->world = world;
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return VGPU_ERR_HIP;
+    if (hipMalloc(&c->words, (2 * (size_t)world + 2) * sizeof(uint64_t)) != hipSuccess) {
+        c->words = nullptr;
+        return VGPU_ERR_OOM;
+    }
+    return VGPU_OK;
+}
 }  // namespace
+
+extern "C" void vgpu_comm_destroy(vgpu_comm* c);
 
 extern "C" int vgpu_comm_init(vgpu_ctx* ctx, int rank, int world, const uint8_t id[128], vgpu_comm** out)
 {
@@ -296,25 +418,77 @@ extern "C" int vgpu_comm_init(vgpu_ctx* ctx, int rank, int world, const uint8_t 
     if (vgpu_ctx_device(ctx, &dev) != VGPU_OK || hipSetDevice(dev) != hipSuccess) return VGPU_ERR_HIP;
     auto* c = new (std::nothrow) vgpu_comm();
     if (!c) return VGPU_ERR_OOM;
-    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
-        delete c;
-        return VGPU_ERR_HIP;
-    }
+    c->rank = rank;
+    // a local allocation failure here still joins ncclCommInitRank (itself collective), then fails
+    const int arc = comm_alloc(c, dev, world);
+    auto* x = new (std::nothrow) RcclExchange();
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     ncclResult_t ir;
     {
         StdoutToStderr quiet;
-        ir = R.init(&c->comm, world, u, rank);
+        ir = x ? R.init(&x->comm, world, u, rank) : ncclSystemError;
     }
-    if (ir != ncclSuccess) {
-        (void)hipStreamDestroy(c->st);
+    c->x.reset(x);
+    if (ir != ncclSuccess || arc != VGPU_OK) {
+        vgpu_comm_destroy(c);
+        return ir != ncclSuccess ? VGPU_ERR_HIP : arc;
+    }
+    *out = c;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_loopback_create(int world, vgpu_loopback** out)
+{
+    if (!out || world < 1) return VGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    auto* h = new (std::nothrow) vgpu_loopback();
+    if (!h) return VGPU_ERR_OOM;
+    h->world = world;
+    h->send.assign(world, nullptr);
+    h->bytes.assign(world, 0);
+    if (const char* t = std::getenv("VGPU_LOOPBACK_TIMEOUT_S")) h->timeout_s = std::max(1, std::atoi(t));
+    *out = h;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_loopback_destroy(vgpu_loopback* h)
+{
+    if (!h) return VGPU_OK;
+    {
+        std::lock_guard<std::mutex> lk(h->mu);
+        if (h->members) return VGPU_ERR_INVALID_ARG;  // communicators still use it
+    }
+    delete h;
+    return VGPU_OK;
+}
+
+extern "C" int vgpu_comm_init_loopback(vgpu_ctx* ctx, int rank, vgpu_loopback* hub, vgpu_comm** out)
+{
+    if (!ctx || !hub || !out || rank < 0 || rank >= hub->world) return VGPU_ERR_INVALID_ARG;
+    *out = nullptr;
+    int dev = 0;
+    if (vgpu_ctx_device(ctx, &dev) != VGPU_OK || hipSetDevice(dev) != hipSuccess) return VGPU_ERR_HIP;
+    auto* c = new (std::nothrow) vgpu_comm();
+    auto* x = new (std::nothrow) LoopbackExchange();
+    if (!c || !x) {
         delete c;
-        return VGPU_ERR_HIP;
+        delete x;
+        return VGPU_ERR_OOM;
     }
+    x->hub = hub;
+    x->rank = rank;
+    {
+        std::lock_guard<std::mutex> lk(hub->mu);
+        ++hub->members;
+    }
+    c->x.reset(x);
     c->rank = rank;
-    c->world = world;
-    c->device = dev;
+    const int rc = comm_alloc(c, dev, hub->world);
+    if (rc != VGPU_OK) {
+        vgpu_comm_destroy(c);
+        return rc;
+    }
     *out = c;
     return VGPU_OK;
 }
@@ -326,8 +500,9 @@ extern "C" void vgpu_comm_destroy(vgpu_comm* c)
     if (c->st) (void)hipStreamSynchronize(c->st);
     for (DevBuf& b : c->buf)
         if (b.p) (void)hipFree(b.p);
+    if (c->words) (void)hipFree(c->words);
     if (c->st) (void)hipStreamDestroy(c->st);
-    if (c->comm && rccl().ok) rccl().destroy(c->comm);
+    c->x.reset();
     delete c;
 }
 
@@ -356,7 +531,9 @@ static bool comm_buf(vgpu_comm* c, int slot, size_t count, T** out)
 }
 
 // Rank-local fault injection for the failure-path tests: VGPU_FAULT_INJECT=<site>[@rank] makes that rank
-// (every rank without @) fail at <site> as an allocation failure would.
+// (every rank without @) fail at <site>.  Sites per stage: "<stage>:args" (an argument error, before
+// anything else), "<stage>:alloc" (the stage's first allocation fails), "<stage>" (after every allocation),
+// with <stage> = prm_vertices | prm_edges.
 static bool injected(const vgpu_comm* c, const char* site)
 {
     const char* v = std::getenv("VGPU_FAULT_INJECT");
@@ -368,21 +545,21 @@ static bool injected(const vgpu_comm* c, const char* site)
 }
 
 // A failing rank still enters every collective its peers enter: exchange 1 carries each rank's count, or
-// kFailTag | -code, so every rank sees the same failure and returns the same error instead of leaving its
-// peers blocked in the next all-gather.
+// kFailTag | -code, so every rank sees the same failure and returns the same error (the lowest failing
+// rank's) instead of leaving its peers blocked in the next all-gather.
 static constexpr uint64_t kFailTag = 0xFFFFFFFF00000000ull;
 
-static int exchange_counts(vgpu_comm* c, uint64_t* dev_words, int local_rc, uint64_t count, std::vector<uint64_t>& all)
+static int exchange_counts(vgpu_comm* c, int local_rc, uint64_t count, std::vector<uint64_t>& all)
 {
-    Rccl& R = rccl();
     const int W = c->world;
+    uint64_t* dev_words = c->words;
     const uint64_t mine = local_rc != VGPU_OK ? (kFailTag | (uint32_t)(-local_rc)) : count;
     all.assign(W, 0);
     if (hipMemcpyAsync(dev_words + W, &mine, 8, hipMemcpyHostToDevice, c->st) != hipSuccess ||
-        R.allgather(dev_words + W, dev_words, 1, ncclUint64, c->comm, c->st) != ncclSuccess ||
+        !c->x->allgather(dev_words + W, dev_words, 8, c->st) ||
         hipMemcpyAsync(all.data(), dev_words, W * 8, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
         hipStreamSynchronize(c->st) != hipSuccess) {
-        c->err = "count exchange (RCCL all-gather) failed";
+        c->err = "count exchange (all-gather) failed";
         return VGPU_ERR_HIP;
     }
     for (int k = 0; k < W; ++k)
@@ -401,22 +578,21 @@ static int rank_fail(vgpu_comm* c, vgpu_ctx* ctx, int rc, const char* what)
 }
 
 // exchange 2: every rank's first cnts[k] items of `send` (padded to max cnts) gathered and concatenated in
-// rank order into out; items are `words` u64 each
-static int gather_padded(vgpu_comm* c, const uint64_t* send, uint64_t* recv, const std::vector<uint64_t>& cnts,
-                         size_t words, uint64_t* out, size_t out_words_per_item_stride)
+// rank order into out; items are `item_bytes` each
+static int gather_padded(vgpu_comm* c, const void* send, void* recv, const std::vector<uint64_t>& cnts,
+                         size_t item_bytes, void* out)
 {
-    Rccl& R = rccl();
     uint64_t mx = 0;
     for (uint64_t k : cnts) mx = std::max(mx, k);
     if (!mx) return VGPU_OK;
-    if (R.allgather(send, recv, mx * words, ncclUint64, c->comm, c->st) != ncclSuccess) {
-        c->err = "RCCL all-gather failed";
+    if (!c->x->allgather(send, recv, mx * item_bytes, c->st)) {
+        c->err = "all-gather failed";
         return VGPU_ERR_HIP;
     }
     size_t at = 0;
     for (size_t k = 0; k < cnts.size(); ++k) {
-        if (cnts[k] && hipMemcpyAsync(out + at * out_words_per_item_stride, recv + k * mx * words, cnts[k] * words * 8,
-                                      hipMemcpyDeviceToDevice, c->st) != hipSuccess) {
+        if (cnts[k] && hipMemcpyAsync((char*)out + at * item_bytes, (const char*)recv + k * mx * item_bytes,
+                                      cnts[k] * item_bytes, hipMemcpyDeviceToDevice, c->st) != hipSuccess) {
             c->err = "device copy failed";
             return VGPU_ERR_HIP;
         }
@@ -429,19 +605,22 @@ static int gather_padded(vgpu_comm* c, const uint64_t* send, uint64_t* recv, con
     return VGPU_OK;
 }
 
-// the communicator's own device, and the context on it (argument errors a peer cannot see become a failed
-// exchange like any other rank-local error)
+// The communicator's device becomes current whatever the arguments (exchange 1 runs there); a context on
+// another device is a rank-local argument error like any other, reported to every rank through exchange 1.
 static int comm_enter(vgpu_ctx* ctx, vgpu_comm* comm)
 {
-    int dev = -1;
-    if (vgpu_ctx_device(ctx, &dev) != VGPU_OK) return VGPU_ERR_INVALID_ARG;
-    if (dev != comm->device) {
-        comm->err = "context device differs from the communicator's";
-        return VGPU_ERR_INVALID_ARG;
-    }
     if (hipSetDevice(comm->device) != hipSuccess) {
         comm->err = "hipSetDevice failed";
         return VGPU_ERR_HIP;
+    }
+    int dev = -1;
+    if (!ctx || vgpu_ctx_device(ctx, &dev) != VGPU_OK) {
+        comm->err = "null or invalid context";
+        return VGPU_ERR_INVALID_ARG;
+    }
+    if (dev != comm->device) {
+        comm->err = "context device differs from the communicator's";
+        return VGPU_ERR_INVALID_ARG;
     }
     return VGPU_OK;
 }
@@ -454,27 +633,28 @@ extern "C" int vgpu_prm_vertices_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const
                                            uint64_t first, size_t n_draws_total, float* rows, uint64_t* draws,
                                            size_t cap, size_t* count)
 {
-    if (!comm || !count) return VGPU_ERR_INVALID_ARG;
-    *count = 0;
+    if (!comm) return VGPU_ERR_INVALID_ARG;  // no communicator: nothing to enter (a caller bug on this rank)
     comm->err.clear();
-    if (!rccl().ok) return VGPU_ERR_UNSUPPORTED;
+    if (count) *count = 0;
     const int W = comm->world;
     const int dim = robot_dim(r);
-    int rc = (!ctx || !rows || !draws || first == 0 || dim < 1) ? VGPU_ERR_INVALID_ARG : VGPU_OK;
-    if (rc == VGPU_OK) rc = comm_enter(ctx, comm);
+    int rc = comm_enter(ctx, comm);
+    if (rc == VGPU_OK && (!count || !rows || !draws || first == 0 || dim < 1))
+        rc = VGPU_ERR_INVALID_ARG, comm->err = "invalid argument";
+    if (rc == VGPU_OK && injected(comm, "prm_vertices:args")) rc = VGPU_ERR_INVALID_ARG, comm->err = "injected failure";
     size_t lo = 0, n = 0, share_max = (n_draws_total + W - 1) / W;
     vgpu_shard_range(n_draws_total, comm->rank, W, &lo, &n);
     float *q = nullptr, *pad_rows = nullptr, *all_rows = nullptr;
     uint8_t* v = nullptr;
     uint32_t* ix = nullptr;
-    uint64_t *words = nullptr, *pad_draws = nullptr, *all_d = nullptr;
+    uint64_t *pad_draws = nullptr, *all_d = nullptr;
     // every buffer (both exchanges') up front, sized by the largest share: an allocation failure is known
     // before exchange 1 and reported through it
-    if (rc == VGPU_OK &&
+    if (rc == VGPU_OK && injected(comm, "prm_vertices:alloc")) rc = VGPU_ERR_OOM, comm->err = "injected failure";
+    if (rc == VGPU_OK && dim > 0 &&
         !(comm_buf(comm, 0, share_max * dim, &q) && comm_buf(comm, 1, share_max, &v) && comm_buf(comm, 2, share_max, &ix) &&
-          comm_buf(comm, 3, (size_t)W + 1, &words) && comm_buf(comm, 4, share_max * dim, &pad_rows) &&
-          comm_buf(comm, 5, share_max, &pad_draws) && comm_buf(comm, 6, W * share_max * dim, &all_rows) &&
-          comm_buf(comm, 7, W * share_max, &all_d)))
+          comm_buf(comm, 4, share_max * dim, &pad_rows) && comm_buf(comm, 5, share_max, &pad_draws) &&
+          comm_buf(comm, 6, W * share_max * dim, &all_rows) && comm_buf(comm, 7, W * share_max, &all_d)))
         rc = VGPU_ERR_OOM, comm->err = "device allocation failed";
     if (rc == VGPU_OK && injected(comm, "prm_vertices")) rc = VGPU_ERR_OOM, comm->err = "injected failure";
     size_t got = 0;
@@ -491,10 +671,8 @@ extern "C" int vgpu_prm_vertices_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const
             rc = VGPU_ERR_HIP;
         if (rc != VGPU_OK) comm->err = "draw index copy failed";
     }
-    // a null communicator word buffer cannot take part: nothing else to do (peers see a broken RCCL call)
-    if (!words) return rc != VGPU_OK ? rc : VGPU_ERR_OOM;
     std::vector<uint64_t> cnts;
-    rc = exchange_counts(comm, words, rc, got, cnts);  // exchange 1, always entered
+    rc = exchange_counts(comm, rc, got, cnts);  // exchange 1, always entered
     if (rc != VGPU_OK) return rc;
     uint64_t total = 0;
     for (uint64_t c : cnts) total += c;
@@ -503,25 +681,8 @@ extern "C" int vgpu_prm_vertices_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const
         return VGPU_ERR_INVALID_ARG;
     }
     // exchange 2: the count-padded rows, then the draw indices
-    uint64_t mx = 0;
-    for (uint64_t c : cnts) mx = std::max(mx, c);
-    Rccl& R = rccl();
-    if (mx) {
-        if (R.allgather(pad_rows, all_rows, mx * dim, ncclFloat32, comm->comm, comm->st) != ncclSuccess) {
-            comm->err = "RCCL all-gather failed";
-            return VGPU_ERR_HIP;
-        }
-        size_t at = 0;
-        for (int k = 0; k < W; ++k) {
-            if (cnts[k] && hipMemcpyAsync(rows + at * dim, all_rows + (size_t)k * mx * dim, cnts[k] * dim * 4,
-                                          hipMemcpyDeviceToDevice, comm->st) != hipSuccess) {
-                comm->err = "device copy failed";
-                return VGPU_ERR_HIP;
-            }
-            at += cnts[k];
-        }
-        if ((rc = gather_padded(comm, pad_draws, all_d, cnts, 1, draws, 1)) != VGPU_OK) return rc;
-    }
+    if ((rc = gather_padded(comm, pad_rows, all_rows, cnts, (size_t)dim * sizeof(float), rows)) != VGPU_OK) return rc;
+    if ((rc = gather_padded(comm, pad_draws, all_d, cnts, sizeof(uint64_t), draws)) != VGPU_OK) return rc;
     *count = (size_t)total;
     return VGPU_OK;
 }
@@ -559,16 +720,18 @@ extern "C" int vgpu_prm_edges_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const vg
                                         uint64_t* offsets, uint32_t* adj, size_t adj_cap, size_t* n_adj,
                                         uint32_t* component)
 {
-    if (!comm || !n_adj) return VGPU_ERR_INVALID_ARG;
-    *n_adj = 0;
+    if (!comm) return VGPU_ERR_INVALID_ARG;  // no communicator: nothing to enter (a caller bug on this rank)
     comm->err.clear();
-    if (!rccl().ok) return VGPU_ERR_UNSUPPORTED;
+    if (n_adj) *n_adj = 0;
     const int W = comm->world;
     const int dim = robot_dim(r);
-    int rc = (!ctx || !offsets || (n && !V) || dim < 1 || n >= ((size_t)1 << 31)) ? VGPU_ERR_INVALID_ARG : VGPU_OK;
-    if (rc == VGPU_OK) rc = comm_enter(ctx, comm);
+    int rc = comm_enter(ctx, comm);
+    if (rc == VGPU_OK && (!n_adj || !offsets || (n && !V) || dim < 1 || n >= ((size_t)1 << 31)))
+        rc = VGPU_ERR_INVALID_ARG, comm->err = "invalid argument";
+    if (rc == VGPU_OK && injected(comm, "prm_edges:args")) rc = VGPU_ERR_INVALID_ARG, comm->err = "injected failure";
     // the neighbour parameters and every rank's candidate bound (query i returns at most min(k_i, i)): the
     // same on every rank, so buffer sizes and the cap check agree everywhere
+    if (rc != VGPU_OK) n = 0;  // no per-query work sized from arguments that failed
     std::vector<uint32_t> k(std::max<size_t>(n, 1));
     std::vector<float> rad(std::max<size_t>(n, 1));
     if (rc == VGPU_OK && vgpu_prm_neighbor_params(dim, space_measure, gamma_scale, n, k.data(), rad.data()) != VGPU_OK)
@@ -593,23 +756,24 @@ extern "C" int vgpu_prm_edges_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const vg
     float *dr = nullptr, *dist = nullptr, *starts = nullptr, *goals = nullptr;
     uint8_t* ok = nullptr;
     unsigned long long *cand = nullptr, *sel = nullptr;
-    uint64_t *words = nullptr, *recv = nullptr, *pairs = nullptr;
+    uint64_t *recv = nullptr, *pairs = nullptr;
     char* tmp = nullptr;
     size_t tmp_bytes = 0;
     if (rc == VGPU_OK &&
         vgpu_launch_valid_pairs(0, 0, nullptr, 1, nullptr, nullptr, nullptr, e_mine, nullptr, nullptr, nullptr, nullptr,
                                 &tmp_bytes, nullptr) != hipSuccess)
         rc = VGPU_ERR_HIP, comm->err = "selection scratch size";
+    if (rc == VGPU_OK && injected(comm, "prm_edges:alloc")) rc = VGPU_ERR_OOM, comm->err = "injected failure";
     if (rc == VGPU_OK &&
         !(comm_buf(comm, 0, n, &dk) && comm_buf(comm, 1, n, &dr) && comm_buf(comm, 2, qc * kmax, &nbr) &&
           comm_buf(comm, 3, qc * kmax, &dist) && comm_buf(comm, 4, qc + 1, &cnt) && comm_buf(comm, 5, qc + 1, &off) &&
           comm_buf(comm, 6, e_mine * dim, &starts) && comm_buf(comm, 7, e_mine * dim, &goals) &&
           comm_buf(comm, 8, e_mine, &ok) && comm_buf(comm, 9, e_mine, &cand) && comm_buf(comm, 10, e_max, &sel) &&
-          comm_buf(comm, 11, (size_t)W + 1 + 1, &words) && comm_buf(comm, 12, (size_t)W * e_max, &recv) &&
-          comm_buf(comm, 13, (size_t)W * e_max, &pairs) && comm_buf(comm, 14, tmp_bytes, &tmp)))
+          comm_buf(comm, 12, (size_t)W * e_max, &recv) && comm_buf(comm, 13, (size_t)W * e_max, &pairs) &&
+          comm_buf(comm, 14, tmp_bytes, &tmp)))
         rc = VGPU_ERR_OOM, comm->err = "device allocation failed";
     if (rc == VGPU_OK && injected(comm, "prm_edges")) rc = VGPU_ERR_OOM, comm->err = "injected failure";
-    selc = words ? (uint32_t*)(words + W + 1) : nullptr;
+    selc = (uint32_t*)(comm->words + W + 1);  // the selection count: the communicator's own word buffer
     size_t got = 0;
     if (rc == VGPU_OK && n) {
         if (hipMemcpy(dk, k.data(), n * 4, hipMemcpyHostToDevice) != hipSuccess ||
@@ -646,9 +810,8 @@ extern "C" int vgpu_prm_edges_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const vg
             rc = VGPU_ERR_HIP, comm->err = "pair selection failed";
         got = hgot;
     }
-    if (!words) return rc != VGPU_OK ? rc : VGPU_ERR_OOM;
     std::vector<uint64_t> cnts;
-    rc = exchange_counts(comm, words, rc, got, cnts);  // exchange 1, always entered
+    rc = exchange_counts(comm, rc, got, cnts);  // exchange 1, always entered
     if (rc != VGPU_OK) return rc;
     uint64_t m = 0;
     for (uint64_t c : cnts) m += c;
@@ -657,7 +820,7 @@ extern "C" int vgpu_prm_edges_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const vg
         comm->err = "adjacency capacity too small (*n_adj = required entries)";
         return VGPU_ERR_INVALID_ARG;
     }
-    if ((rc = gather_padded(comm, (const uint64_t*)sel, recv, cnts, 1, pairs, 1)) != VGPU_OK) return rc;  // exchange 2
+    if ((rc = gather_padded(comm, sel, recv, cnts, sizeof(uint64_t), pairs)) != VGPU_OK) return rc;  // exchange 2
     return rank_fail(comm, ctx,
                      vgpu_roadmap_assemble_device(ctx, n, (const uint32_t*)pairs, (size_t)m, offsets, adj, component),
                      "roadmap assembly");

@@ -260,8 +260,15 @@ class Environment:
             self._apply(lib, h, None, op)
 
     def _push(self, op):
+        """Apply op to every realised copy, then record it.  If it fails on some copy (an invalid shape),
+        every copy is dropped and the op is not recorded: the copies cannot diverge, and later contexts
+        realise the environment without it."""
+        try:
+            self._apply_live(op)
+        except Exception:
+            self._changed()
+            raise
         self._ops.append(op)
-        self._apply_live(op)
 
     def add_sphere(self, s: Sphere):
         self._push(("sphere", s))

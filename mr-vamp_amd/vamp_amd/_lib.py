@@ -136,6 +136,9 @@ SIGNATURES = {
     "vgpu_comm_init": (C.c_int, [VP, C.c_int, C.c_int, C.POINTER(C.c_uint8), C.POINTER(VP)]),
     "vgpu_comm_destroy": (None, [VP]),
     "vgpu_comm_last_error": (C.c_char_p, [VP]),
+    "vgpu_loopback_create": (C.c_int, [C.c_int, C.POINTER(VP)]),
+    "vgpu_loopback_destroy": (C.c_int, [VP]),
+    "vgpu_comm_init_loopback": (C.c_int, [VP, C.c_int, VP, C.POINTER(VP)]),
     "vgpu_env_upload_stats": (C.c_int, [VP, C.POINTER(C.c_uint64)]),
     "vgpu_env_pointcloud_grid": (C.c_int, [VP, C.c_int, C.POINTER(C.c_uint32)]),
     "vgpu_debug_build": (C.c_int, []),

@@ -342,12 +342,16 @@ class Comm:
     128-byte id is made on rank 0 and shipped by the caller -- ``from_torch`` ships it over an
     initialised torch.distributed group (any backend), which then carries no data-path traffic."""
 
-    def __init__(self, ctx, rank: int, world: int, uid: bytes):
+    def __init__(self, ctx, rank: int, world: int, uid: Optional[bytes] = None, hub: Optional["Loopback"] = None):
         import ctypes as C
 
         from ._lib import check, load
         self.ctx, self.rank, self.world = ctx, rank, world
         self.h = C.c_void_p()
+        if hub is not None:  # a rank of an in-process loopback hub (vgpu_comm_init_loopback)
+            assert hub.world == world
+            check(load().vgpu_comm_init_loopback(ctx.h, rank, hub.h, C.byref(self.h)), ctx.h)
+            return
         buf = (C.c_uint8 * 128).from_buffer_copy(bytes(uid))
         check(load().vgpu_comm_init(ctx.h, rank, world, buf, C.byref(self.h)), ctx.h)
 
@@ -399,6 +403,26 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+class Loopback:
+    """An in-process loopback hub (vgpu_loopback_create): ``world`` ranks as threads of this process, each
+    with its own context and ``Comm(ctx, rank, world, hub=self)``; the C stages' all-gathers become device
+    copies between the ranks' buffers.  Close every Comm on it before closing the hub."""
+
+    def __init__(self, world: int):
+        import ctypes as C
+
+        from ._lib import check, load
+        self.world = world
+        self.h = C.c_void_p()
+        check(load().vgpu_loopback_create(world, C.byref(self.h)))
+
+    def close(self):
+        from ._lib import check, load
+        if self.h:
+            check(load().vgpu_loopback_destroy(self.h))
+            self.h = None
 
 
 def query_split_c(n: int, rank: int, world: int) -> Tuple[int, int]:

@@ -465,6 +465,30 @@ def robot_validate_motions(robot, env: Env, starts, goals, base100=(0, 0, 0), th
     return ok.astype(bool), n
 
 
+def robot_validate_flops(robot, env: Env, starts, goals, base100=(0, 0, 0), threads=8):
+    """Executed float ops of validate_motion per edge (reference semantics, early exit) for any robot, counted
+    by the instrumented restatement (vo_robot_validate_motion's vo_stats.flops); edges in parallel chunks"""
+    from concurrent.futures import ThreadPoolExecutor
+    rid, dim, _ = ROBOTS[robot]
+    ce = env.c()
+    L = lib()
+    s = np.ascontiguousarray(starts, np.float32).reshape(-1, dim)
+    g = np.ascontiguousarray(goals, np.float32).reshape(-1, dim)
+    fl = np.zeros(len(s))
+
+    def run(lo, hi):
+        for i in range(lo, hi):
+            st = VoStats(np.inf, np.inf, 0.0)
+            n = C.c_int()
+            L.vo_robot_validate_motion(rid, C.byref(ce), fp(s[i]), fp(g[i]), *base100, C.byref(n), C.byref(st))
+            fl[i] = st.flops
+
+    chunks = np.linspace(0, len(s), max(1, threads) + 1).astype(int)
+    with ThreadPoolExecutor(max(1, threads)) as ex:
+        list(ex.map(lambda k: run(chunks[k], chunks[k + 1]), range(len(chunks) - 1)))
+    return fl
+
+
 def mbm_env(scene: dict) -> Env:
     """A MotionBenchMaker scene (resources/<robot>/problems.tar.bz2 scene*.yaml) as an
     environment: boxes -> cuboids by the RESOLVED axes of the pose quaternion (columns of its

@@ -243,3 +243,184 @@ def test_host_staging_lands_on_the_context_device():
     q = np.zeros((64, 7), F)
     got = vamp.panda_0_0.fkcc_batch(q, env, ctx1)
     assert got.shape == (64,)
+
+
+# ---- world size > 1 on one GPU: the in-process loopback hub (vgpu_comm_init_loopback) -----------------
+def _run_ranks(world, fn):
+    """fn(rank) on one host thread per rank (ctypes releases the GIL inside the C calls); returns the
+    per-rank results, re-raising the first exception"""
+    import threading
+    out, errs = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            out[r] = fn(r)
+        except BaseException as e:  # noqa: BLE001 -- re-raised below
+            errs[r] = e
+
+    th = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=150)
+        assert not t.is_alive(), "a rank did not return (hung exchange)"
+    for e in errs:
+        if e is not None:
+            raise e
+    return out
+
+
+@pytest.fixture
+def loopback_ranks(monkeypatch):
+    """make(world) -> (contexts, comms): one fresh context per rank on device 0, one loopback hub"""
+    import vamp_amd as vamp
+    from vamp_amd import roadmap
+    monkeypatch.setenv("VGPU_LOOPBACK_TIMEOUT_S", "30")
+    made = []
+
+    def make(world):
+        ctxs = [vamp.Context(0) for _ in range(world)]
+        hub = roadmap.Loopback(world)
+        comms = [roadmap.Comm(ctxs[r], r, world, hub=hub) for r in range(world)]
+        made.append((ctxs, hub, comms))
+        return ctxs, comms
+
+    yield make
+    for ctxs, hub, comms in made:
+        for c in comms:
+            c.close()
+        hub.close()
+
+
+def _vertices_call(lib, vamp, ctx, comm, robot, env, first, n, rows, draws, cap, cnt):
+    return lib.vgpu_prm_vertices_allgather(ctx.h if ctx else None, comm.h, C.byref(robot.c_robot),
+                                           env.handle(ctx) if ctx else None, first, n,
+                                           C.c_void_p(rows.data_ptr()) if rows is not None else None,
+                                           C.c_void_p(draws.data_ptr()), cap, C.byref(cnt))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_loopback_vertex_stage_equals_single_process(loopback_ranks, world):
+    """vgpu_prm_vertices_allgather at world size 2 / 3 (ranks = threads, each its own context on device 0,
+    loopback all-gathers): every rank gets build_roadmap's vertex sequence -- the single-process sampler's
+    valid draws in draw order, bit for bit -- including ranks whose share is shorter (n not divisible)."""
+    import torch
+
+    import vamp_amd as vamp
+    from vamp_amd._lib import load
+    lib = load()
+    ctxs, comms = loopback_ranks(world)
+    env = vamp.Environment()  # a scene the Fetch collides with for some draws only
+    env.add_sphere(vamp.Sphere([0.9, 0.3, 0.8], 0.2))
+    robot = vamp.fetch
+    n, first = 40001, 3
+    for c in ctxs:
+        env.handle(c)  # realised on every context before the threads start
+    q, v = robot.sample_fkcc(first, n, env)
+    want_rows, want_draws = q[v], first + np.nonzero(v)[0]
+    bufs = [(torch.zeros((n, 8), dtype=torch.float32, device="cuda"), torch.zeros(n, dtype=torch.int64, device="cuda"))
+            for _ in range(world)]
+    torch.cuda.synchronize()
+
+    def rank(r):
+        cnt = C.c_size_t()
+        rc = _vertices_call(lib, vamp, ctxs[r], comms[r], robot, env, first, n, bufs[r][0], bufs[r][1], n, cnt)
+        return rc, cnt.value
+
+    res = _run_ranks(world, rank)
+    torch.cuda.synchronize()
+    for r, (rc, cnt) in enumerate(res):
+        assert rc == 0, (r, comms[r].last_error())
+        assert cnt == len(want_rows) and 0 < cnt < n
+        assert np.array_equal(bufs[r][0][:cnt].cpu().numpy().view(np.uint32), want_rows.view(np.uint32))
+        assert np.array_equal(bufs[r][1][:cnt].cpu().numpy(), want_draws)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_loopback_edge_stage_equals_oracle(oracle, loopback_ranks, world):
+    """vgpu_prm_edges_allgather at world size 2 / 3: each rank's query range (vgpu_query_split), its valid
+    pairs all-gathered in rank order, the roadmap assembled on every rank == the single-process C stage ==
+    the oracle's build_roadmap graph (adjacency lists in append order, components)."""
+    import torch
+
+    import vamp_amd as vamp
+    from vamp_amd import roadmap
+    ctxs, comms = loopback_ranks(world)
+    rng = np.random.default_rng(25)
+    oenv = random_scene(oracle, rng, 4, 4, 2)
+    env = gpu_env_from_oracle(vamp, oenv)
+    for c in ctxs:
+        env.handle(c)
+    q = oracle.robot_scale("fetch", rng.random((6000, 8), dtype=F))
+    V = q[oracle.robot_fkcc_threads("fetch", oenv, q)][:2500]
+    Vd = torch.from_numpy(V).cuda()
+    torch.cuda.synchronize()
+    edges, _ = oracle.build_roadmap_edges("fetch", oenv, V)
+    comp_ref = oracle.components(len(V), edges)
+
+    def rank(r):
+        off, adj, comp = roadmap.build_roadmap_edges_comm(torch, vamp.fetch, env, Vd, comms[r], ctx=ctxs[r])
+        ctxs[r].sync()
+        return off.cpu().numpy(), adj.cpu().numpy(), comp.cpu().numpy()
+
+    for off, adj, comp in _run_ranks(world, rank):
+        assert [adj[off[i]:off[i + 1]].tolist() for i in range(len(V))] == edges
+        assert np.array_equal(comp, comp_ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("stage", ["prm_vertices", "prm_edges"])
+def test_loopback_rank_failure_reaches_every_rank(loopback_ranks, monkeypatch, world, stage):
+    """A failure on rank 1 only -- an argument error (injected, and a real null output / null context), its
+    first allocation, or after every allocation -- comes back as the SAME error code from every rank, none
+    hangs in an all-gather, and the communicators stay usable for the next call."""
+    import torch
+
+    import vamp_amd as vamp
+    from vamp_amd import roadmap
+    from vamp_amd._lib import load
+    lib = load()
+    ctxs, comms = loopback_ranks(world)
+    env = vamp.Environment()
+    env.add_sphere(vamp.Sphere([0.5, 0.0, 0.5], 0.3))
+    for c in ctxs:
+        env.handle(c)
+    robot = vamp.panda_0_0
+    n = 20000
+    bufs = [(torch.zeros((n, 7), dtype=torch.float32, device="cuda"), torch.zeros(n, dtype=torch.int64, device="cuda"))
+            for _ in range(world)]
+    V = bufs[0][0][:1500].clone()
+    ebufs = [roadmap.EdgeStageBuffers(torch, 1500, V.device, 200000) for _ in range(world)]
+    torch.cuda.synchronize()
+    null = {"ctx": False, "out": False}
+
+    def call(r):
+        bad = r == 1
+        ctx = None if (bad and null["ctx"]) else ctxs[r]
+        if stage == "prm_vertices":
+            cnt = C.c_size_t()
+            rows = None if (bad and null["out"]) else bufs[r][0]
+            return _vertices_call(lib, vamp, ctx, comms[r], robot, env, 1, n, rows, bufs[r][1], n, cnt)
+        n_adj = C.c_size_t()
+        b = ebufs[r]
+        return lib.vgpu_prm_edges_allgather(ctx.h if ctx else None, comms[r].h, C.byref(robot.c_robot),
+                                            env.handle(ctxs[r]), V.data_ptr(), 1500, robot.space_measure(), 2.0,
+                                            None if (bad and null["out"]) else b.offsets.data_ptr(),
+                                            b.adj.data_ptr(), b.adj.numel(), C.byref(n_adj), b.comp.data_ptr())
+
+    assert _run_ranks(world, call) == [0] * world
+    for site, code in ((":args", -1), (":alloc", -3), ("", -3)):
+        monkeypatch.setenv("VGPU_FAULT_INJECT", f"{stage}{site}@1")
+        got = _run_ranks(world, call)
+        assert got == [code] * world, (site, got, [c.last_error() for c in comms])
+        assert "injected" in comms[1].last_error()
+        assert "rank 1 failed" in comms[0].last_error()
+    monkeypatch.delenv("VGPU_FAULT_INJECT")
+    for key in ("out", "ctx"):  # real argument errors on rank 1
+        null[key] = True
+        assert _run_ranks(world, call) == [-1] * world, key
+        null[key] = False
+    assert _run_ranks(world, call) == [0] * world

@@ -840,6 +840,17 @@ class RobotGen:
                 E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c}))) mask |= {one} << {c};")
             elif c in gated:
                 E.raw(f"if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c};")
+            elif kind == "self" and ck.get("never_fires") and not TY["cpu"]:
+                # tools/prove_self_checks.py: no child pair can fire while these joints stay in the proven box;
+                # a group with every lane inside it gets no bit (the bounding test is not even evaluated)
+                def inward(v, up):  # the float32 bound on the box's side of v
+                    f = F(v)
+                    if (up and float(f) < v) or (not up and float(f) > v):
+                        f = np.nextafter(f, F(np.inf) if up else F(-np.inf))
+                    return flit(f)
+                inside = " && ".join(f"q{d} >= {inward(lo, True)} && q{d} <= {inward(hi, False)}"
+                                     for d, lo, hi in zip(ck["never_dofs"], ck["never_lo"], ck["never_hi"]))
+                E.raw(f"if (Grp::any(!({inside})) && Grp::any({test})) mask |= {one} << {c};  // proven silent inside")
             else:
                 E.raw(f"if (Grp::any({test})) mask |= {one} << {c};")
         E.raw("return mask;")
