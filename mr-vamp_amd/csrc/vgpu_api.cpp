@@ -70,7 +70,10 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
     hipError_t vgpu_##NAME##_staged_lead(int kind, const void* s0, const void* s1, const void* s2, const void* s3,   \
                                          uint64_t first, uint32_t n_groups, const EnvView* env, const float* bases,  \
                                          uint8_t* valid, hipStream_t st);
-VGPU_STAGED_DECL(panda)
+VGPU_STAGED_DECL(panda_p0)
+VGPU_STAGED_DECL(panda_p1)
+VGPU_STAGED_DECL(panda_p2)
+VGPU_STAGED_DECL(panda_p3)
 VGPU_STAGED_DECL(fetch_p0)
 VGPU_STAGED_DECL(fetch_p1)
 VGPU_STAGED_DECL(fetch_p2)
@@ -1249,7 +1252,17 @@ struct StagedOps {
             vgpu_##NAME##_staged_queue, vgpu_##NAME##_staged_children, ONE_ROUND, vgpu_##NAME##_staged_lead_check,   \
             vgpu_##NAME##_staged_lead, LEAD                                                                          \
     }
-static const StagedOps kPandaStaged = VGPU_STAGED_OPS(panda, (1u << 3) | (1u << 4), 1u << 2);
+static const StagedOps kPandaParts[4] = {VGPU_STAGED_OPS(panda_p0, (1u << 3) | (1u << 4), 1u << 2),
+                                         VGPU_STAGED_OPS(panda_p1, (1u << 3) | (1u << 4), 1u << 2),
+                                         VGPU_STAGED_OPS(panda_p2, (1u << 3) | (1u << 4), 1u << 2),
+                                         VGPU_STAGED_OPS(panda_p3, (1u << 3) | (1u << 4), 1u << 2)};
+static const StagedOps* const kPandaByKind[5] = {&kPandaParts[0], &kPandaParts[0], &kPandaParts[1], &kPandaParts[2],
+                                                 &kPandaParts[3]};
+static const StagedOps kPandaStaged = [] {
+    StagedOps o = kPandaParts[0];
+    o.by_kind = kPandaByKind;
+    return o;
+}();
 // the Fetch: the sampler and the validate tails as one round (edge stage at 100k vertices 26.12-26.14 ->
 // 25.81-25.97 ms per step, profiles/r04t_fetch_rounds_ab.log)
 static const StagedOps kFetchParts[4] = {VGPU_STAGED_OPS(fetch_p0, (1u << 1) | (1u << 3) | (1u << 4), 0u),
@@ -1332,6 +1345,8 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const voi
     const int lead = ops.lead_check();
     const unsigned lead_kinds = c->lead >= 0 ? (unsigned)c->lead : ops.lead_kinds;
     const bool use_lead = lead >= 0 && !chain && ((lead_kinds >> kind) & 1u) && v->n_hf == 0 && v->n_pc == 0;
+    // (round 5: the lead check fused into the bound kernel -- its children inside, no second FK -- measured
+    // slower on MI355X, set B 2.33 -> 2.41 ms, set A 0.81 -> 0.90: profiles/r05c_ab.log; not kept)
     if (use_lead) {
         HIPCHK(c, ops.lead(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, valid, c->cur));
         chain = 1;

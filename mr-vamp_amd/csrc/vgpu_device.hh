@@ -317,6 +317,8 @@ __device__ __forceinline__ float max0(float v) { return (v > 0.0f) ? v : 0.0f; }
 #define VGPU_SCAN_UNROLL 2  // records per loop trip (A/B on MI355X: 1 -> 5.15 ms, 2 -> 4.97, 4 -> 5.17)
 #endif
 static_assert(kObsPad >= 2 * VGPU_SCAN_UNROLL - 1, "sentinel padding must cover the prefetch");
+// (round 5, A/B on MI355X: loading the next trip's whole sphere records ahead as well -- the tests no longer
+// waiting on their own records' scalar loads -- was slower: set B 2.32 -> 2.39-2.41 ms, profiles/r05d_ab.log)
 template <int S>
 struct ObsRec {
     float v[S];

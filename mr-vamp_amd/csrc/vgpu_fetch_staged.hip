@@ -23,9 +23,11 @@
 #ifndef VGPU_FETCH_BOUND8_WAVES
 #define VGPU_FETCH_BOUND8_WAVES 4
 #endif
-// children register classes (ChildClasses, vgpu_staged.hh): VGPRs per check compiled alone
-// (gfx950, Grp8 and Grp1 alike): <= 62 except checks 8, 17, 27, 48, 51, 56, 59 (65-70) and 23 (89);
-// one kernel over all 63 at 6 waves/EU (80 VGPRs) spilled 84-116 B/lane
+// children register classes (ChildClasses, vgpu_staged.hh) from the VGPRs each check's children kernel needs
+// compiled alone (tools/probe_children_vgprs.py, gfx950, validate tails): <= 56 for 48 checks; 60-66 for
+// checks 9, 10, 17, 20, 24, 26, 27, 33, 42, 48, 51, 56, 59; 73 for check 8; 90 for check 23.  Each class runs
+// at the occupancy whose budget holds its largest check with headroom (64 / 72 / 80 / 96 VGPRs): no scratch
+// (round 4's three classes at 64 / 72 / 96 spilled 30-60 VGPRs in classes 0 and 1)
 #ifndef VGPU_FETCH_CLASS0_WAVES
 #define VGPU_FETCH_CLASS0_WAVES 8
 #endif
@@ -33,7 +35,10 @@
 #define VGPU_FETCH_CLASS1_WAVES 7
 #endif
 #ifndef VGPU_FETCH_CLASS2_WAVES
-#define VGPU_FETCH_CLASS2_WAVES 5
+#define VGPU_FETCH_CLASS2_WAVES 6
+#endif
+#ifndef VGPU_FETCH_CLASS3_WAVES
+#define VGPU_FETCH_CLASS3_WAVES 5
 #endif
 
 namespace vgpu {
@@ -48,12 +53,10 @@ struct FetchR {
     using Mask = fetch_mask_t;
     static constexpr Mask kEnvChecks = fetch_env_check_bits;
     static constexpr unsigned kSourceKinds = VGPU_FETCH_PART == 0 ? 0x3u : (0x4u << (VGPU_FETCH_PART - 1));
-    static constexpr int kClasses = 3;
-    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0,
-                                              0, 0, 2, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,
-                                              0, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0};
+    static constexpr int kClasses = 4;
+    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 0, 0, 2, 1, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 3, 1, 0, 1, 1, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0};
     static constexpr int kClassWaves[kClasses] = {VGPU_FETCH_CLASS0_WAVES, VGPU_FETCH_CLASS1_WAVES,
-                                                  VGPU_FETCH_CLASS2_WAVES};
+                                                  VGPU_FETCH_CLASS2_WAVES, VGPU_FETCH_CLASS3_WAVES};
     __device__ static __forceinline__ void sample(uint64_t k, float v[8]) { sample_d<8>(k, fetch_s_m, fetch_s_a, v); }
     __device__ static __forceinline__ void head(const float* s, const float* g, int lane, float v[8])
     {

@@ -556,6 +556,233 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
     }
 }
 
+// ---- block-cooperative group queries (VAMP_AMD_KNN_COOP, default) --------------------------------------
+// group_kernel fetches every candidate tile once per WAVE (4 queries): at 2.7M Fetch vertices each wave
+// visits ~700 tiles spread over the whole vertex set, so the tiles miss the 4 MB L2 and ~1.1 TB per call
+// comes from the Infinity Cache.  Here the WV waves of a workgroup (4 * WV Morton-consecutive
+// queries, whose neighbourhoods overlap) decide together which super-tiles and tiles to visit -- the union
+// of their needs, a block-wide OR of each wave's ballot -- and stage each needed tile ONCE per workgroup in
+// LDS (one tile per wave per batch, double buffered: the next batch's global loads are in flight while the current
+// one is tested); a wave tests a staged tile only if one of its own queries needs it.  Same visiting rules
+// (home super-tile first, then chunks outward), same admission: the lists are again exactly the brute
+// force's.
+template <int D, int QG, int WV>
+__global__ __launch_bounds__(64 * WV) void coop_kernel(const float* __restrict__ Vs, const uint32_t* __restrict__ perm,
+                                                       uint32_t n, uint32_t T, uint32_t S,
+                                                       const float* __restrict__ tbox, const uint32_t* __restrict__ tmin,
+                                                       const float* __restrict__ sbox, const uint32_t* __restrict__ smin,
+                                                       const uint32_t* __restrict__ qlist, uint32_t q_first,
+                                                       uint32_t q_count, const uint32_t* __restrict__ kq,
+                                                       const float* __restrict__ rq, uint32_t kmax,
+                                                       uint32_t* __restrict__ nbr, float* __restrict__ dist,
+                                                       uint32_t* __restrict__ cnt, uint32_t* __restrict__ dbg)
+{
+    constexpr int NT = 64 * WV;
+    constexpr int kCoopBT = WV;  // tiles per staged batch: one candidate per thread
+    constexpr int CPT = kCoopBT * kTile / NT;
+    __shared__ float scand[2][kCoopBT][D][kTile];  // [buffer][tile][dim][candidate]: lane reads are conflict-free
+    __shared__ uint32_t sidx[2][kCoopBT][kTile];
+    __shared__ uint64_t sneed[WV];
+    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t wave = xcd_block(blockIdx.x, gridDim.x) * WV + w;
+    const uint32_t g0 = wave * QG;
+    // a wave past the queries still takes part in every barrier, with nothing to need
+    const bool active = g0 < q_count;
+    uint32_t qi[QG], kk[QG], c[QG], wi[QG];
+    float me[QG][D], wd[QG], thr[QG];
+    uint32_t p0 = 0;
+    auto uni = [](uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+    auto unf = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        const uint32_t qo = g0 + q;
+        const bool inq = qo < q_count;
+        const uint32_t p = uni(VGPU_DCLAMP(dbg, inq ? (qlist ? qlist[qo] : qo) : 0u, n, DBG_KNN_QUERY));
+        if (q == 0) p0 = p;
+        qi[q] = uni(inq ? VGPU_DCLAMP(dbg, perm[p], n, DBG_KNN_VERTEX) : 0u);
+        const bool live = inq && qi[q] >= 2;  // vertices 0, 1 (start, goal) query nothing (prm.hh:228-233)
+#pragma unroll
+        for (int d = 0; d < D; ++d) me[q][d] = unf(inq ? Vs[(size_t)p * D + d] : 0.0f);
+        kk[q] = uni(live ? min(kq[qi[q]], 64u) : 0u);
+        wd[q] = unf(live ? rq[qi[q]] : -1.0f);
+        wi[q] = 0xFFFFFFFFu;
+        c[q] = 0;
+        thr[q] = (live && kk[q]) ? wd[q] * wd[q] * 1.000001f : -1.0f;
+    }
+    float bd[QG];
+    uint32_t bi[QG];
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        bd[q] = __builtin_inff();
+        bi[q] = 0xFFFFFFFFu;
+    }
+    auto consider = [&](const float* cv, uint32_t cj) {
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+            const float s = sumsq<D>(cv, me[q]);
+            uint64_t m = __builtin_amdgcn_ballot_w64(cj < qi[q] && s <= thr[q]);
+            if (m == 0ull) continue;
+            const float dl = __builtin_sqrtf(s);
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                const float d = bcast(dl, b);
+                const uint32_t j = bcast(cj, b);
+                const bool take = c[q] < kk[q] ? d <= wd[q] : (d < wd[q] || (d == wd[q] && j < wi[q]));
+                if (!take) continue;
+                const uint32_t lt = (d < bd[q] || (d == bd[q] && j < bi[q])) ? 1u : 0u;
+                const float pd = shfl_up1(bd[q]);
+                const uint32_t pi = shfl_up1(bi[q]);
+                const uint32_t plt_raw = shfl_up1(lt);
+                const bool plt = lane > 0 && plt_raw != 0u;
+                bd[q] = lt ? (plt ? pd : d) : bd[q];
+                bi[q] = lt ? (plt ? pi : j) : bi[q];
+                c[q] = min(c[q] + 1u, kk[q]);
+                if (c[q] == kk[q]) {
+                    wd[q] = bcast(bd[q], kk[q] - 1u);
+                    wi[q] = bcast(bi[q], kk[q] - 1u);
+                    thr[q] = wd[q] * wd[q] * 1.000001f;
+                }
+            }
+        }
+    };
+    auto need_box = [&](const float* __restrict__ bx, uint32_t mn) {
+        bool need = false;
+#pragma unroll
+        for (int q = 0; q < QG; ++q) need |= mn < qi[q] && box_lb<D>(bx, me[q]) <= thr[q] * 1.0001f;
+        return need;
+    };
+    // the block-wide OR of every wave's 64-bit mask (two barriers)
+    auto block_or = [&](uint64_t m) {
+        if (lane == 0) sneed[w] = m;
+        __syncthreads();
+        uint64_t r = 0ull;
+#pragma unroll
+        for (int i = 0; i < WV; ++i) r |= sneed[i];
+        __syncthreads();
+        return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r) |
+               ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(r >> 32)) << 32);
+    };
+    // candidate slot e of a batch (tile e / 64 of the batch's list, candidate e % 64): staged by thread
+    // e mod NT; tile lists are fixed-size arrays indexed by compile-time positions only (no scratch)
+    float rv[CPT][D];
+    uint32_t rj[CPT];
+    auto fetch = [&](const uint32_t (&tl)[kCoopBT], int nt) {  // global -> registers
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+            const uint32_t e = threadIdx.x + (uint32_t)k * NT;
+            const uint32_t tb = e / kTile;
+            uint32_t tile = 0xFFFFFFFFu;
+#pragma unroll
+            for (int i = 0; i < kCoopBT; ++i)
+                if (tb == (uint32_t)i && i < nt) tile = tl[i];
+            const bool okt = tile != 0xFFFFFFFFu;
+            const uint32_t cp = (okt ? VGPU_DCLAMP(dbg, tile, T, DBG_KNN_TILE) : 0u) * kTile + (e % kTile);
+            const bool ok = okt && cp < n;
+#pragma unroll
+            for (int d = 0; d < D; ++d) rv[k][d] = ok ? Vs[(size_t)cp * D + d] : 0.0f;
+            rj[k] = ok ? perm[cp] : 0xFFFFFFFFu;  // a missing candidate is never < i
+        }
+    };
+    auto stage = [&](int buf) {  // registers -> LDS
+#pragma unroll
+        for (int k = 0; k < CPT; ++k) {
+            const uint32_t e = threadIdx.x + (uint32_t)k * NT;
+#pragma unroll
+            for (int d = 0; d < D; ++d) scand[buf][e / kTile][d][e % kTile] = rv[k][d];
+            sidx[buf][e / kTile][e % kTile] = rj[k];
+        }
+    };
+    // this wave's tests of a staged batch: only the tiles one of its own queries needs
+    auto test = [&](int buf, const uint32_t (&tl)[kCoopBT], int nt, uint32_t sp, uint64_t mine) {
+#pragma unroll
+        for (int b = 0; b < kCoopBT; ++b) {
+            if (b >= nt) break;
+            if (!((mine >> (tl[b] - sp * kSuper)) & 1ull)) continue;
+            float cv[D];
+#pragma unroll
+            for (int d = 0; d < D; ++d) cv[d] = scand[buf][b][d][lane];
+            consider(cv, sidx[buf][b][lane]);
+        }
+    };
+    // every tile of super-tile sp in the block's union of needs, staged batch by batch (double buffered,
+    // the loop unrolled by two so every buffer and list index is a constant)
+    auto visit_super = [&](uint32_t sp) {
+        sp = VGPU_DCLAMP(dbg, sp, S, DBG_KNN_SUPER);
+        const uint32_t t = sp * kSuper + lane;
+        const bool need = active && t < T && need_box(tbox + (size_t)t * 2 * D, tmin[t]);
+        const uint64_t mine = __builtin_amdgcn_ballot_w64(need);
+        uint64_t m = block_or(mine);
+        uint32_t ta[kCoopBT], tb[kCoopBT];
+        int na = 0, nb = 0;
+        auto take = [&](uint32_t (&tl)[kCoopBT], int& nt) {
+            nt = 0;
+#pragma unroll
+            for (int i = 0; i < kCoopBT; ++i) {
+                tl[i] = 0u;
+                if (m) {
+                    tl[i] = sp * kSuper + (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1ull;
+                    nt = i + 1;
+                }
+            }
+        };
+        take(ta, na);
+        if (!na) return;
+        fetch(ta, na);
+        for (;;) {
+            stage(0);
+            __syncthreads();
+            take(tb, nb);
+            if (nb) fetch(tb, nb);  // in flight while the staged batch is tested
+            test(0, ta, na, sp, mine);
+            __syncthreads();
+            if (!nb) break;
+            stage(1);
+            __syncthreads();
+            take(ta, na);
+            if (na) fetch(ta, na);
+            test(1, tb, nb, sp, mine);
+            __syncthreads();
+            if (!na) break;
+        }
+    };
+    // the block's home super-tile first (its first query's), then the other super-tiles in chunks of 64
+    // outward; a super-tile is visited when some query of the block can take from it
+    const uint32_t home_s = uni(__builtin_amdgcn_readfirstlane(p0) / kTile / kSuper);
+    __shared__ uint32_t shome;
+    if (threadIdx.x == 0) shome = home_s;
+    __syncthreads();
+    const uint32_t bhome = shome;  // wave 0's
+    visit_super(bhome);
+    const uint32_t chunks = (S + 63) / 64, home_c = bhome / 64;
+    for (uint32_t st = 0; st < 2 * chunks; ++st) {
+        const int64_t c64 = (st & 1u) ? (int64_t)home_c - (int64_t)((st + 1) / 2) : (int64_t)home_c + (int64_t)(st / 2);
+        if (c64 < 0 || c64 >= (int64_t)chunks) continue;
+        const uint32_t sp = (uint32_t)c64 * 64 + lane;
+        const bool need = active && sp < S && sp != bhome && need_box(sbox + (size_t)sp * 2 * D, smin[sp]);
+        uint64_t m = block_or(__builtin_amdgcn_ballot_w64(need));
+        if ((uint64_t)c64 == home_c) m &= ~(1ull << (bhome & 63u));  // visited first, never twice
+        while (m) {
+            const uint32_t b = (uint32_t)__builtin_ctzll(m);
+            m &= m - 1ull;
+            visit_super((uint32_t)c64 * 64 + b);
+        }
+    }
+    if (!active) return;
+#pragma unroll
+    for (int q = 0; q < QG; ++q) {
+        if (g0 + q >= q_count) break;
+        const size_t o = VGPU_DCLAMP(dbg, qi[q] - q_first, q_count, DBG_KNN_QUERY);
+        if (lane == 0) cnt[o] = c[q];
+        if (lane < c[q]) {
+            nbr[o * kmax + lane] = bi[q];
+            dist[o * kmax + lane] = bd[q];
+        }
+    }
+}
+
 inline size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct Layout {
@@ -660,6 +887,22 @@ hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, c
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t QG = group >= 8 ? 8 : (group >= 4 ? 4 : (group >= 2 ? 2 : 1));
     const uint64_t waves = (q_count + QG - 1) / QG;
+    // block-cooperative tiles (VAMP_AMD_KNN_COOP: waves per workgroup, 4 or 8; 0 = group_kernel)
+    static const int coop = [] {
+        const char* s = std::getenv("VAMP_AMD_KNN_COOP");
+        return s ? std::atoi(s) : 4;
+    }();
+    if (coop > 0 && QG == 4) {
+        const int WV = coop >= 8 ? 8 : 4;
+        const unsigned cgrid = (unsigned)((waves + WV - 1) / WV);
+        if (WV == 8)
+            hipLaunchKernelGGL((coop_kernel<D, 4, 8>), dim3(cgrid), dim3(512), 0, st, Vs, perm, n, T, S, tbox, tmin, sbox,
+                               smin, ql, q_first, q_count, k, r, kmax, nbr, dist, cnt, dbg);
+        else
+            hipLaunchKernelGGL((coop_kernel<D, 4, 4>), dim3(cgrid), dim3(256), 0, st, Vs, perm, n, T, S, tbox, tmin, sbox,
+                               smin, ql, q_first, q_count, k, r, kmax, nbr, dist, cnt, dbg);
+        return hipGetLastError();
+    }
     const unsigned grid = (unsigned)((waves + kQBlock / 64 - 1) / (kQBlock / 64));
 #define VGPU_KNN_GROUP_LAUNCH(Q)                                                                                      \
     hipLaunchKernelGGL((group_kernel<D, Q>), dim3(grid), dim3(kQBlock), 0, st, Vs, perm, n, T, S, tbox, tmin, sbox, \

@@ -15,17 +15,20 @@
 #include "gen/panda_pair_staged.inc"
 
 #ifndef VGPU_PAIR_BOUND_WAVES
-#define VGPU_PAIR_BOUND_WAVES 5
+#define VGPU_PAIR_BOUND_WAVES 4
 #endif
 // the inter-arm passes' bound kernels over 8-lane rake groups (validate head / tail): both arms' link
 // frames are live at once -- 176 B/lane of scratch at 5 waves/EU, 12 B at 4 (128 VGPRs), none at 3
 // (132); A/B on MI355X (2^20 composite edges, 2 x 2 alternating): 4 waves 10.58-10.68 ms, 3 waves
-// 10.72-10.77 (profiles/r04d_pair_ab.log)
+// 10.72-10.77 (profiles/r04d_pair_ab.log).  Round 5: 3, spill-free (tests/test_kernel_resources.py)
 #ifndef VGPU_PAIR_INTER_BOUND8_WAVES
-#define VGPU_PAIR_INTER_BOUND8_WAVES 4
+#define VGPU_PAIR_INTER_BOUND8_WAVES 3
 #endif
+// inter-arm children: both links' frames plus the held side's sphere centres (up to 30 spheres) -- 136-227
+// VGPRs spilled at 6 waves/EU (80 VGPRs); they run only for the rare groups whose inter-arm bounding pairs
+// overlap, so they get the registers (2 waves/EU, 256 VGPRs) rather than scratch
 #ifndef VGPU_PAIR_INTER_WAVES
-#define VGPU_PAIR_INTER_WAVES 6
+#define VGPU_PAIR_INTER_WAVES 2
 #endif
 
 namespace vgpu {

@@ -4,6 +4,15 @@
 #include "vgpu_panda.hh"
 #include "vgpu_staged.hh"
 
+// One translation unit per part of the source kinds (VGPU_PANDA_PART, compiled in parallel: one TU with every
+// kind took ~18 min): part 0 = configurations + Halton samples (+ the head -> tail bookkeeping kernels),
+// 1 = validate heads, 2 = validate tails, 3 = full-mask tails.  vgpu_api.cpp dispatches a kind to its part.
+#ifndef VGPU_PANDA_PART
+#define VGPU_PANDA_PART 0
+#endif
+#define VGPU_CAT_(a, b) a##b
+#define VGPU_CAT(a, b) VGPU_CAT_(a, b)
+
 // bound kernels: 86 VGPRs when unconstrained (Grp8 sources); at 7 waves/EU (72 VGPRs) they spilled
 // 56 B/lane (~0.95 GB of scratch traffic per validate call), at 5 waves/EU none -- same speed on
 // MI355X (A/B 3.31-3.40 vs 3.32-3.37 ms per 2^20-edge call), so the spill-free budget is the default
@@ -43,6 +52,7 @@ struct PandaR {
 #endif
     using Mask = panda_mask_t;
     static constexpr Mask kEnvChecks = panda_env_check_bits;
+    static constexpr unsigned kSourceKinds = VGPU_PANDA_PART == 0 ? 0x3u : (0x4u << (VGPU_PANDA_PART - 1));
     // children register classes (ChildClasses): VGPRs per check when compiled alone (Grp8, gfx950):
     // most <= 49; 6, 7, 19, 20: 59-65; 15, 21: 90, 105
     static constexpr int kClasses = 3;
@@ -82,6 +92,7 @@ struct PandaR {
     }
 };
 
+#if VGPU_PANDA_PART == 0
 // validate head -> tail: back-step items for edges still valid after block 0
 __global__ __launch_bounds__(kBlock) void tail_counts_kernel(const float* __restrict__ starts,
                                                              const float* __restrict__ goals, size_t n_edges,
@@ -111,9 +122,27 @@ __global__ __launch_bounds__(kBlock) void mask_finish_kernel(size_t n_edges, con
     ok[e] = all;
 }
 
+#endif
+
 }  // namespace vgpu
 
-VGPU_STAGED_EXPORTS(vgpu::PandaR, panda)
+#define VGPU_STAGED_EXPORTS_X(R, NAME) VGPU_STAGED_EXPORTS(R, NAME)  // expands NAME before the pasting
+VGPU_STAGED_EXPORTS_X(vgpu::PandaR, VGPU_CAT(panda_p, VGPU_PANDA_PART))
+
+#ifdef VGPU_HITSTATS
+// development statistics of the VGPU_HITSTATS variant: this part's counters
+extern "C" int VGPU_CAT(VGPU_CAT(vgpu_panda_p, VGPU_PANDA_PART), _hitstats)(unsigned int* out, int reset)
+{
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vgpu::vgpu_hitstats), sizeof(vgpu::vgpu_hitstats)) != hipSuccess) return -2;
+    if (reset) {
+        static const unsigned int zero[5][64][2] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(vgpu::vgpu_hitstats), zero, sizeof(zero)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
+
+#if VGPU_PANDA_PART == 0
 
 extern "C" hipError_t vgpu_launch_mask_finish(size_t n_edges, const uint32_t* off, uint8_t* ok, uint8_t* block_ok,
                                                hipStream_t st)
@@ -136,15 +165,22 @@ extern "C" hipError_t vgpu_launch_tail_counts(const float* starts, const float* 
 }
 
 #ifdef VGPU_HITSTATS
+extern "C" int vgpu_panda_p1_hitstats(unsigned int*, int);
+extern "C" int vgpu_panda_p2_hitstats(unsigned int*, int);
+extern "C" int vgpu_panda_p3_hitstats(unsigned int*, int);
 // development statistics of the VGPU_HITSTATS variant: out[5][64][2] (items, items with a children hit)
-// per (source kind, check) since the last call; reset = 1 zeroes them
+// per (source kind, check) since the last call, summed over the parts; reset = 1 zeroes them
 extern "C" int vgpu_panda_hitstats(unsigned int* out, int reset)
 {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(vgpu::vgpu_hitstats), sizeof(vgpu::vgpu_hitstats)) != hipSuccess) return -2;
-    if (reset) {
-        static const unsigned int zero[5][64][2] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(vgpu::vgpu_hitstats), zero, sizeof(zero)) != hipSuccess) return -2;
+    static unsigned int part[5][64][2];
+    int (*fn[4])(unsigned int*, int) = {vgpu_panda_p0_hitstats, vgpu_panda_p1_hitstats, vgpu_panda_p2_hitstats,
+                                        vgpu_panda_p3_hitstats};
+    for (int i = 0; i < 5 * 64 * 2; ++i) out[i] = 0;
+    for (auto f : fn) {
+        if (int rc = f(&part[0][0][0], reset)) return rc;
+        for (int i = 0; i < 5 * 64 * 2; ++i) out[i] += (&part[0][0][0])[i];
     }
     return 0;
 }
+#endif
 #endif

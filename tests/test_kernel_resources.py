@@ -27,7 +27,8 @@ def staged(robot, ext, kinds=r"\w+"):
     R = re.escape(robot)
     e = "true" if ext else "false"
     src = rf"vgpu::Src(?:{kinds})<{R} ?>"
-    return [rf"vgpu::bound_kernel<{R}, {src}, {e}>", rf"vgpu::children_kernel<{R}, {src}, {e}, \d>"] + \
+    # bound kernels: <R, Src, EXT, FUSE>; the fused-lead instantiations (FUSE = true, an A/B knob) are not listed
+    return [rf"vgpu::bound_kernel<{R}, {src}, {e}, false>", rf"vgpu::children_kernel<{R}, {src}, {e}, \d>"] + \
         ([rf"vgpu::lead_kernel<{R}, {src} ?>"] if not ext else [])
 
 

@@ -832,27 +832,7 @@ class RobotGen:
             E.raw(f"const uint32_t gate = Grp::or_bits({self.name}_gate(q{d0}, q{d1}));  // per group: checks that can fire")
             gated = {c: b for b, c in enumerate(gate["checks"])}
         for c, o in enumerate(order):
-            kind, test, ck = self.bound_test(fr, o)
-            mids = self.mids_of(ck, kind) if (MIDS and c not in gated) else None
-            if mids:
-                self.emit_mid_check(E, fr, kind, test, ck, mids, c, one)
-            elif kind == "env":  # the check's bit is its deferred-query tag (vgpu_device.hh capt_defer_*)
-                E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c}))) mask |= {one} << {c};")
-            elif c in gated:
-                E.raw(f"if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c};")
-            elif kind == "self" and ck.get("never_fires") and not TY["cpu"]:
-                # tools/prove_self_checks.py: no child pair can fire while these joints stay in the proven box;
-                # a group with every lane inside it gets no bit (the bounding test is not even evaluated)
-                def inward(v, up):  # the float32 bound on the box's side of v
-                    f = F(v)
-                    if (up and float(f) < v) or (not up and float(f) > v):
-                        f = np.nextafter(f, F(np.inf) if up else F(-np.inf))
-                    return flit(f)
-                inside = " && ".join(f"q{d} >= {inward(lo, True)} && q{d} <= {inward(hi, False)}"
-                                     for d, lo, hi in zip(ck["never_dofs"], ck["never_lo"], ck["never_hi"]))
-                E.raw(f"if (Grp::any(!({inside})) && Grp::any({test})) mask |= {one} << {c};  // proven silent inside")
-            else:
-                E.raw(f"if (Grp::any({test})) mask |= {one} << {c};")
+            self.emit_bound_check(E, fr, c, o, gated, one, mids_on=bool(MIDS))
         E.raw("return mask;")
         env_bits = sum(1 << c for c, o in enumerate(order) if o["kind"] == "env")
         out = [f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
@@ -872,7 +852,32 @@ class RobotGen:
                                   [f"// staged lead pass: check {c} ({LEAD[self.name]} vs the environment) alone, "
                                    "monolithic -- true when it passes; a group leaves at its first child hit"],
                                   early=True)]
+
         return "\n".join(out)
+
+    def emit_bound_check(self, E, fr, c, o, gated, one, mids_on):
+        """check c's bounding test in the staged bound stage: bit c of mask set when it fires for the group"""
+        kind, test, ck = self.bound_test(fr, o)
+        mids = self.mids_of(ck, kind) if (mids_on and c not in gated) else None
+        if mids:
+            self.emit_mid_check(E, fr, kind, test, ck, mids, c, one)
+        elif kind == "env":  # the check's bit is its deferred-query tag (vgpu_device.hh capt_defer_*)
+            E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c}))) mask |= {one} << {c};")
+        elif c in gated:
+            E.raw(f"if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c};")
+        elif kind == "self" and ck.get("never_fires") and not TY["cpu"]:
+            # tools/prove_self_checks.py: no child pair can fire while these joints stay in the proven box;
+            # a group with every lane inside it gets no bit (the bounding test is not even evaluated)
+            def inward(v, up):  # the float32 bound on the box's side of v
+                f = F(v)
+                if (up and float(f) < v) or (not up and float(f) > v):
+                    f = np.nextafter(f, F(np.inf) if up else F(-np.inf))
+                return flit(f)
+            inside = " && ".join(f"q{d} >= {inward(lo, True)} && q{d} <= {inward(hi, False)}"
+                                 for d, lo, hi in zip(ck["never_dofs"], ck["never_lo"], ck["never_hi"]))
+            E.raw(f"if (Grp::any(!({inside})) && Grp::any({test})) mask |= {one} << {c};  // proven silent inside")
+        else:
+            E.raw(f"if (Grp::any({test})) mask |= {one} << {c};")
 
     def side_spheres(self, ck, side):
         """sphere indices of one side of a self check's child pairs"""

@@ -55,6 +55,9 @@ def main():
         rec = {"dispatches_per_call": kern[name]["dispatches"] / calls, "ms_per_call": kern[name]["ns"] / calls / 1e6}
         for c, v in ctr[name].items():
             rec[c] = v / calls
+        h, m = rec.get("TCC_HIT_sum"), rec.get("TCC_MISS_sum")
+        if h is not None and m is not None and h + m > 0:
+            rec["L2_hit_rate"] = h / (h + m)  # MI355X_MICROARCH.md "L2 (per XCD)"
         kernels[name] = rec
         tot["ms"] += rec["ms_per_call"]
         for c in ("SQ_INSTS_VALU", "SQ_INSTS_VALU_ADD_F32", "SQ_INSTS_VALU_MUL_F32", "SQ_INSTS_VALU_FMA_F32",
