@@ -96,7 +96,8 @@ VCPU_INLINE V sphere_sphere(V ax, V ay, V az, V ar, V bx, V by, V bz, V br)
 
 // ---- environment view: the same blob layout as the device buffer (vgpu_device.hh EnvView) ----
 enum : int { OBS_SPHERE = 0, OBS_CAPSULE = 1, OBS_ZCAPSULE = 2, OBS_CUBOID = 3, OBS_ZCUBOID = 4, OBS_TYPES = 5 };
-constexpr int kObsStride[OBS_TYPES] = {8, 16, 16, 16, 16};
+constexpr int kObsStride[OBS_TYPES] = {8, 16, 16, 20, 20};  // = vgpu_device.hh (bounding spheres unused here)
+constexpr int kSphereBlock = 16;  // spheres: pair blocks md_a md_b x_a x_b y_a y_b z_a z_b r_a r_b (vgpu_device.hh)
 constexpr int kAttHdr = 8;
 constexpr int kExtHdr = 32;  // = vgpu_device.hh (the host view leaves the device-only cell grid fields 0)
 enum : int { HF_X = 0, HF_Y, HF_Z, HF_XS, HF_YS, HF_ZS, HF_XD, HF_YD, HF_XD2, HF_YD2, HF_OFF, HF_CELLS };
@@ -200,7 +201,15 @@ __attribute__((noinline)) static VB env_bits(const EnvView& env, V x, V y, V z, 
             if (signmask(t)) return acc | VB(t);                                     \
         }                                                                            \
     }
-    VCPU_SCAN(OBS_SPHERE, sphere_sphere(o[1], o[2], o[3], o[4], x, y, z, R))  // sphere_sphere.hh:10-22
+    {  // sphere_sphere.hh:10-22; record j is half j & 1 of pair block j / 2
+        const float* s = env.obs[OBS_SPHERE];
+        for (int j = 0; j < env.n[OBS_SPHERE]; ++j) {
+            const float* o = s + (j >> 1) * kSphereBlock + (j & 1);
+            if (signmask(V(o[0]) - me) == 0) break;
+            const V t = sphere_sphere(o[2], o[4], o[6], o[8], x, y, z, R);
+            if (signmask(t)) return acc | VB(t);
+        }
+    }
     VCPU_SCAN(OBS_CAPSULE, ([&] {                                              // sphere_capsule.hh:9-22
                   const V dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
                   const V cdf = vmin(vmax(dot * o[8], 0.0f), 1.0f);

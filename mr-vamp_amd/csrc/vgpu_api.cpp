@@ -902,6 +902,49 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
     while (blob.size() % 16) blob.push_back(0.0f);
 }
 
+// The bounding sphere of a capsule / cuboid record (vgpu_device.hh kObsBound): centre and a radius R such
+// that the reference's test for a sphere (p, r) can only come out negative when |p - centre| <= r + R.
+// Capsule: the segment's midpoint, |v| / 2 + radius (the closest point the test picks lies on the segment,
+// sphere_capsule.hh:9-22; the z-capsule's test reads only the z component of v, :30-43).  Cuboid: the centre
+// and the half diagonal |(r1, r2, r3)| -- the box distance is at least the centre distance less the half
+// diagonal when the axes are orthonormal (sphere_cuboid.hh:9-52); other axes get R = +inf (never skipped).
+// R is widened by 1e-5 of the record's scale (+ 1e-5) -- orders of magnitude above the float rounding of
+// either test -- so the prefilter never skips a record whose test would fire.
+static void obstacle_bound(int type, const float* row, float* out)
+{
+    double c[3], R;
+    if (type == OBS_CAPSULE || type == OBS_ZCAPSULE) {
+        const double vx = type == OBS_CAPSULE ? row[3] : 0.0, vy = type == OBS_CAPSULE ? row[4] : 0.0, vz = row[5];
+        c[0] = row[0] + 0.5 * vx;
+        c[1] = row[1] + 0.5 * vy;
+        c[2] = row[2] + 0.5 * vz;
+        R = 0.5 * std::sqrt(vx * vx + vy * vy + vz * vz) + std::fabs((double)row[6]);
+    } else {
+        for (int i = 0; i < 3; ++i) c[i] = row[i];
+        double ax[3][3];
+        for (int k = 0; k < 3; ++k)
+            for (int i = 0; i < 3; ++i) ax[k][i] = row[3 + 3 * k + i];
+        if (type == OBS_ZCUBOID) {  // the test uses a1, a2 in the xy plane and the z axis
+            ax[0][2] = ax[1][2] = 0.0;
+            ax[2][0] = ax[2][1] = 0.0;
+            ax[2][2] = 1.0;
+        }
+        bool ortho = true;
+        for (int a = 0; a < 3; ++a)
+            for (int b = 0; b < 3; ++b) {
+                const double d = ax[a][0] * ax[b][0] + ax[a][1] * ax[b][1] + ax[a][2] * ax[b][2];
+                ortho = ortho && std::fabs(d - (a == b ? 1.0 : 0.0)) <= 1e-6;
+            }
+        const double h0 = row[12], h1 = row[13], h2 = row[14];
+        R = ortho ? std::sqrt(h0 * h0 + h1 * h1 + h2 * h2) : HUGE_VAL;
+    }
+    const double scale = std::fabs(c[0]) + std::fabs(c[1]) + std::fabs(c[2]) + R;
+    R += 1e-5 * (1.0 + scale);
+    for (int i = 0; i < 3; ++i) out[i] = (float)c[i];
+    out[3] = std::isfinite(R) && std::isfinite(scale) && R < 3e38 ? std::nextafter((float)R, HUGE_VALF) : HUGE_VALF;
+    if (!(std::isfinite(out[0]) && std::isfinite(out[1]) && std::isfinite(out[2]))) out[3] = HUGE_VALF;
+}
+
 // The tail section as its own vector; its offsets are recorded relative to the blob, starting at base.
 static void build_tail(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& tail, size_t base)
 {
@@ -915,11 +958,30 @@ static void build_tail(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& tai
         const int S = kObsStride[type];
         L.off[type] = base + tail.size();
         L.cnt[type] = (int)v.size();
+        if (type == OBS_SPHERE) {  // pair blocks (vgpu_device.hh scan_spheres), then sentinel blocks
+            const size_t blocks = (v.size() + kObsPad + 1) / 2;
+            for (size_t b = 0; b < blocks; ++b) {
+                const size_t at = tail.size();
+                tail.resize(at + kSphereBlock, 0.0f);
+                for (int h = 0; h < 2; ++h) {
+                    const size_t j = 2 * b + h;
+                    if (j < v.size()) {
+                        tail[at + h] = v[j][np];  // min_distance
+                        for (int i = 0; i < np; ++i) tail[at + 2 + 2 * i + h] = v[j][i];
+                    } else {
+                        tail[at + h] = __builtin_inff();
+                    }
+                }
+            }
+            while (tail.size() % 16) tail.push_back(0.0f);
+            return;
+        }
         for (auto& row : v) {
             const size_t at = tail.size();
             tail.resize(at + S, 0.0f);
             tail[at] = row[np];  // min_distance is the last field of the host row
             for (int i = 0; i < np; ++i) tail[at + 1 + i] = row[i];
+            if (kObsBound[type] >= 0) obstacle_bound(type, row.data(), &tail[at + kObsBound[type]]);
         }
         for (int k = 0; k < kObsPad; ++k) {
             const size_t at = tail.size();

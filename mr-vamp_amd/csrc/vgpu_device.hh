@@ -211,11 +211,15 @@ __device__ __forceinline__ float halton_coord(uint32_t idx, uint32_t b)
 // ascending by min_distance (environment.hh:40-66) and terminated by kObsPad sentinel records
 // whose min_distance is +inf (never evaluated; lets the loops prefetch past the end).
 // Records (float32, field 0 = min_distance):
-//   sphere   stride  8: md x y z r
-//   capsule  stride 16: md x1 y1 z1 xv yv zv r rdv            (z-capsule: same)
-//   cuboid   stride 16: md x y z a1x a1y a1z a2x a2y a2z a3x a3y a3z r1 r2 r3   (z-cuboid: same)
+//   sphere   pair blocks of 16: md_a md_b x_a x_b y_a y_b z_a z_b r_a r_b (records 2k, 2k + 1; scan_spheres)
+//   capsule  stride 16: md x1 y1 z1 xv yv zv r rdv | bx by bz bR            (z-capsule: same)
+//   cuboid   stride 20: md x y z a1x a1y a1z a2x a2y a2z a3x a3y a3z r1 r2 r3 | bx by bz bR   (z-cuboid: same)
+// (bx by bz bR: the record's bounding sphere, vgpu_api.cpp obstacle_bound -- not part of the reference's record;
+// scan_type skips a record for a wave none of whose live lanes' spheres reach it)
 enum : int { OBS_SPHERE = 0, OBS_CAPSULE = 1, OBS_ZCAPSULE = 2, OBS_CUBOID = 3, OBS_ZCUBOID = 4, OBS_TYPES = 5 };
-constexpr int kObsStride[OBS_TYPES] = {8, 16, 16, 16, 16};
+constexpr int kObsStride[OBS_TYPES] = {8, 16, 16, 20, 20};  // spheres: 16 floats per PAIR of records
+constexpr int kSphereBlock = 16;
+constexpr int kObsBound[OBS_TYPES] = {-1, 9, 9, 16, 16};  // first bounding-sphere field (-1: none)
 constexpr int kObsPad = 8;  // >= 2 * VGPU_SCAN_UNROLL - 1 (the loop's prefetch reach)
 
 struct EnvView {
@@ -326,14 +330,22 @@ struct ObsRec {
 // obstacle records are read through the scalar cache (address space 4, s_load): every lane of a wave reads
 // the same record, one s_load into SGPRs the tests use directly (a per-workgroup LDS copy measured 7-11 %
 // slower in round 3: a ds_read broadcast per field plus the copy and barrier)
+// Records with a bounding sphere (kObsBound) are tested only when some live lane's sphere (x, y, z, r)
+// reaches it: |p - b| <= r + bR is implied by the test firing (obstacle_bound), so a wave-uniform skip of
+// the others leaves acc bit-identical.  VGPU_OBS_PREFILTER=0 restores the unconditional tests (A/B).
+#ifndef VGPU_OBS_PREFILTER
+#define VGPU_OBS_PREFILTER 1
+#endif
 template <int TYPE, class TestFn>
-__device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float emax, uint32_t acc, TestFn test)
+__device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float emax, uint32_t acc, TestFn test,
+                                              float x, float y, float z, float r)
 {
     // The lane state is kept as VALU bit masks (acc: sign bit = hit) instead of per-lane bools:
     // combining divergent bools costs a 64-bit SALU op each, and the scalar unit -- shared by
     // the waves of a SIMD -- was the busiest pipe of these kernels.
     constexpr int S = kObsStride[TYPE];
     constexpr int U = VGPU_SCAN_UNROLL;
+    constexpr int B = VGPU_OBS_PREFILTER ? kObsBound[TYPE] : -1;
     using Rec = ObsRec<S>;  // one record: a single s_load per field group
     const VGPU_CONST Rec* p = (const VGPU_CONST Rec*)o;
     float md[U];
@@ -354,11 +366,76 @@ __device__ __forceinline__ uint32_t scan_type(const VGPU_CONST float* o, float e
         for (int u = 0; u < U; ++u) nmd[u] = p[U + u].v[0];  // prefetch (sentinel-padded)
         uint32_t hit = 0u;
 #pragma unroll
-        for (int u = 0; u < U; ++u) hit |= __float_as_uint(test(p[u].v)) & live[u];
+        for (int u = 0; u < U; ++u) {
+            if constexpr (B >= 0) {
+                const float dx = x - p[u].v[B], dy = y - p[u].v[B + 1], dz = z - p[u].v[B + 2];
+                const float lim = r + p[u].v[B + 3];
+                // NaN distances count as near (the exact test decides them)
+                uint32_t near = (dot3(dx, dy, dz, dx, dy, dz) > lim * lim) ? 0u : live[u] & ~acc;
+                __asm__("" : "+v"(near));
+                if (__builtin_amdgcn_ballot_w64((int)near < 0) != 0) hit |= __float_as_uint(test(p[u].v)) & live[u];
+            } else {
+                hit |= __float_as_uint(test(p[u].v)) & live[u];
+            }
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u) md[u] = nmd[u];
         acc |= hit;
         p += U;
+    }
+    return acc;
+}
+
+// Spheres, two records per block and per loop trip: one s_load brings both records' fields.  The two tests
+// are sphere_sphere's operations in its order (bit-identical values).  VGPU_SPHERE_PACKED=1 runs them as
+// packed FP32 (v_pk_add / v_pk_mul / v_pk_fma_f32 on the block's SGPR pairs: 7 VALU instructions for two
+// records instead of 14) -- measured SLOWER on MI355X (set B 2.29-2.31 vs 2.22-2.25 ms unpacked,
+// profiles/r05g_panda_ab.log): a packed FP32 instruction costs the issue of two (MI355X_MICROARCH.md), and
+// the duplicated lane operands cost VGPRs.
+typedef float f2v __attribute__((ext_vector_type(2)));
+struct SphereBlk {
+    f2v md, x, y, z, r, pad[3];
+};
+static_assert(sizeof(SphereBlk) == kSphereBlock * 4, "sphere block layout");
+#ifndef VGPU_SPHERE_PACKED
+#define VGPU_SPHERE_PACKED 0
+#endif
+__device__ __forceinline__ uint32_t scan_spheres(const VGPU_CONST float* o, float emax, uint32_t acc, float x, float y,
+                                                 float z, float r)
+{
+    const VGPU_CONST SphereBlk* p = (const VGPU_CONST SphereBlk*)o;
+    f2v md = p->md;
+    if constexpr (VGPU_SPHERE_PACKED) {
+        const f2v X = {x, x}, Y = {y, y}, Z = {z, z}, R = {r, r};
+        for (;;) {
+            const uint32_t la = (md.x < emax) ? 0xFFFFFFFFu : 0u, lb = (md.y < emax) ? 0xFFFFFFFFu : 0u;
+            uint32_t pend = la & ~acc;  // sorted: lb implies la
+            __asm__("" : "+v"(pend));
+            if (__builtin_amdgcn_ballot_w64((int)pend < 0) == 0) break;
+            const f2v nmd = p[1].md;  // prefetch (sentinel-padded)
+            const f2v xs = p->x - X, ys = p->y - Y, zs = p->z - Z, rs = p->r + R;
+            f2v d = ys * ys;  // sphere_sphere: fma(-rs, rs, fma(xs, xs, fma(zs, zs, ys * ys)))
+            d = __builtin_elementwise_fma(zs, zs, d);
+            d = __builtin_elementwise_fma(xs, xs, d);
+            d = __builtin_elementwise_fma(-rs, rs, d);
+            acc |= (__float_as_uint(d.x) & la) | (__float_as_uint(d.y) & lb);
+            md = nmd;
+            ++p;
+        }
+    } else {
+        for (;;) {
+            const uint32_t la = (md.x < emax) ? 0xFFFFFFFFu : 0u, lb = (md.y < emax) ? 0xFFFFFFFFu : 0u;
+            uint32_t pend = la & ~acc;
+            __asm__("" : "+v"(pend));
+            if (__builtin_amdgcn_ballot_w64((int)pend < 0) == 0) break;
+            const f2v nmd = p[1].md;
+            const f2v bx = p->x, by = p->y, bz = p->z, br = p->r;
+            const uint32_t ha = __float_as_uint(sphere_sphere(bx.x, by.x, bz.x, br.x, x, y, z, r));
+            const uint32_t hb = __float_as_uint(sphere_sphere(bx.y, by.y, bz.y, br.y, x, y, z, r));
+            acc |= (ha & la) | (hb & lb);
+            md = nmd;
+            ++p;
+        }
     }
     return acc;
 }
@@ -627,9 +704,10 @@ __device__ __forceinline__ uint64_t capt_defer_finish(const VGPU_CONST float* pc
 }
 
 template <int TYPE, class TestFn>
-__device__ __forceinline__ uint32_t scan_env_type(const EnvView& env, float emax, uint32_t acc, TestFn test)
+__device__ __forceinline__ uint32_t scan_env_type(const EnvView& env, float emax, uint32_t acc, TestFn test, float x,
+                                                  float y, float z, float r)
 {
-    return scan_type<TYPE>(env.obs[TYPE], emax, acc, test);
+    return scan_type<TYPE>(env.obs[TYPE], emax, acc, test, x, y, z, r);
 }
 
 // Conservative environment test of a mid-level sphere (tools/gen_kernels.py --mids): sign bit set when the
@@ -647,10 +725,7 @@ __device__ __forceinline__ uint32_t mid_env_bits(const EnvView& env, float x, fl
     if (me != me) me = __builtin_inff();
     const float emax = Grp::max(me);
     const float rsq = r * r;
-    if (env.n[OBS_SPHERE])
-        acc = scan_env_type<OBS_SPHERE>(env, emax, acc, [&](const auto* o) {
-            return sphere_sphere(o[1], o[2], o[3], o[4], x, y, z, r);
-        });
+    if (env.n[OBS_SPHERE]) acc = scan_spheres(env.obs[OBS_SPHERE], emax, acc, x, y, z, r);
     if (env.n[OBS_CAPSULE])
         acc = scan_env_type<OBS_CAPSULE>(env, emax, acc, [&](const auto* o) {
             const float dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
@@ -661,7 +736,7 @@ __device__ __forceinline__ uint32_t mid_env_bits(const EnvView& env, float x, fl
             const float xs = x - px, ys = y - py, zs = z - pz;
             const float rs = r + o[7];
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
-        });
+        }, x, y, z, r);
     if (env.n[OBS_ZCAPSULE])
         acc = scan_env_type<OBS_ZCAPSULE>(env, emax, acc, [&](const auto* o) {
             const float dot = (z - o[3]) * o[6];
@@ -670,7 +745,7 @@ __device__ __forceinline__ uint32_t mid_env_bits(const EnvView& env, float x, fl
             const float xs = x - o[1], ys = y - o[2], zs = z - pz;
             const float rs = r + o[7];
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
-        });
+        }, x, y, z, r);
     if (env.n[OBS_CUBOID])
         acc = scan_env_type<OBS_CUBOID>(env, emax, acc, [&](const auto* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
@@ -678,7 +753,7 @@ __device__ __forceinline__ uint32_t mid_env_bits(const EnvView& env, float x, fl
             const float a2 = max0(__builtin_fabsf(dot3(o[7], o[8], o[9], xs, ys, zs)) - o[14]);
             const float a3 = max0(__builtin_fabsf(dot3(o[10], o[11], o[12], xs, ys, zs)) - o[15]);
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
-        });
+        }, x, y, z, r);
     if (env.n[OBS_ZCUBOID])
         acc = scan_env_type<OBS_ZCUBOID>(env, emax, acc, [&](const auto* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
@@ -686,7 +761,7 @@ __device__ __forceinline__ uint32_t mid_env_bits(const EnvView& env, float x, fl
             const float a2 = max0(__builtin_fabsf(dot2(o[7], o[8], xs, ys)) - o[14]);
             const float a3 = max0(__builtin_fabsf(zs) - o[15]);
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
-        });
+        }, x, y, z, r);
     return acc;
 }
 
@@ -704,10 +779,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
     const float emax = Grp::max(me);
     const float rsq = r * r;
 
-    if (env.n[OBS_SPHERE])  // sphere_sphere.hh:10-22
-        acc = scan_env_type<OBS_SPHERE>(env, emax, acc, [&](const auto* o) {
-            return sphere_sphere(o[1], o[2], o[3], o[4], x, y, z, r);
-        });
+    if (env.n[OBS_SPHERE]) acc = scan_spheres(env.obs[OBS_SPHERE], emax, acc, x, y, z, r);  // sphere_sphere.hh:10-22
     if (env.n[OBS_CAPSULE])  // sphere_capsule.hh:9-22
         acc = scan_env_type<OBS_CAPSULE>(env, emax, acc, [&](const auto* o) {
             const float dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
@@ -718,7 +790,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             const float xs = x - px, ys = y - py, zs = z - pz;
             const float rs = r + o[7];
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
-        });
+        }, x, y, z, r);
     if (env.n[OBS_ZCAPSULE])  // sphere_capsule.hh:30-43
         acc = scan_env_type<OBS_ZCAPSULE>(env, emax, acc, [&](const auto* o) {
             const float dot = (z - o[3]) * o[6];
@@ -727,7 +799,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             const float xs = x - o[1], ys = y - o[2], zs = z - pz;
             const float rs = r + o[7];
             return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
-        });
+        }, x, y, z, r);
     if (env.n[OBS_CUBOID])  // sphere_cuboid.hh:9-27
         acc = scan_env_type<OBS_CUBOID>(env, emax, acc, [&](const auto* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
@@ -735,7 +807,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             const float a2 = max0(__builtin_fabsf(dot3(o[7], o[8], o[9], xs, ys, zs)) - o[14]);
             const float a3 = max0(__builtin_fabsf(dot3(o[10], o[11], o[12], xs, ys, zs)) - o[15]);
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
-        });
+        }, x, y, z, r);
     if (env.n[OBS_ZCUBOID])  // sphere_cuboid.hh:35-52
         acc = scan_env_type<OBS_ZCUBOID>(env, emax, acc, [&](const auto* o) {
             const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
@@ -743,7 +815,7 @@ __device__ __forceinline__ uint32_t env_bits(const EnvView& env, float x, float 
             const float a2 = max0(__builtin_fabsf(dot2(o[7], o[8], xs, ys)) - o[14]);
             const float a3 = max0(__builtin_fabsf(zs) - o[15]);
             return dot3(a1, a2, a3, a1, a2, a3) - rsq;
-        });
+        }, x, y, z, r);
     if constexpr (EXT) {
         bool hit = (acc >> 31) != 0u;
         for (int i = 0; i < env.n_hf; ++i)

@@ -26,13 +26,17 @@
 // children register classes (ChildClasses, vgpu_staged.hh) from the VGPRs each check's children kernel needs
 // compiled alone (tools/probe_children_vgprs.py, gfx950, validate tails): <= 56 for 48 checks; 60-66 for
 // checks 9, 10, 17, 20, 24, 26, 27, 33, 42, 48, 51, 56, 59; 73 for check 8; 90 for check 23.  Each class runs
-// at the occupancy whose budget holds its largest check with headroom (64 / 72 / 80 / 96 VGPRs): no scratch
-// (round 4's three classes at 64 / 72 / 96 spilled 30-60 VGPRs in classes 0 and 1)
+// at an occupancy whose budget holds it in the full kernel -- which needs more than the check compiled alone:
+// at 64 / 72 VGPRs classes 0 and 1 still spilled 4-63 VGPRs, at 96 / 128 (5 / 4 waves) none do (at 80 the
+// validate-head kernel of class 0 still spilled 3; tests/test_kernel_resources.py).  A/B on MI355X
+// (profiles/r05e_ab.log: 8/7 vs 6/5 vs 6/4 waves): edge stage 2.68M vertices 777 / 783 / 784 ms, validate
+// 1.30 / 1.29 / 1.31 ms -- within a percent, and no scratch traffic.  With point clouds (EXT) classes 0 and 1
+// need one wave/EU less again (kExtClassWaves)
 #ifndef VGPU_FETCH_CLASS0_WAVES
-#define VGPU_FETCH_CLASS0_WAVES 8
+#define VGPU_FETCH_CLASS0_WAVES 5
 #endif
 #ifndef VGPU_FETCH_CLASS1_WAVES
-#define VGPU_FETCH_CLASS1_WAVES 7
+#define VGPU_FETCH_CLASS1_WAVES 4
 #endif
 #ifndef VGPU_FETCH_CLASS2_WAVES
 #define VGPU_FETCH_CLASS2_WAVES 6
@@ -49,6 +53,7 @@ struct FetchR {
     static constexpr int kChecks = fetch_n_checks;
     static constexpr int kWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
     static constexpr int kBoundWaves8 = VGPU_FETCH_BOUND8_WAVES;
+    static constexpr int kExtBoundWaves = 3;  // point-cloud bound kernels (vgpu_staged.hh BoundWavesE)
     static constexpr int kChildWavesPerEU = VGPU_FETCH_STAGED_WAVES_PER_EU;
     using Mask = fetch_mask_t;
     static constexpr Mask kEnvChecks = fetch_env_check_bits;
@@ -57,6 +62,7 @@ struct FetchR {
     static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 0, 0, 2, 1, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 3, 1, 0, 1, 1, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 1, 0, 0, 0};
     static constexpr int kClassWaves[kClasses] = {VGPU_FETCH_CLASS0_WAVES, VGPU_FETCH_CLASS1_WAVES,
                                                   VGPU_FETCH_CLASS2_WAVES, VGPU_FETCH_CLASS3_WAVES};
+    static constexpr int kExtClassWaves[kClasses] = {4, 3, 5, 5};
     __device__ static __forceinline__ void sample(uint64_t k, float v[8]) { sample_d<8>(k, fetch_s_m, fetch_s_a, v); }
     __device__ static __forceinline__ void head(const float* s, const float* g, int lane, float v[8])
     {

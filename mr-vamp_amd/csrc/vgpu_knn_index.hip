@@ -173,11 +173,22 @@ __global__ __launch_bounds__(256) void key_kernel(const float* __restrict__ V, u
     id[i] = i;
 }
 
-// one wave per tile: sorted coordinates, the box and the smallest vertex index
+// Candidate codes: each tile's coordinates quantised to 8 bits per dimension against the tile's own box,
+// x' = fma(code, step, lo) with step = (hi - lo) / 255 -- D bytes per candidate instead of 4 D + 4, read for
+// every candidate of a visited tile; the exact coordinates and vertex index are read only for the candidates
+// whose coded distance can pass (group_kernel QC).  The tile header holds step[D] and delta, an upper bound of
+// |x - x'| over the tile's candidates measured from the decoded values themselves (the same fma as the
+// query side), so |d(q, x) - d(q, x')| <= delta exactly; the prefilter widens it further for the float
+// rounding of both distance sums.
+template <int D>
+constexpr int code_words() { return (D + 3) / 4; }
+
+// one wave per tile: sorted coordinates, the box and the smallest vertex index (+ the codes)
 template <int D>
 __global__ __launch_bounds__(64) void tile_kernel(const float* __restrict__ V, const uint32_t* __restrict__ perm,
                                                   uint32_t n, float* __restrict__ Vs, float* __restrict__ tbox,
-                                                  uint32_t* __restrict__ tmin)
+                                                  uint32_t* __restrict__ tmin, uint32_t* __restrict__ qc,
+                                                  float* __restrict__ qh)
 {
     const uint32_t t = blockIdx.x;
     const uint32_t p = t * kTile + threadIdx.x;
@@ -199,6 +210,34 @@ __global__ __launch_bounds__(64) void tile_kernel(const float* __restrict__ V, c
             tbox[(size_t)t * 2 * D + D + d] = hi[d];
         }
         tmin[t] = jm;
+    }
+    if (!qc) return;  // codes only for the coded group queries
+    constexpr int W = code_words<D>();
+    uint32_t word[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) word[w] = 0u;
+    float e2 = 0.0f;
+    float step[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float x = ok ? Vs[(size_t)p * D + d] : lo[d];
+        float st = (hi[d] - lo[d]) * (1.0f / 255.0f);
+        if (!(st > 0.0f && st < __builtin_inff())) st = 0.0f;
+        step[d] = st;
+        const float f = st > 0.0f ? fminf(fmaxf(__builtin_rintf((x - lo[d]) / st), 0.0f), 255.0f) : 0.0f;
+        const uint32_t code = (uint32_t)f;
+        word[d / 4] |= code << (8 * (d % 4));
+        const float err = wave_max(ok ? __builtin_fabsf(x - __builtin_fmaf((float)code, st, lo[d])) : 0.0f);
+        e2 = __builtin_fmaf(err, err, e2);
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) qc[((size_t)t * W + w) * kTile + threadIdx.x] = word[w];
+    if (threadIdx.x == 0) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) qh[(size_t)t * (D + 1) + d] = step[d];
+        float delta = __builtin_sqrtf(e2) * 1.0001f;  // the sum's and sqrt's rounding (a few ulp) covered
+        if (!(delta < __builtin_inff())) delta = __builtin_inff();  // NaN / inf coordinates: no prefilter
+        qh[(size_t)t * (D + 1) + D] = delta;
     }
 }
 
@@ -402,13 +441,19 @@ __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb)
     return x * q + (x < r ? x : r) + (b >> 3);
 }
 
-template <int D, int QG>
+// QC: candidates are first tested on their codes (tile_kernel) and only those that can pass for some query of
+// the group read their exact coordinates and index -- the exact test and admission below are unchanged, so the
+// lists are the same; the tiles' bytes per visit drop from 36 to D per candidate.  The codes of the next tile
+// are in flight while the current one's exact candidates are tested.
+template <int D, int QG, bool QC>
 __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict__ Vs, const uint32_t* __restrict__ perm,
                                                         uint32_t n, uint32_t T, uint32_t S,
                                                         const float* __restrict__ tbox,
                                                         const uint32_t* __restrict__ tmin,
                                                         const float* __restrict__ sbox,
                                                         const uint32_t* __restrict__ smin,
+                                                        const uint32_t* __restrict__ qc,
+                                                        const float* __restrict__ qh,
                                                         const uint32_t* __restrict__ qlist, uint32_t q_first,
                                                         uint32_t q_count, const uint32_t* __restrict__ kq,
                                                         const float* __restrict__ rq, uint32_t kmax,
@@ -454,6 +499,7 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
     struct Cand {
         float v[D];
         uint32_t j;
+        bool live;  // wave-uniform: some lane holds a candidate
     };
     auto load = [&](uint32_t t, Cand& cd) {
         t = VGPU_DCLAMP(dbg, t, T, DBG_KNN_TILE);
@@ -462,6 +508,43 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
 #pragma unroll
         for (int d = 0; d < D; ++d) cd.v[d] = ok ? Vs[(size_t)cp * D + d] : 0.0f;
         cd.j = ok ? perm[cp] : 0xFFFFFFFFu;  // a missing candidate is never < i
+        cd.live = true;
+    };
+    constexpr int W = code_words<D>();
+    struct Codes {
+        uint32_t w[W];
+    };
+    auto load_codes = [&](uint32_t t, Codes& cc) {
+        t = VGPU_DCLAMP(dbg, t, T, DBG_KNN_TILE);
+#pragma unroll
+        for (int w = 0; w < W; ++w) cc.w[w] = qc[((size_t)t * W + w) * kTile + lane];
+    };
+    // coded distances of tile t's candidates; exact coordinates and index only where some query can take one
+    // (its threshold now -- thresholds only shrink, so a later test is no looser)
+    auto refine = [&](uint32_t t, const Codes& cc, Cand& cd) {
+        t = VGPU_DCLAMP(dbg, t, T, DBG_KNN_TILE);
+        const float* __restrict__ h = qh + (size_t)t * (D + 1);
+        const float* __restrict__ bx = tbox + (size_t)t * 2 * D;
+        float xa[D];
+#pragma unroll
+        for (int d = 0; d < D; ++d)
+            xa[d] = __builtin_fmaf((float)((cc.w[d / 4] >> (8 * (d % 4))) & 0xFFu), h[d], bx[d]);
+        const float delta = h[D];
+        bool pass = false;
+#pragma unroll
+        for (int q = 0; q < QG; ++q) {
+            // |x - me| <= |x' - me| + delta; thr >= s_exact implies |x - me| <= sqrt(thr) (1 + 2^-23); the
+            // coded sum's own rounding (< 1e-6 relative) is covered by the last factor.  A dead query
+            // (thr = -1) gives NaN: never passes.
+            const float b = __builtin_sqrtf(thr[q]) * 1.000002f + delta;
+            pass |= sumsq<D>(xa, me[q]) <= b * b * 1.00001f;
+        }
+        const uint32_t cp = t * kTile + lane;
+        const bool ok = pass && cp < n;
+#pragma unroll
+        for (int d = 0; d < D; ++d) cd.v[d] = ok ? Vs[(size_t)cp * D + d] : 0.0f;
+        cd.j = ok ? perm[cp] : 0xFFFFFFFFu;
+        cd.live = __builtin_amdgcn_ballot_w64(ok) != 0ull;
     };
     auto consider = [&](const Cand& cd) {
         const float* cv = cd.v;
@@ -512,16 +595,46 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
         const bool need = t < T && t != skip && need_box(tbox + (size_t)t * 2 * D, tmin[t]);
         uint64_t m = __builtin_amdgcn_ballot_w64(need);
         if (m == 0ull) return;
-        Cand cur, nxt;
-        load(sp * kSuper + (uint32_t)__builtin_ctzll(m), cur);
-        m &= m - 1ull;
-        for (;;) {
-            const bool more = m != 0ull;
-            if (more) load(sp * kSuper + (uint32_t)__builtin_ctzll(m), nxt);
-            consider(cur);
-            if (!more) break;
+        if constexpr (QC) {
+            // two stages in flight: the next tile's codes while this tile's exact candidates are tested
+            uint32_t t1 = sp * kSuper + (uint32_t)__builtin_ctzll(m);
             m &= m - 1ull;
-            cur = nxt;
+            Codes c1;
+            load_codes(t1, c1);
+            Cand cur;
+            refine(t1, c1, cur);
+            bool has1 = m != 0ull;
+            if (has1) {
+                t1 = sp * kSuper + (uint32_t)__builtin_ctzll(m);
+                m &= m - 1ull;
+                load_codes(t1, c1);
+            }
+            for (;;) {
+                Cand nxt;
+                const bool hasn = has1;
+                if (hasn) refine(t1, c1, nxt);
+                has1 = m != 0ull;
+                if (has1) {
+                    t1 = sp * kSuper + (uint32_t)__builtin_ctzll(m);
+                    m &= m - 1ull;
+                    load_codes(t1, c1);
+                }
+                if (cur.live) consider(cur);
+                if (!hasn) break;
+                cur = nxt;
+            }
+        } else {
+            Cand cur, nxt;
+            load(sp * kSuper + (uint32_t)__builtin_ctzll(m), cur);
+            m &= m - 1ull;
+            for (;;) {
+                const bool more = m != 0ull;
+                if (more) load(sp * kSuper + (uint32_t)__builtin_ctzll(m), nxt);
+                consider(cur);
+                if (!more) break;
+                m &= m - 1ull;
+                cur = nxt;
+            }
         }
     };
     const uint32_t home_t = p0 / kTile, home_s = home_t / kSuper;
@@ -556,7 +669,7 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
     }
 }
 
-// ---- block-cooperative group queries (VAMP_AMD_KNN_COOP, default) --------------------------------------
+// ---- block-cooperative group queries (VAMP_AMD_KNN_COOP=4 or 8; an A/B option, not the default) ----------
 // group_kernel fetches every candidate tile once per WAVE (4 queries): at 2.7M Fetch vertices each wave
 // visits ~700 tiles spread over the whole vertex set, so the tiles miss the 4 MB L2 and ~1.1 TB per call
 // comes from the Infinity Cache.  Here the WV waves of a workgroup (4 * WV Morton-consecutive
@@ -786,7 +899,7 @@ __global__ __launch_bounds__(64 * WV) void coop_kernel(const float* __restrict__
 inline size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 
 struct Layout {
-    size_t part, ls, key0, key1, id0, perm, Vs, tbox, tmin, sbox, smin, flag, qlist, nsel, tmp, total;
+    size_t part, ls, key0, key1, id0, perm, Vs, tbox, tmin, qc, qh, sbox, smin, flag, qlist, nsel, tmp, total;
 };
 
 template <int D>
@@ -816,6 +929,8 @@ hipError_t layout(uint32_t n, uint32_t q_count, Layout& L)
     L.Vs = take((size_t)n * D * 4);
     L.tbox = take((size_t)T * 2 * D * 4);
     L.tmin = take((size_t)T * 4);
+    L.qc = take((size_t)T * code_words<D>() * kTile * 4);
+    L.qh = take((size_t)T * (D + 1) * 4);
     const uint32_t S = (T + kSuper - 1) / kSuper;
     L.sbox = take((size_t)S * 2 * D * 4);
     L.smin = take((size_t)S * 4);
@@ -846,6 +961,8 @@ hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, c
     float* Vs = (float*)(pool + L.Vs);
     float* tbox = (float*)(pool + L.tbox);
     uint32_t* tmin = (uint32_t*)(pool + L.tmin);
+    uint32_t* qc = (uint32_t*)(pool + L.qc);
+    float* qh = (float*)(pool + L.qh);
     uint8_t* flag = (uint8_t*)(pool + L.flag);
     uint32_t* qlist = (uint32_t*)(pool + L.qlist);
     uint32_t* nsel = (uint32_t*)(pool + L.nsel);
@@ -861,7 +978,16 @@ hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, c
     size_t tb = tbytes;
     e = hipcub::DeviceRadixSort::SortPairs(tmp, tb, key0, key1, id0, perm, (int)n, 0, D * bits_per_dim<D>(), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL((tile_kernel<D>), dim3(T), dim3(kTile), 0, st, V, perm, n, Vs, tbox, tmin);
+    // coded candidates (VAMP_AMD_KNN_QCODE=1; an A/B option, default 0 = every visited candidate read exactly).
+    // A/B on MI355X (profiles/r05g_ab.log): 2.68M vertices 216 ms exact vs 380 ms coded, 100k 3.6 vs 6.8 ms --
+    // the tile's bytes were not the bound: the coded test adds a dependent load (codes -> test -> exact rows)
+    // and registers, and the kernel waits on latency, not on bandwidth
+    static const bool qcode = [] {
+        const char* s = std::getenv("VAMP_AMD_KNN_QCODE");
+        return s ? std::atoi(s) != 0 : false;
+    }();
+    hipLaunchKernelGGL((tile_kernel<D>), dim3(T), dim3(kTile), 0, st, V, perm, n, Vs, tbox, tmin,
+                       qcode && group > 0 ? qc : nullptr, qh);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t* ql = nullptr;
     if (!(q_first == 0 && q_count == n)) {
@@ -887,10 +1013,13 @@ hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, c
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const uint32_t QG = group >= 8 ? 8 : (group >= 4 ? 4 : (group >= 2 ? 2 : 1));
     const uint64_t waves = (q_count + QG - 1) / QG;
-    // block-cooperative tiles (VAMP_AMD_KNN_COOP: waves per workgroup, 4 or 8; 0 = group_kernel)
+    // block-cooperative tiles (VAMP_AMD_KNN_COOP: waves per workgroup, 4 or 8; 0 = group_kernel, the default).
+    // A/B on MI355X, 2.68M Fetch vertices (profiles/r05e_ab.log): group_kernel 212 ms, coop 4 waves 263 ms,
+    // 8 waves 326 ms -- the shared tiles cost a block barrier per batch and the union of four waves' needs,
+    // more than the L2 misses they save.
     static const int coop = [] {
         const char* s = std::getenv("VAMP_AMD_KNN_COOP");
-        return s ? std::atoi(s) : 4;
+        return s ? std::atoi(s) : 0;
     }();
     if (coop > 0 && QG == 4) {
         const int WV = coop >= 8 ? 8 : 4;
@@ -904,14 +1033,18 @@ hipError_t run(const float* V, uint32_t n, uint32_t q_first, uint32_t q_count, c
         return hipGetLastError();
     }
     const unsigned grid = (unsigned)((waves + kQBlock / 64 - 1) / (kQBlock / 64));
-#define VGPU_KNN_GROUP_LAUNCH(Q)                                                                                      \
-    hipLaunchKernelGGL((group_kernel<D, Q>), dim3(grid), dim3(kQBlock), 0, st, Vs, perm, n, T, S, tbox, tmin, sbox, \
-                       smin, ql, q_first, q_count, k, r, kmax, nbr, dist, cnt, dbg)
-    switch (QG) {
-    case 1: VGPU_KNN_GROUP_LAUNCH(1); break;
-    case 2: VGPU_KNN_GROUP_LAUNCH(2); break;
-    case 4: VGPU_KNN_GROUP_LAUNCH(4); break;
-    default: VGPU_KNN_GROUP_LAUNCH(8); break;
+#define VGPU_KNN_GROUP_LAUNCH(Q, C)                                                                                   \
+    hipLaunchKernelGGL((group_kernel<D, Q, C>), dim3(grid), dim3(kQBlock), 0, st, Vs, perm, n, T, S, tbox, tmin,   \
+                       sbox, smin, qc, qh, ql, q_first, q_count, k, r, kmax, nbr, dist, cnt, dbg)
+    switch (QG * 2 + (qcode ? 1 : 0)) {
+    case 2: VGPU_KNN_GROUP_LAUNCH(1, false); break;
+    case 3: VGPU_KNN_GROUP_LAUNCH(1, true); break;
+    case 4: VGPU_KNN_GROUP_LAUNCH(2, false); break;
+    case 5: VGPU_KNN_GROUP_LAUNCH(2, true); break;
+    case 8: VGPU_KNN_GROUP_LAUNCH(4, false); break;
+    case 9: VGPU_KNN_GROUP_LAUNCH(4, true); break;
+    case 16: VGPU_KNN_GROUP_LAUNCH(8, false); break;
+    default: VGPU_KNN_GROUP_LAUNCH(8, true); break;
     }
 #undef VGPU_KNN_GROUP_LAUNCH
     return hipGetLastError();

@@ -15,7 +15,11 @@
 #include "gen/panda_pair_staged.inc"
 
 #ifndef VGPU_PAIR_BOUND_WAVES
-#define VGPU_PAIR_BOUND_WAVES 4
+#define VGPU_PAIR_BOUND_WAVES 5  // the arm passes' bound kernels
+#endif
+// the inter-arm passes' bound kernels over single configurations (fkcc): the second chunk spilled 5 VGPRs at 5
+#ifndef VGPU_PAIR_INTER_BOUND_WAVES
+#define VGPU_PAIR_INTER_BOUND_WAVES 4
 #endif
 // the inter-arm passes' bound kernels over 8-lane rake groups (validate head / tail): both arms' link
 // frames are live at once -- 176 B/lane of scratch at 5 waves/EU, 12 B at 4 (128 VGPRs), none at 3
@@ -97,8 +101,9 @@ struct PairInterR : PairRakeR {
     static constexpr int kFirst = K * panda_pair_chunk;
     static constexpr int kChecks = (panda_pair_n_checks - kFirst) < panda_pair_chunk ? (panda_pair_n_checks - kFirst)
                                                                                       : panda_pair_chunk;
-    static constexpr int kWavesPerEU = VGPU_PAIR_BOUND_WAVES;
+    static constexpr int kWavesPerEU = VGPU_PAIR_INTER_BOUND_WAVES;
     static constexpr int kBoundWaves8 = VGPU_PAIR_INTER_BOUND8_WAVES;
+    static constexpr int kExtBoundWaves = 2;  // point-cloud bound kernels (vgpu_staged.hh BoundWavesE)
     static constexpr int kChildWavesPerEU = VGPU_PAIR_INTER_WAVES;
     using Mask = uint64_t;
     static constexpr Mask kEnvChecks = 0u;

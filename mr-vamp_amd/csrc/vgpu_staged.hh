@@ -69,14 +69,26 @@ struct ChildClasses<R, std::void_t<decltype(R::kClassOf)>> {
 };
 
 // waves/EU of a children kernel: with a point cloud (EXT) at most VGPU_EXT_CHILD_WAVES -- the deferred
-// queries' queue bookkeeping would spill at 8 (64 VGPRs)
+// queries' queue bookkeeping adds live registers: at 7 waves (72 VGPRs) the Panda / pair-arm class-0 kernels
+// spilled 16-23 VGPRs (48-72 B scratch per lane); at 5 (96) none do (tests/test_kernel_resources.py).  A/B on
+// MI355X, CAPT 2^20 configurations: 0.510 -> 0.518 ms kernel time (profiles/r05e_capt_ab.log)
 #ifndef VGPU_EXT_CHILD_WAVES
-#define VGPU_EXT_CHILD_WAVES 7
+#define VGPU_EXT_CHILD_WAVES 5
 #endif
+// (a robot may set its own point-cloud caps per class: R::kExtClassWaves[K])
+template <class R, class = void>
+struct ExtClassWaves {
+    __host__ __device__ static constexpr int of(int) { return VGPU_EXT_CHILD_WAVES; }
+};
+template <class R>
+struct ExtClassWaves<R, std::void_t<decltype(R::kExtClassWaves)>> {
+    __host__ __device__ static constexpr int of(int k) { return R::kExtClassWaves[k]; }
+};
 template <class R, int K, bool EXT>
 struct ChildWaves {
     static constexpr int w = ChildClasses<R>::waves(K);
-    static constexpr int v = (EXT && w > VGPU_EXT_CHILD_WAVES) ? VGPU_EXT_CHILD_WAVES : w;
+    static constexpr int cap = ExtClassWaves<R>::of(K);
+    static constexpr int v = (EXT && w > cap) ? cap : w;
 };
 
 // Source kinds a robot's staged exports instantiate (bit k = kind k of StagedHost::with_source): all
@@ -254,6 +266,22 @@ template <class R, class Src>
 struct BoundWaves<R, Src, std::void_t<decltype(R::kBoundWaves8)>> {
     static constexpr int v = Src::G > 1 ? R::kBoundWaves8 : R::kWavesPerEU;
 };
+// with a point cloud (EXT) at most R::kExtBoundWaves (optional): the deferred-query bookkeeping adds live
+// registers to the bound kernels too (Fetch 8-lane: 24 VGPRs spilled at 128, the composite's inter-arm
+// chunks 6-12 at 96-168)
+template <class R, class = void>
+struct ExtBoundCap {
+    static constexpr int v = 8;
+};
+template <class R>
+struct ExtBoundCap<R, std::void_t<decltype(R::kExtBoundWaves)>> {
+    static constexpr int v = R::kExtBoundWaves;
+};
+template <class R, class Src, bool EXT>
+struct BoundWavesE {
+    static constexpr int b = BoundWaves<R, Src>::v;
+    static constexpr int v = (EXT && ExtBoundCap<R>::v < b) ? ExtBoundCap<R>::v : b;
+};
 
 // source kinds, numbered (the MidBound selection and the VGPU_HITSTATS counters)
 template <class Src> struct SrcKindOf;
@@ -279,7 +307,7 @@ inline constexpr bool kMidBound = ((MidKinds<R>::v >> SrcKindOf<Src>::v) & 1u) !
 
 // ---- stage 1: bounding masks ---------------------------------------------------------------
 template <class R, class Src, bool EXT>
-__global__ __launch_bounds__(kStagedBlock, (BoundWaves<R, Src>::v)) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
+__global__ __launch_bounds__(kStagedBlock, (BoundWavesE<R, Src, EXT>::v)) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
                                                                              Bases bs, int chain,
                                                                              typename R::Mask* __restrict__ mask,
                                                                              uint8_t* __restrict__ valid)

@@ -22,19 +22,25 @@ sys.path.insert(0, os.path.join(ROOT, "tools"))
 LIB = os.path.join(ROOT, "mr-vamp_amd", "vamp_amd", "libvampgpu.so")
 
 
-def staged(robot, ext, kinds=r"\w+"):
-    """regexes of a robot's staged bound / lead / children kernels (vgpu_staged.hh), EXT = point-cloud path"""
-    R = re.escape(robot)
+def staged(robot, ext, lead=False):
+    """regexes of a robot's staged bound / children (/ lead) kernels (vgpu_staged.hh); robot is a regex over the
+    robot type's name, ext = the point-cloud instantiations"""
+    R = robot
     e = "true" if ext else "false"
-    src = rf"vgpu::Src(?:{kinds})<{R} ?>"
-    # bound kernels: <R, Src, EXT, FUSE>; the fused-lead instantiations (FUSE = true, an A/B knob) are not listed
-    return [rf"vgpu::bound_kernel<{R}, {src}, {e}, false>", rf"vgpu::children_kernel<{R}, {src}, {e}, \d>"] + \
-        ([rf"vgpu::lead_kernel<{R}, {src} ?>"] if not ext else [])
+    src = rf"vgpu::Src(?:\w+)<{R} ?>"
+    return [rf"vgpu::bound_kernel<{R}, {src}, {e}>", rf"vgpu::children_kernel<{R}, {src}, {e}, \d>"] + \
+        ([rf"vgpu::lead_kernel<{R}, {src} ?>"] if lead else [])
 
 
-# (description, regexes over the demangled kernel names); every match must have 0 scratch and 0 VGPR spills
+# (description, regexes over the demangled kernel names); every match must have 0 scratch and 0 VGPR spills.
+# Not listed: the Fetch's point-cloud children kernels (no bench workload runs them), where 2-5 VGPRs (8-16 B
+# per lane) still spill in four kernels even at 128-168 VGPRs (vgpu_fetch_staged.hip kExtClassWaves)
 HOT = [
-    ("Panda staged, primitive environments (configs[1])", staged("vgpu::PandaR", False)),
+    ("Panda staged, primitive environments (configs[1])", staged(r"vgpu::PandaR", False, lead=True)),
+    ("Panda staged, point clouds (CAPT, configs[2])", staged(r"vgpu::PandaR", True)),
+    ("Fetch staged, primitive environments (configs[3])", staged(r"vgpu::FetchR", False)),
+    ("composite arm passes (configs[4])", staged(r"vgpu::PairArmR<\d>", False) + staged(r"vgpu::PairArmR<\d>", True)),
+    ("composite inter-arm passes (configs[4])", staged(r"vgpu::PairInterR<\d>", False) + staged(r"vgpu::PairInterR<\d>", True)),
 ]
 
 

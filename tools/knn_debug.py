@@ -1,4 +1,4 @@
-"""Development: the spatial-index kNN (VAMP_AMD_KNN_COOP selects the kernel) vs the GPU brute force on n Halton
+"""Development: the spatial-index kNN (VAMP_AMD_KNN_COOP / VAMP_AMD_KNN_QCODE select the kernel) vs the GPU brute force on n Halton
 Fetch vertices; prints the mismatched queries.   python tools/knn_debug.py [n]"""
 import os
 import sys
@@ -30,3 +30,4 @@ for i in bad[:5]:
     for j in sorted(sa - sb)[:3]:
         print("   extra", j, "dist", float(ad[i, list(an[i, :ac[i]]).index(j)]))
     print("   order equal as sets:", sa == sb)
+sys.exit(1 if bad else 0)
