@@ -883,7 +883,9 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
             g.starts_off = (uint32_t)o_starts;
             g.aff_off = (uint32_t)o_aff;
             g.cells_off = (uint32_t)dpos();
-            const size_t hole = (2 * (size_t)g.nx * g.ny * g.nz + 15) & ~(size_t)15;
+            const size_t cell_f = (2 * (size_t)g.nx * g.ny * g.nz + 15) & ~(size_t)15;
+            g.leaf_off = (uint32_t)(g.cells_off + cell_f);  // the build's leaf summaries follow the cells
+            const size_t hole = cell_f + ((((size_t)vgpu::kCaptLeafSummary << t.nlog2) + 15) & ~(size_t)15);
             if (holes) holes->push_back({blob.size(), hole});
             shift += hole;
             const float gv[] = {g.x0, g.y0, g.z0, g.inv_h};
@@ -1378,9 +1380,11 @@ static StagedChain generic_chain(int32_t kind)
 // device (plan_kernel) and read there by queue and children.
 // b: the robot base (b[0..2]) -- and the composite's second arm (b[3..5]); chain != 0: a later pass
 // over the same groups (the flags are ANDed into, groups already invalid skip every stage)
+// masks_ready: this pass's masks were stored by the previous pass's bound kernel at c->st_mask + mask_off
+// (vgpu_staged.hh BothChunks) -- its own bound kernel is skipped
 static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const void* s0, const void* s1, const void* s2,
                        const void* s3, uint64_t first, size_t n, const EnvView* v, const float b[3], uint8_t* valid,
-                       int chain = 0, const float* b2 = nullptr)
+                       int chain = 0, const float* b2 = nullptr, bool masks_ready = false, size_t mask_off = 0)
 {
     if (kind < 0 || kind > 4) return fail(c, VGPU_ERR_INVALID_ARG, "staged pass: source kind");
     const StagedOps& ops = ops_in.by_kind ? *ops_in.by_kind[kind] : ops_in;
@@ -1395,7 +1399,8 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const voi
     const size_t cells_al = (cells + 1 + 63) & ~(size_t)63;
     const size_t plan_words = ((ops.plan_bytes() + 3) / 4 + 63) & ~(size_t)63;  // keeps tmp 256-B aligned
     int rc;
-    if ((rc = grow(c, &c->st_mask, &c->st_mask_cap, n * (size_t)ops.mask_bytes() / 4))) return rc;
+    if (!masks_ready && (rc = grow(c, &c->st_mask, &c->st_mask_cap, n * (size_t)ops.mask_bytes() / 4))) return rc;
+    uint32_t* const mask = c->st_mask + mask_off;
     if ((rc = grow(c, &c->st_cnt, &c->st_cnt_cap, 2 * cells_al + scan_bytes / 4 + 64 + plan_words))) return rc;
     if (!c->st_host) HIPCHK(c, hipHostMalloc((void**)&c->st_host, 128 * sizeof(uint32_t), hipHostMallocDefault));
     uint32_t* counts = c->st_cnt;
@@ -1413,12 +1418,12 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const voi
         HIPCHK(c, ops.lead(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, valid, c->cur));
         chain = 1;
     }
-    HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, chain, c->st_mask, valid, c->cur));
+    if (!masks_ready) HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, chain, mask, valid, c->cur));
     uint64_t all = checks >= 64 ? ~0ull : ((1ull << checks) - 1ull);
     if (use_lead) all &= ~(1ull << lead);  // decided by the lead pass
     const uint64_t env_bits = ops.env_checks();
     // every check's fired groups (groups still valid): segment boundaries offs[k * nb], k = 0..checks
-    HIPCHK(c, ops.count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, all, valid, counts, c->cur));
+    HIPCHK(c, ops.count(kind, s0, s1, s2, s3, mask, (uint32_t)n, all, valid, counts, c->cur));
     HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
     HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t), checks + 1,
                                hipMemcpyDeviceToHost, c->cur));
@@ -1461,12 +1466,12 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const voi
             if ((set >> k) & 1u) ub[ops.child_class(k)] += (fired[k] + W - 1) / W * W;
         if (!(ub[0] | ub[1] | ub[2] | ub[3])) continue;
         if (!first_round) {
-            HIPCHK(c, ops.count(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, valid, counts, c->cur));
+            HIPCHK(c, ops.count(kind, s0, s1, s2, s3, mask, (uint32_t)n, set, valid, counts, c->cur));
             HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
         }
         first_round = false;
         HIPCHK(c, ops.plan(offs, (uint32_t)nb, W, set, (uint32_t)n, plan, c->cur));
-        HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, c->st_mask, (uint32_t)n, set, plan, valid, offs, c->st_items, v->base,
+        HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, mask, (uint32_t)n, set, plan, valid, offs, c->st_items, v->base,
                             c->cur));
         HIPCHK(c, ops.children(kind, s0, s1, s2, s3, first, plan, ub, c->st_items, v, bases, valid, c->cur));
     }
@@ -1485,10 +1490,19 @@ static int chain_pass(vgpu_ctx* c, const StagedChain& ch, int kind, const void* 
 }
 
 // The composite's validity fkcc_A && fkcc_B && !inter (vgpu_pair_staged.hip): arm A, arm B, inter-arm chunks
+// (inter-arm chunk 0's bound kernel also stores chunk 1's masks, after its own: vgpu_pair_staged.hip PairInterR,
+// so chunk 1 runs without a bound kernel of its own -- both arms' FK once for all 121 inter-arm bounding pairs)
 static int pair_staged(vgpu_ctx* c, int kind, const void* s0, const void* s1, const void* s2, const void* s3, size_t n,
                        const EnvView* v, const float pb[6], uint8_t* valid)
 {
-    return chain_pass(c, StagedChain{kPairStaged, 4}, kind, s0, s1, s2, s3, 0, n, v, pb, valid, pb + 3);
+    const bool both = kPairStaged[2].mask_bytes() == 2 * kPairStaged[3].mask_bytes();
+    for (int p = 0; p < 4; ++p) {
+        const bool ready = both && p == 3;
+        const size_t off = ready ? n * (size_t)kPairStaged[3].mask_bytes() / 4 : 0;
+        if (int rc = staged_pass(c, kPairStaged[p], kind, s0, s1, s2, s3, 0, n, v, pb, valid, p, pb + 3, ready, off))
+            return rc;
+    }
+    return VGPU_OK;
 }
 
 extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n, uint8_t* valid)

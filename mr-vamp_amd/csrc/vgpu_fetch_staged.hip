@@ -45,6 +45,14 @@
 #define VGPU_FETCH_CLASS3_WAVES 5
 #endif
 
+// source kinds whose bound stage runs the mid-sphere tests (vgpu_staged.hh MidKinds; tools/gen_kernels.py
+// MID_SELF_CHECKS: the head / base / torso vs arm self checks whose validate-tail items almost never confirm):
+// validate heads and tails.  A/B on MI355X (profiles/r05h_ab.log): edge stage at 2.68M vertices, validation
+// 424 -> 384 ms with tails only, 371 ms with heads too; 100k vertices 24.6 -> 22.3 ms; sampler unchanged
+#ifndef VGPU_FETCH_MID_KINDS
+#define VGPU_FETCH_MID_KINDS ((1u << 2) | (1u << 3) | (1u << 4))
+#endif
+
 namespace vgpu {
 
 struct FetchR {
@@ -63,6 +71,7 @@ struct FetchR {
     static constexpr int kClassWaves[kClasses] = {VGPU_FETCH_CLASS0_WAVES, VGPU_FETCH_CLASS1_WAVES,
                                                   VGPU_FETCH_CLASS2_WAVES, VGPU_FETCH_CLASS3_WAVES};
     static constexpr int kExtClassWaves[kClasses] = {4, 3, 5, 5};
+    static constexpr uint32_t kMidKinds = VGPU_FETCH_MID_KINDS;
     __device__ static __forceinline__ void sample(uint64_t k, float v[8]) { sample_d<8>(k, fetch_s_m, fetch_s_a, v); }
     __device__ static __forceinline__ void head(const float* s, const float* g, int lane, float v[8])
     {
@@ -74,10 +83,10 @@ struct FetchR {
         const RakeD<8> rk = rake_setup_d<8, kRes>(s, g);
         rake_block_d<8>(s, rk, lane, k, v);
     }
-    template <class Grp, bool EXT>
+    template <class Grp, bool EXT, bool MID = false>
     __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, const Bases&)
     {
-        return fetch_bound_mask<Grp, EXT>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], env, 0.0f, 0.0f, 0.0f);
+        return fetch_bound_mask<Grp, EXT, MID>(v[0], v[1], v[2], v[3], v[4], v[5], v[6], v[7], env, 0.0f, 0.0f, 0.0f);
     }
     template <class Grp, bool EXT>
     __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, const Bases&)

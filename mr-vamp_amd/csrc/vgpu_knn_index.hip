@@ -390,6 +390,11 @@ __global__ __launch_bounds__(kQBlock) void query_kernel(const float* __restrict_
 // lane); a super-tile / tile is visited only if some query of the group can take from it.
 // Admission is the same full-key rule, so the lists are again exactly the brute force's.
 constexpr int kSuper = 64;  // tiles per super-tile
+// candidate tiles held in registers per visit pipeline (2: one load in flight while a tile is tested; 3: two).
+// A/B on MI355X (profiles/r05h_ab.log): 2.68M vertices 211 -> 195 ms, 100k 3.47 -> 3.23 ms with 3
+#ifndef VGPU_KNN_DEPTH
+#define VGPU_KNN_DEPTH 3
+#endif
 
 // one wave per super-tile: the box of its tiles' boxes and their smallest vertex index
 template <int D>
@@ -622,6 +627,30 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
                 if (cur.live) consider(cur);
                 if (!hasn) break;
                 cur = nxt;
+            }
+        } else if constexpr (VGPU_KNN_DEPTH >= 3) {
+            // three tiles in registers: two loads in flight while one is tested (slots rotate a, b, c)
+            Cand a, b, c;
+            bool ha, hb, hc;
+            auto next = [&](Cand& x, bool& h) {
+                h = m != 0ull;
+                if (h) {
+                    load(sp * kSuper + (uint32_t)__builtin_ctzll(m), x);
+                    m &= m - 1ull;
+                }
+            };
+            next(a, ha);
+            next(b, hb);
+            for (;;) {
+                next(c, hc);
+                if (!ha) break;
+                consider(a);
+                next(a, ha);
+                if (!hb) break;
+                consider(b);
+                next(b, hb);
+                if (!hc) break;
+                consider(c);
             }
         } else {
             Cand cur, nxt;

@@ -34,6 +34,13 @@
 #ifndef VGPU_PAIR_INTER_WAVES
 #define VGPU_PAIR_INTER_WAVES 2
 #endif
+#ifndef VGPU_PAIR_BOTH
+#define VGPU_PAIR_BOTH 1
+#endif
+// the combined chunks' bound kernel over 8-lane rake groups (both arms' link centres, 121 tests)
+#ifndef VGPU_PAIR_BOTH8_WAVES
+#define VGPU_PAIR_BOTH8_WAVES 3
+#endif
 
 namespace vgpu {
 
@@ -102,11 +109,19 @@ struct PairInterR : PairRakeR {
     static constexpr int kChecks = (panda_pair_n_checks - kFirst) < panda_pair_chunk ? (panda_pair_n_checks - kFirst)
                                                                                       : panda_pair_chunk;
     static constexpr int kWavesPerEU = VGPU_PAIR_INTER_BOUND_WAVES;
-    static constexpr int kBoundWaves8 = VGPU_PAIR_INTER_BOUND8_WAVES;
+    static constexpr int kBoundWaves8 = (K == 0 && VGPU_PAIR_BOTH) ? VGPU_PAIR_BOTH8_WAVES : VGPU_PAIR_INTER_BOUND8_WAVES;
     static constexpr int kExtBoundWaves = 2;  // point-cloud bound kernels (vgpu_staged.hh BoundWavesE)
     static constexpr int kChildWavesPerEU = VGPU_PAIR_INTER_WAVES;
     using Mask = uint64_t;
     static constexpr Mask kEnvChecks = 0u;
+    // chunk 0's bound stage also computes chunk 1's masks (vgpu_staged.hh BothChunks; VGPU_PAIR_BOTH=0: one
+    // bound kernel per chunk, for A/B runs)
+    static constexpr bool kBothChunks = K == 0 && VGPU_PAIR_BOTH;
+    template <class Grp>
+    __device__ static __forceinline__ Mask bound_both(const float* v, const Bases& b, Mask& m1)
+    {
+        return panda_pair_bound_both<Grp>(PAIR_Q(v), b.x, b.y, b.z, b.x2, b.y2, b.z2, m1);
+    }
     template <class Grp, bool EXT>
     __device__ static __forceinline__ Mask bound(const float* v, const EnvView&, const Bases& b)
     {

@@ -305,6 +305,18 @@ struct MidKinds<R, std::void_t<decltype(R::kMidKinds)>> {
 template <class R, class Src>
 inline constexpr bool kMidBound = ((MidKinds<R>::v >> SrcKindOf<Src>::v) & 1u) != 0u;
 
+// R::kBothChunks (optional): the bound stage of this pass also computes the NEXT chained pass's masks (the
+// composite's two inter-arm chunks from one FK of both arms, R::bound_both) and stores them after its own,
+// mask[n_groups + g]; the host then skips the next pass's bound kernel and hands it that half
+template <class R, class = void>
+struct BothChunks {
+    static constexpr bool v = false;
+};
+template <class R>
+struct BothChunks<R, std::void_t<decltype(R::kBothChunks)>> {
+    static constexpr bool v = R::kBothChunks;
+};
+
 // ---- stage 1: bounding masks ---------------------------------------------------------------
 template <class R, class Src, bool EXT>
 __global__ __launch_bounds__(kStagedBlock, (BoundWavesE<R, Src, EXT>::v)) void bound_kernel(Src src, uint32_t n_groups, EnvView env,
@@ -324,7 +336,10 @@ __global__ __launch_bounds__(kStagedBlock, (BoundWavesE<R, Src, EXT>::v)) void b
     // a chained pass (a later pass over the same groups, e.g. the composite's arm B after arm A): a
     // group already invalid is done -- its mask stays 0 -- and the flag is not re-initialised
     if (chain && !valid[src.out(g)]) {
-        if (lane == 0) mask[g] = 0;
+        if (lane == 0) {
+            mask[g] = 0;
+            if constexpr (BothChunks<R>::v) mask[n_groups + g] = 0;
+        }
         return;
     }
     float v[R::D];
@@ -336,11 +351,14 @@ __global__ __launch_bounds__(kStagedBlock, (BoundWavesE<R, Src, EXT>::v)) void b
         }
     }
     typename R::Mask m;
-    if constexpr (kMidBound<R, Src>) m = R::template bound<Grp, EXT, true>(v, env, bs);
+    [[maybe_unused]] typename R::Mask m1 = 0;
+    if constexpr (BothChunks<R>::v) m = R::template bound_both<Grp>(v, bs, m1);
+    else if constexpr (kMidBound<R, Src>) m = R::template bound<Grp, EXT, true>(v, env, bs);
     else m = R::template bound<Grp, EXT>(v, env, bs);
     if constexpr (EXT) m |= (typename R::Mask)group_or64<Grp>(capt_defer_finish(env.pc, env.base, env.pc_lds_levels));
     if (lane == 0) {
         mask[g] = m;
+        if constexpr (BothChunks<R>::v) mask[n_groups + g] = m1;
         if constexpr (Src::kInit) {
             if (!chain) valid[src.out(g)] = 1;
         }
@@ -680,7 +698,7 @@ struct StagedHost {
     extern "C" {                                                                                                     \
     int vgpu_##NAME##_staged_checks(void) { return R::kChecks; }                                                     \
     uint64_t vgpu_##NAME##_staged_env_checks(void) { return (uint64_t)R::kEnvChecks; }                             \
-    int vgpu_##NAME##_staged_mask_bytes(void) { return (int)sizeof(typename R::Mask); }                              \
+    int vgpu_##NAME##_staged_mask_bytes(void) { return (int)sizeof(typename R::Mask) * (vgpu::BothChunks<R>::v ? 2 : 1); } \
     int vgpu_##NAME##_staged_class(int c) { return vgpu::ChildClasses<R>::of(c); }                                   \
     size_t vgpu_##NAME##_staged_plan_bytes(void) { return sizeof(vgpu::StagedPlan); }                               \
     uint32_t vgpu_##NAME##_staged_blocks(int, uint32_t n_groups)                                                     \

@@ -45,9 +45,22 @@ LEAD = {"panda": "panda_link5"}
 # environments).  Off: for the Panda it changed nothing measurable (set B 2.33-2.36 vs 2.33-2.34 ms, pair
 # 10.49 vs 10.43-10.50; profiles/r04q_early_ab.log) -- unlike the lead pass, where it took set A 1.06 -> 0.81
 EARLY_CHILDREN = set()
+# GPU staged bound stage: each check's test bit accumulated per LANE (lm |= bit << c), one OR over the
+# group at the end -- instead of a group reduction (3 DPP ops) and a divergent branch per check (--no-lane-bits).
+# Checks whose branch saves work keep it: mid-sphere tests, the never-fires guard, the gate.
+LANE_BITS = True
 MID_ENV = {"panda_link5": 4, "panda_hand": 4, "panda_link7": 3}
-MID_SELF_LINKS = {"panda_link1": 2, "panda_link2": 2, "panda_link5": 4}
-MID_SELF_CHECKS = [("panda_link1", "panda_link5"), ("panda_link2", "panda_link5")]
+MID_SELF_LINKS = {"panda_link1": 2, "panda_link2": 2, "panda_link5": 4,
+                  # Fetch (--mids on fetch.json): the self checks whose tails queue the most children items and
+                  # whose children almost never confirm (tools/hitstats.py --fetch, profiles/r04n_hitstats_fetch.json)
+                  "head_pan_link": 4, "upperarm_roll_link": 2, "elbow_flex_link": 2, "forearm_roll_link": 2,
+                  "base_link": 3, "torso_lift_link": 2, "torso_fixed_link": 2}
+MID_SELF_CHECKS = [("panda_link1", "panda_link5"), ("panda_link2", "panda_link5"),
+                   ("head_pan_link", "upperarm_roll_link"), ("head_pan_link", "elbow_flex_link"),
+                   ("head_pan_link", "forearm_roll_link"), ("base_link", "elbow_flex_link"),
+                   ("base_link", "forearm_roll_link"), ("torso_lift_link", "forearm_roll_link"),
+                   ("forearm_roll_link", "torso_fixed_link"), ("elbow_flex_link", "torso_fixed_link"),
+                   ("torso_lift_link", "elbow_flex_link")]
 MID_MARGIN = 1e-4
 
 # Emitted types.  The HIP kernels compute one configuration per lane in `float` with the
@@ -661,6 +674,31 @@ class RobotGen:
             out += ["template <class Grp>",
                     f"{TY['qual']} uint64_t {self.name}_pair_bound_mask_{k // chunk}(",
                     f"    {args},", f"    {base_args})", "{"] + E.lines + ["}", ""]
+        # every chunk's bounding tests in ONE pass (vgpu_pair_staged.hip PairInterR<0>::bound_both): arm A's link
+        # centres first, then arm B's links one at a time, each tested against all of A's -- both arms' FK once
+        # instead of once per chunk, and only A's centres held.  Bit c of the group's mask = some lane's test fires
+        # (Grp::any of each test, as in the chunked functions, taken as one OR over the group at the end)
+        E = Emitter()
+        fa, fb = self.Frames(self, E, 0), self.Frames(self, E, dim)
+        nck = len(checks)
+        E.raw("uint64_t mask[2] = {0u, 0u};")
+        bca = {la: wc(E, fa.bound_center(la), "a") for la in range(nb)}
+        for lb in range(nb):
+            B_ = wc(E, fb.bound_center(lb), "b")
+            rb = m["bounding"][lb]["radius"]
+            for la in range(nb):
+                c = la * nb + lb
+                A_, ra = bca[la], m["bounding"][la]["radius"]
+                E.raw(f"mask[{c // chunk}] |= (uint64_t)self_lane({A_[0].expr()}, {A_[1].expr()}, {A_[2].expr()}, "
+                      f"{flit(ra)}, {B_[0].expr()}, {B_[1].expr()}, {B_[2].expr()}, {flit(rb)}) << {c % chunk};"
+                      f"  // {links[la]} (A) vs {links[lb]} (B)")
+        # per-lane bits, OR-ed over the group once at the end (not one group reduction per test)
+        E.raw("m1 = vgpu::group_or64<Grp>(mask[1]);")
+        E.raw("return vgpu::group_or64<Grp>(mask[0]);")
+        assert nck <= 2 * chunk
+        out += ["template <class Grp>",
+                f"{TY['qual']} uint64_t {self.name}_pair_bound_both(",
+                f"    {args},", f"    {base_args}, uint64_t& m1)", "{"] + E.lines + ["}", ""]
         body = []
         for c, (la, lb) in enumerate(checks):
             E = Emitter()
@@ -825,6 +863,8 @@ class RobotGen:
         E = Emitter()
         fr = self.Frames(self, E)
         E.raw(f"{mt} mask = 0u;")
+        if LANE_BITS:
+            E.raw(f"{mt} lm = 0u;  // per-lane test bits, OR-ed over the group at the end")
         gate = self.load_gate()
         gated = {}
         if gate is not None:  # the wrist self checks' (q_a, q_b) gate table (tools/make_pair_gate.py)
@@ -832,8 +872,11 @@ class RobotGen:
             E.raw(f"const uint32_t gate = Grp::or_bits({self.name}_gate(q{d0}, q{d1}));  // per group: checks that can fire")
             gated = {c: b for b, c in enumerate(gate["checks"])}
         for c, o in enumerate(order):
-            self.emit_bound_check(E, fr, c, o, gated, one, mids_on=bool(MIDS))
-        E.raw("return mask;")
+            self.emit_bound_check(E, fr, c, o, gated, one, mids_on=bool(MIDS), mt=mt)
+        if LANE_BITS:
+            E.raw(f"return mask | {self.group_or(mt, 'lm')};")
+        else:
+            E.raw("return mask;")
         env_bits = sum(1 << c for c, o in enumerate(order) if o["kind"] == "env")
         out = [f"// GENERATED by tools/gen_kernels.py from model/{self.name}.json -- do not edit.",
                f"constexpr int {self.name}_n_checks = {len(order)};",
@@ -855,14 +898,26 @@ class RobotGen:
 
         return "\n".join(out)
 
-    def emit_bound_check(self, E, fr, c, o, gated, one, mids_on):
+    @staticmethod
+    def group_or(mt, v):
+        """OR of a per-lane check mask over the lane's group (Grp::or_bits on 32-bit halves)"""
+        if mt == "uint32_t":
+            return f"Grp::or_bits({v})"
+        return f"(((uint64_t)Grp::or_bits((uint32_t)({v} >> 32)) << 32) | (uint64_t)Grp::or_bits((uint32_t){v}))"
+
+    def emit_bound_check(self, E, fr, c, o, gated, one, mids_on, mt="uint32_t"):
         """check c's bounding test in the staged bound stage: bit c of mask set when it fires for the group"""
         kind, test, ck = self.bound_test(fr, o)
         mids = self.mids_of(ck, kind) if (mids_on and c not in gated) else None
+        lane = LANE_BITS and not TY["cpu"]
         if mids:
             self.emit_mid_check(E, fr, kind, test, ck, mids, c, one)
+        elif kind == "env" and lane:  # per lane: the sign bit of the check's env bits
+            E.raw(f"lm |= ({mt})({test[:-1]}, 0u, {c}) >> 31) << {c};")
         elif kind == "env":  # the check's bit is its deferred-query tag (vgpu_device.hh capt_defer_*)
             E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c}))) mask |= {one} << {c};")
+        elif c in gated and lane:
+            E.raw(f"if ((gate >> {gated[c]}) & 1u) lm |= ({mt})({test}) << {c};")
         elif c in gated:
             E.raw(f"if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c};")
         elif kind == "self" and ck.get("never_fires") and not TY["cpu"]:
@@ -875,7 +930,12 @@ class RobotGen:
                 return flit(f)
             inside = " && ".join(f"q{d} >= {inward(lo, True)} && q{d} <= {inward(hi, False)}"
                                  for d, lo, hi in zip(ck["never_dofs"], ck["never_lo"], ck["never_hi"]))
-            E.raw(f"if (Grp::any(!({inside})) && Grp::any({test})) mask |= {one} << {c};  // proven silent inside")
+            if lane:
+                E.raw(f"if (Grp::any(!({inside}))) lm |= ({mt})({test}) << {c};  // proven silent inside")
+            else:
+                E.raw(f"if (Grp::any(!({inside})) && Grp::any({test})) mask |= {one} << {c};  // proven silent inside")
+        elif lane:
+            E.raw(f"lm |= ({mt})({test}) << {c};")
         else:
             E.raw(f"if (Grp::any({test})) mask |= {one} << {c};")
 
@@ -996,11 +1056,15 @@ class RobotGen:
             E.raw("uint64_t mask = 0u;")
             for c in range(k, min(k + chunk, len(order))):
                 kind, test, ck = self.bound_test(fr, order[c])
-                if kind == "env":  # the check's bit in the chunk mask is its deferred-query tag
+                if kind == "env" and LANE_BITS:
+                    E.raw(f"mask |= (uint64_t)({test[:-1]}, 0u, {c - k}) >> 31) << {c - k};")
+                elif kind == "env":  # the check's bit in the chunk mask is its deferred-query tag
                     E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c - k}))) mask |= 1ull << {c - k};")
+                elif LANE_BITS:
+                    E.raw(f"mask |= (uint64_t)({test}) << {c - k};")
                 else:
                     E.raw(f"if (Grp::any({test})) mask |= 1ull << {c - k};")
-            E.raw("return mask;")
+            E.raw(f"return {self.group_or('uint64_t', 'mask')};" if LANE_BITS else "return mask;")
             out += self.signature("uint64_t", f"bound_mask_{k // chunk}") + E.lines + ["}", ""]
             envs.append(sum(1 << (c - k) for c in range(k, min(k + chunk, len(order)))
                             if order[c]["kind"] == "env"))
@@ -1024,7 +1088,7 @@ def gen_radii(paths) -> str:
 
 
 def main():
-    global REMAT, TY, HOLD, GATE, MIDS
+    global REMAT, TY, HOLD, GATE, MIDS, LANE_BITS
     if "--radii" in sys.argv:  # tools/gen_kernels.py --radii OUT model/a.json model/b.json ...
         args = [a for a in sys.argv[1:] if a != "--radii"]
         open(args[0], "w").write(gen_radii(args[1:]))
@@ -1041,6 +1105,9 @@ def main():
     if "--no-gate" in sys.argv:
         GATE = False
         sys.argv.remove("--no-gate")
+    if "--no-lane-bits" in sys.argv:
+        LANE_BITS = False
+        sys.argv.remove("--no-lane-bits")
     if "--mids" in sys.argv:
         MIDS = True
         sys.argv.remove("--mids")
