@@ -883,9 +883,7 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
             g.starts_off = (uint32_t)o_starts;
             g.aff_off = (uint32_t)o_aff;
             g.cells_off = (uint32_t)dpos();
-            const size_t cell_f = (2 * (size_t)g.nx * g.ny * g.nz + 15) & ~(size_t)15;
-            g.leaf_off = (uint32_t)(g.cells_off + cell_f);  // the build's leaf summaries follow the cells
-            const size_t hole = cell_f + ((((size_t)vgpu::kCaptLeafSummary << t.nlog2) + 15) & ~(size_t)15);
+            const size_t hole = (2 * (size_t)g.nx * g.ny * g.nz + 15) & ~(size_t)15;
             if (holes) holes->push_back({blob.size(), hole});
             shift += hole;
             const float gv[] = {g.x0, g.y0, g.z0, g.inv_h};

@@ -35,9 +35,7 @@ struct CaptGridArgs {
     uint32_t nx, ny, nz;
     float unit;
     uint32_t cells_off;
-    uint32_t leaf_off;  // per-leaf summaries for the build (vgpu_capt_grid.hip capt_leaf_kernel; 0: none)
 };
-constexpr int kCaptLeafSummary = 12;  // floats per leaf: affordance box lo[3] hi[3], one affordance, flag, pad
 
 // Sizes the grid of tree t: the top box grown by r_max + r_point, cubic cells, about `cells`
 // of them (0 = default: 128 per leaf, within [2^12, 2^22]; 8 B each).  false: no grid (empty cloud).

@@ -51,40 +51,10 @@ __device__ __forceinline__ float round_up(double x)
     return (double)f < x ? next_up(f) : f;
 }
 
-// One thread per leaf: the box of its finite affordances and one of them (the grid build's pruning below).
-__global__ __launch_bounds__(kGridBlock) void capt_leaf_kernel(float* __restrict__ base, CaptGridArgs g)
-{
-    const uint32_t leaf = blockIdx.x * (uint32_t)kGridBlock + threadIdx.x;
-    if (leaf >= (1u << g.nlog2)) return;
-    const uint32_t* __restrict__ starts = (const uint32_t*)(base + g.starts_off);
-    const float* __restrict__ aff = base + g.aff_off;
-    float lo[3] = {__builtin_inff(), __builtin_inff(), __builtin_inff()};
-    float hi[3] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-    float rep[3] = {0.0f, 0.0f, 0.0f};
-    bool have = false;
-    for (uint32_t j = starts[leaf], e = starts[leaf + 1]; j < e; ++j) {
-        const float* v = aff + 24u * j;
-        for (int l = 0; l < 8; ++l) {
-            const float p[3] = {v[l], v[8 + l], v[16 + l]};
-            if (!(__builtin_isfinite(p[0]) && __builtin_isfinite(p[1]) && __builtin_isfinite(p[2]))) continue;
-            for (int k = 0; k < 3; ++k) {
-                lo[k] = fminf(lo[k], p[k]);
-                hi[k] = fmaxf(hi[k], p[k]);
-                if (!have) rep[k] = p[k];
-            }
-            have = true;
-        }
-    }
-    float* s = base + g.leaf_off + (size_t)kCaptLeafSummary * leaf;
-    for (int k = 0; k < 3; ++k) {
-        s[k] = lo[k];
-        s[3 + k] = hi[k];
-        s[6 + k] = rep[k];
-    }
-    s[9] = have ? 1.0f : 0.0f;
-    s[10] = s[11] = 0.0f;
-}
-
+// (Round 5: skipping a reachable leaf's affordance loop when a per-leaf box / representative-affordance test shows
+// it cannot move either bound -- exact -- measured no gain on MI355X: 1.73 -> 1.79 ms for 2M cells plus 0.05 ms
+// for the summaries, profiles/r05j_capt_rel_kernel_stats.csv; most cells reach one or two leaves, whose loops
+// decide the bounds.)
 // One thread per cell.  The walk's stack lives in LDS (a private array indexed by a variable would go to
 // scratch memory), and the affordance loop runs in float over the expanded cell rounded OUTWARD to float
 // (a larger box: lo can only shrink and hi only grow), so its float rounding (< 1e-6 relative on distances
@@ -139,27 +109,6 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
                 break;
             }
             const uint32_t leaf = n - first_leaf;
-            if (g.leaf_off) {
-                // Skip the affordance loop when it cannot change either bound: the leaf's nearest affordance is
-                // at least the distance between the cell and the affordances' box (lo2 keeps its minimum), and
-                // its least farthest-corner distance is at most that of any one affordance (hi2 keeps its
-                // maximum).  Float rounding of either test (< 1e-6 relative) is covered by the final rounding
-                // of lo down and hi up by a further whole unit.
-                const float* s = base + g.leaf_off + (size_t)kCaptLeafSummary * leaf;
-                if (s[9] == 0.0f) {  // no finite affordance: the loop below would leave hmin = +inf
-                    hi2 = __builtin_inff();
-                    continue;
-                }
-                float db = 0.0f, fr = 0.0f;
-#pragma unroll
-                for (int k = 0; k < 3; ++k) {
-                    const float gap = fmaxf(fmaxf(s[k] - Uf[k], Lf[k] - s[3 + k]), 0.0f);
-                    const float far = fmaxf(fabsf(s[6 + k] - Lf[k]), fabsf(s[6 + k] - Uf[k]));
-                    db = __builtin_fmaf(gap, gap, db);
-                    fr = __builtin_fmaf(far, far, fr);
-                }
-                if (db >= lo2 && fr <= hi2) continue;
-            }
             float lmin = __builtin_inff(), hmin = __builtin_inff();
             for (uint32_t j = starts[leaf], e = starts[leaf + 1]; j < e; ++j) {
                 const float* v = aff + 24u * j;
@@ -214,11 +163,6 @@ extern "C" hipError_t vgpu_launch_capt_grid(float* base, const vgpu::CaptGridArg
     const uint64_t n = (uint64_t)g->nx * g->ny * g->nz;
     if (n == 0) return hipSuccess;
     if (n >= ((uint64_t)1 << 31)) return hipErrorInvalidValue;
-    if (g->leaf_off) {
-        const uint64_t leaves = (uint64_t)1 << g->nlog2;
-        hipLaunchKernelGGL(vgpu::capt_leaf_kernel, dim3((unsigned)((leaves + vgpu::kGridBlock - 1) / vgpu::kGridBlock)),
-                           dim3(vgpu::kGridBlock), 0, st, base, *g);
-    }
     hipLaunchKernelGGL(vgpu::capt_grid_kernel, dim3((unsigned)((n + vgpu::kGridBlock - 1) / vgpu::kGridBlock)),
                        dim3(vgpu::kGridBlock), 0, st, base, *g);
     return hipGetLastError();

@@ -47,7 +47,10 @@ LEAD = {"panda": "panda_link5"}
 EARLY_CHILDREN = set()
 # GPU staged bound stage: each check's test bit accumulated per LANE (lm |= bit << c), one OR over the
 # group at the end -- instead of a group reduction (3 DPP ops) and a divergent branch per check (--no-lane-bits).
-# Checks whose branch saves work keep it: mid-sphere tests, the never-fires guard, the gate.
+# Checks whose branch saves work keep it: mid-sphere tests, the never-fires guard, the gate.  8-lane groups
+# only (validate heads and tails): A/B on MI355X (profiles/r05j_ab.log) Fetch edge-stage validation 371 -> 298 ms
+# at 2.68M vertices (its 8-lane bound kernels 92 -> 62 VGPRs), Panda set B 2.22-2.24 -> 2.17-2.19 ms, composite
+# 8.67 -> 8.50 ms; single-lane groups keep the branch (the CAPT bound kernel went 77 -> 81 VGPRs, 0.52 -> 0.54 ms)
 LANE_BITS = True
 MID_ENV = {"panda_link5": 4, "panda_hand": 4, "panda_link7": 3}
 MID_SELF_LINKS = {"panda_link1": 2, "panda_link2": 2, "panda_link5": 4,
@@ -912,12 +915,14 @@ class RobotGen:
         lane = LANE_BITS and not TY["cpu"]
         if mids:
             self.emit_mid_check(E, fr, kind, test, ck, mids, c, one)
-        elif kind == "env" and lane:  # per lane: the sign bit of the check's env bits
-            E.raw(f"lm |= ({mt})({test[:-1]}, 0u, {c}) >> 31) << {c};")
+        elif kind == "env" and lane:  # per lane: the sign bit of the check's env bits (8-lane groups)
+            E.raw(f"if constexpr (Grp::G == 1) {{ if (Grp::any_bits({test[:-1]}, 0u, {c}))) mask |= {one} << {c}; }}")
+            E.raw(f"else {{ lm |= ({mt})({test[:-1]}, 0u, {c}) >> 31) << {c}; }}")
         elif kind == "env":  # the check's bit is its deferred-query tag (vgpu_device.hh capt_defer_*)
             E.raw(f"if (Grp::any_bits({test[:-1]}, 0u, {c}))) mask |= {one} << {c};")
         elif c in gated and lane:
-            E.raw(f"if ((gate >> {gated[c]}) & 1u) lm |= ({mt})({test}) << {c};")
+            E.raw(f"if constexpr (Grp::G == 1) {{ if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c}; }}")
+            E.raw(f"else {{ if ((gate >> {gated[c]}) & 1u) lm |= ({mt})({test}) << {c}; }}")
         elif c in gated:
             E.raw(f"if (((gate >> {gated[c]}) & 1u) && Grp::any({test})) mask |= {one} << {c};")
         elif kind == "self" and ck.get("never_fires") and not TY["cpu"]:
@@ -931,11 +936,13 @@ class RobotGen:
             inside = " && ".join(f"q{d} >= {inward(lo, True)} && q{d} <= {inward(hi, False)}"
                                  for d, lo, hi in zip(ck["never_dofs"], ck["never_lo"], ck["never_hi"]))
             if lane:
-                E.raw(f"if (Grp::any(!({inside}))) lm |= ({mt})({test}) << {c};  // proven silent inside")
+                E.raw(f"if constexpr (Grp::G == 1) {{ if (Grp::any(!({inside})) && Grp::any({test})) mask |= {one} << {c}; }}")
+                E.raw(f"else {{ if (Grp::any(!({inside}))) lm |= ({mt})({test}) << {c}; }}  // proven silent inside")
             else:
                 E.raw(f"if (Grp::any(!({inside})) && Grp::any({test})) mask |= {one} << {c};  // proven silent inside")
         elif lane:
-            E.raw(f"lm |= ({mt})({test}) << {c};")
+            E.raw(f"if constexpr (Grp::G == 1) {{ if (Grp::any({test})) mask |= {one} << {c}; }}")
+            E.raw(f"else {{ lm |= ({mt})({test}) << {c}; }}")
         else:
             E.raw(f"if (Grp::any({test})) mask |= {one} << {c};")
 
