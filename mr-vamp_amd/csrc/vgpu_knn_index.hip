@@ -390,6 +390,14 @@ __global__ __launch_bounds__(kQBlock) void query_kernel(const float* __restrict_
 // lane); a super-tile / tile is visited only if some query of the group can take from it.
 // Admission is the same full-key rule, so the lists are again exactly the brute force's.
 constexpr int kSuper = 64;  // tiles per super-tile
+// VGPU_KNN_ORDER bit 0: super-tiles visited nearest first (their box lower bound over the group's queries, one
+// global order when S <= 64 * kKeySlots) instead of outward by index, each re-checked against the thresholds as
+// they stand when its turn comes -- the lists tighten sooner, so fewer far tiles pass; bit 1: the same for the
+// tiles inside a super-tile.
+#ifndef VGPU_KNN_ORDER
+#define VGPU_KNN_ORDER 0
+#endif
+constexpr int kKeySlots = 16;
 // candidate tiles held in registers per visit pipeline (2: one load in flight while a tile is tested; 3: two).
 // A/B on MI355X (profiles/r05h_ab.log): 2.68M vertices 211 -> 195 ms, 100k 3.47 -> 3.23 ms with 3
 #ifndef VGPU_KNN_DEPTH
@@ -597,6 +605,53 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
     auto visit_super = [&](uint32_t sp, uint32_t skip) {
         sp = VGPU_DCLAMP(dbg, sp, S, DBG_KNN_SUPER);
         const uint32_t t = sp * kSuper + lane;
+        if constexpr ((VGPU_KNN_ORDER & 2) && !QC) {
+            // this lane's tile: its box lower bound per query (need = some query could take from it)
+            float lbq[QG];
+            float key = __builtin_inff();
+            const bool ok = t < T && t != skip;
+            const uint32_t mn = ok ? tmin[t] : 0u;
+#pragma unroll
+            for (int q = 0; q < QG; ++q) {
+                lbq[q] = ok ? box_lb<D>(tbox + (size_t)t * 2 * D, me[q]) : __builtin_inff();
+                if (mn < qi[q] && lbq[q] <= thr[q] * 1.0001f) key = fminf(key, lbq[q]);
+            }
+            uint64_t m = __builtin_amdgcn_ballot_w64(key < __builtin_inff());
+            // the needed tile with the least bound, still needed under the current thresholds (0xFFFFFFFF: none)
+            auto pick = [&]() -> uint32_t {
+                bool still = false;
+#pragma unroll
+                for (int q = 0; q < QG; ++q) still |= mn < qi[q] && lbq[q] <= thr[q] * 1.0001f;
+                m &= __builtin_amdgcn_ballot_w64(still);
+                if (m == 0ull) return 0xFFFFFFFFu;
+                const float k = ((m >> lane) & 1ull) ? key : __builtin_inff();
+                const float kmin = wave_min(k);
+                const uint32_t sel = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(k == kmin) & m);
+                m &= ~(1ull << sel);
+                return sel;
+            };
+            Cand a, b, c;
+            bool ha, hb, hc;
+            auto next = [&](Cand& x, bool& h) {
+                const uint32_t sel = pick();
+                h = sel != 0xFFFFFFFFu;
+                if (h) load(sp * kSuper + sel, x);
+            };
+            next(a, ha);
+            next(b, hb);
+            for (;;) {
+                next(c, hc);
+                if (!ha) break;
+                consider(a);
+                next(a, ha);
+                if (!hb) break;
+                consider(b);
+                next(b, hb);
+                if (!hc) break;
+                consider(c);
+            }
+            return;
+        }
         const bool need = t < T && t != skip && need_box(tbox + (size_t)t * 2 * D, tmin[t]);
         uint64_t m = __builtin_amdgcn_ballot_w64(need);
         if (m == 0ull) return;
@@ -673,6 +728,55 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
         consider(h);
     }
     visit_super(home_s, home_t);
+    if constexpr ((VGPU_KNN_ORDER & 1) && !QC) {
+        if (S <= 64u * kKeySlots) {
+            // every super-tile's bound (lane + 64 j) into this wave's LDS row, the lane's least one in registers;
+            // then the wave's least first, each re-checked when its turn comes
+            __shared__ float skey[kQBlock / 64][64 * kKeySlots];
+            float* row = skey[threadIdx.x >> 6];
+            float kl = __builtin_inff();
+            uint32_t jl = 0;
+            for (uint32_t j = 0; j < (uint32_t)kKeySlots; ++j) {
+                const uint32_t sp = lane + 64u * j;
+                float k = __builtin_inff();
+                if (sp < S && sp != home_s) {
+                    const float* bx = sbox + (size_t)sp * 2 * D;
+                    const uint32_t mn = smin[sp];
+#pragma unroll
+                    for (int q = 0; q < QG; ++q) {
+                        const float lb = box_lb<D>(bx, me[q]);
+                        if (mn < qi[q] && lb <= thr[q] * 1.0001f) k = fminf(k, lb);
+                    }
+                }
+                row[sp] = k;
+                if (k < kl) {
+                    kl = k;
+                    jl = j;
+                }
+            }
+            for (;;) {
+                const float kmin = wave_min(kl);
+                if (!(kmin < __builtin_inff())) break;
+                const uint32_t sl = (uint32_t)__builtin_ctzll(__builtin_amdgcn_ballot_w64(kl == kmin));
+                const uint32_t js = (uint32_t)__builtin_amdgcn_readlane((int)jl, (int)sl);
+                if (lane == sl) {  // drop the pick from this lane's entries, find its next least
+                    row[sl + 64u * js] = __builtin_inff();
+                    kl = __builtin_inff();
+                    for (uint32_t j = 0; j < (uint32_t)kKeySlots; ++j) {
+                        const float k = row[lane + 64u * j];
+                        if (k < kl) {
+                            kl = k;
+                            jl = j;
+                        }
+                    }
+                }
+                const uint32_t sp = sl + 64u * js;
+                if (need_box(sbox + (size_t)sp * 2 * D, smin[sp])) visit_super(sp, 0xFFFFFFFFu);
+            }
+            goto done;
+        }
+    }
+    {
     const uint32_t chunks = (S + 63) / 64, home_c = home_s / 64;
     for (uint32_t st = 0; st < 2 * chunks; ++st) {
         const int64_t c64 = (st & 1u) ? (int64_t)home_c - (int64_t)((st + 1) / 2) : (int64_t)home_c + (int64_t)(st / 2);
@@ -686,6 +790,8 @@ __global__ __launch_bounds__(kQBlock) void group_kernel(const float* __restrict_
             visit_super((uint32_t)c64 * 64 + b, 0xFFFFFFFFu);
         }
     }
+    }
+done:
 #pragma unroll
     for (int q = 0; q < QG; ++q) {
         if (g0 + q >= q_count) break;
