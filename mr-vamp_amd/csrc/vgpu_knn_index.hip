@@ -393,7 +393,9 @@ constexpr int kSuper = 64;  // tiles per super-tile
 // VGPU_KNN_ORDER bit 0: super-tiles visited nearest first (their box lower bound over the group's queries, one
 // global order when S <= 64 * kKeySlots) instead of outward by index, each re-checked against the thresholds as
 // they stand when its turn comes -- the lists tighten sooner, so fewer far tiles pass; bit 1: the same for the
-// tiles inside a super-tile.
+// tiles inside a super-tile.  A/B on MI355X (profiles/r05l_ab.log, 2.68M vertices): 200 ms in index order, 214 ms
+// with bit 0, 270 ms with both -- the selection's reductions and the key registers (57 -> 77 / 87 VGPRs: fewer
+// waves) cost more than the tighter lists save; off.
 #ifndef VGPU_KNN_ORDER
 #define VGPU_KNN_ORDER 0
 #endif

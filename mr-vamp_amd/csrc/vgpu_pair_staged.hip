@@ -37,7 +37,14 @@
 #ifndef VGPU_PAIR_BOTH
 #define VGPU_PAIR_BOTH 1
 #endif
-// the combined chunks' bound kernel over 8-lane rake groups (both arms' link centres, 121 tests)
+// source kinds whose arm-pass bound stage runs the mid-sphere tests (vgpu_staged.hh MidKinds)
+#ifndef VGPU_PAIR_MID_KINDS
+#define VGPU_PAIR_MID_KINDS 0u
+#endif
+// the combined chunks' bound kernel over 8-lane rake groups (both arms' link centres, 121 tests): it uses 94 VGPRs
+// (5 waves/EU).  A/B on MI355X (profiles/r05l_pair_ab.log): forced to 6 or 7 waves it runs 8.16-8.23 vs 8.51-8.55
+// ms per composite step but spills 11-26 VGPRs; holding arm A's centres in halves (arm B's FK streamed, and
+// both recomputed, per half) still spilled 3-8 at 6 waves -- kept at 5, spill-free
 #ifndef VGPU_PAIR_BOTH8_WAVES
 #define VGPU_PAIR_BOTH8_WAVES 3
 #endif
@@ -80,14 +87,17 @@ struct PairArmR : PairRakeR {
     static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 0, 0, 2,
                                               0, 0, 0, 1, 1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     static constexpr int kClassWaves[kClasses] = {8, 7, 6};
-    template <class Grp, bool EXT>
+    // validate tails run the Panda's mid-sphere tests in their bound stage, as the single Panda does
+    // (vgpu_staged.hip PandaR::kMidKinds)
+    static constexpr uint32_t kMidKinds = VGPU_PAIR_MID_KINDS;
+    template <class Grp, bool EXT, bool MID = false>
     __device__ static __forceinline__ Mask bound(const float* v, const EnvView& env, const Bases& b)
     {
         constexpr int o = 7 * ARM;
-        return ARM == 0 ? panda_bound_mask<Grp, EXT>(v[o], v[o + 1], v[o + 2], v[o + 3], v[o + 4], v[o + 5], v[o + 6],
-                                                      env, b.x, b.y, b.z)
-                        : panda_bound_mask<Grp, EXT>(v[o], v[o + 1], v[o + 2], v[o + 3], v[o + 4], v[o + 5], v[o + 6],
-                                                      env, b.x2, b.y2, b.z2);
+        return ARM == 0 ? panda_bound_mask<Grp, EXT, MID>(v[o], v[o + 1], v[o + 2], v[o + 3], v[o + 4], v[o + 5],
+                                                           v[o + 6], env, b.x, b.y, b.z)
+                        : panda_bound_mask<Grp, EXT, MID>(v[o], v[o + 1], v[o + 2], v[o + 3], v[o + 4], v[o + 5],
+                                                           v[o + 6], env, b.x2, b.y2, b.z2);
     }
     template <class Grp, bool EXT>
     __device__ static __forceinline__ bool children(int c, const float* v, const EnvView& env, const Bases& b)

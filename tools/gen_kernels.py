@@ -222,7 +222,7 @@ def xform(E: Emitter, R, P, o):
     return out
 
 
-def joint(E: Emitter, fr: dict, A, R_A, P, qoff: int = 0):
+def joint(E: Emitter, fr: dict, A, R_A, P, qoff: int = 0, qname: str = "q"):
     """Apply frame fr's joint after its fixed rotation: returns (Q, P).  Revolute about the unit
     axis a: Q = A (x) (c, s*a) (other components structurally zero; a negative axis negates s).
     Prismatic along a: Q = A, P += R(A) (a*q) (oracle/vamp_oracle.c robot_fk_frames)."""
@@ -232,7 +232,7 @@ def joint(E: Emitter, fr: dict, A, R_A, P, qoff: int = 0):
     d += qoff  # joint variable q<d>: a composite's second arm reads q7..q13
     ax = fr.get("axis", [0.0, 0.0, 1.0])
     if fr.get("jtype") == "prismatic":
-        qv = SV("var", name=f"q{d}")
+        qv = SV("var", name=f"{qname}{d}")
         dq = [SV.zero() if a == 0 else (qv if a > 0 else E.neg(qv)) for a in ax]
         RA = R_A()
         out = []
@@ -242,7 +242,7 @@ def joint(E: Emitter, fr: dict, A, R_A, P, qoff: int = 0):
                 acc = E.add(acc, E.mul(RA[i][k], dq[k]))
             out.append(E.add(P[i], acc))
         return A, out
-    h = E.tmp(f"q{d} * 0.5f")
+    h = E.tmp(f"{qname}{d} * 0.5f")
     c = E.tmp(f"vamp_cos({h.name})")
     sn = E.tmp(f"vamp_sin({h.name})")
     E.flops += 2 * 16
@@ -335,8 +335,8 @@ class RobotGen:
     class Frames:
         """Lazily emitted frame poses (Q, P, R) and bounding centres over one Emitter."""
 
-        def __init__(self, gen, E, qoff=0):
-            self.g, self.E, self.qoff = gen, E, qoff
+        def __init__(self, gen, E, qoff=0, qname="q"):
+            self.g, self.E, self.qoff, self.qname = gen, E, qoff, qname
             self.Q, self.P, self.R, self.bc = {}, {}, {}, {}
             self.built = set()
 
@@ -356,9 +356,9 @@ class RobotGen:
             A = Q[p] if ident else qmul(E, Q[p], qf)
             if fr.get("jtype") == "prismatic":
                 Pt = xform(E, self.R[p], P[p], fr["t"])
-                Q[f], P[f] = joint(E, fr, A, lambda: self.R[p] if ident else qmat(E, A), Pt, self.qoff)
+                Q[f], P[f] = joint(E, fr, A, lambda: self.R[p] if ident else qmat(E, A), Pt, self.qoff, self.qname)
             else:
-                Q[f], _ = joint(E, fr, A, None, None, self.qoff)
+                Q[f], _ = joint(E, fr, A, None, None, self.qoff, self.qname)
                 P[f] = xform(E, self.R[p], P[p], fr["t"])
 
         def rot(self, f):
