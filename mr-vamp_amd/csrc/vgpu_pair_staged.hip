@@ -37,9 +37,11 @@
 #ifndef VGPU_PAIR_BOTH
 #define VGPU_PAIR_BOTH 1
 #endif
-// source kinds whose arm-pass bound stage runs the mid-sphere tests (vgpu_staged.hh MidKinds)
+// source kinds whose arm-pass bound stage runs the mid-sphere tests (vgpu_staged.hh MidKinds): validate tails, as
+// for the single Panda.  A/B on MI355X (profiles/r05m_pair_ab.log, three alternating runs): 8.50-8.60 -> 7.99-8.09
+// ms per 2^20 composite edges
 #ifndef VGPU_PAIR_MID_KINDS
-#define VGPU_PAIR_MID_KINDS 0u
+#define VGPU_PAIR_MID_KINDS ((1u << 3) | (1u << 4))
 #endif
 // the combined chunks' bound kernel over 8-lane rake groups (both arms' link centres, 121 tests): it uses 94 VGPRs
 // (5 waves/EU).  A/B on MI355X (profiles/r05l_pair_ab.log): forced to 6 or 7 waves it runs 8.16-8.23 vs 8.51-8.55

@@ -19,7 +19,7 @@ namespace asmb {
 
 __global__ __launch_bounds__(256) void expand_kernel(const uint32_t* __restrict__ pairs, size_t m, uint32_t n,
                                                      uint32_t* __restrict__ key, uint32_t* __restrict__ val,
-                                                     uint32_t* __restrict__ cnt, uint32_t* __restrict__ bad)
+                                                     uint32_t* __restrict__ bad)
 {
     const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
     if (p >= m) return;
@@ -34,8 +34,19 @@ __global__ __launch_bounds__(256) void expand_kernel(const uint32_t* __restrict_
     val[2 * p] = j;
     key[2 * p + 1] = j;
     val[2 * p + 1] = i;
-    atomicAdd(&cnt[i], 1u);
-    atomicAdd(&cnt[j], 1u);
+}
+
+// offsets from the SORTED keys: off[v] = the first position whose key is >= v (the exclusive scan of the
+// per-vertex counts, without 2m random atomics -- 10 ms of the 2.68M-vertex step in round 4's profile); each
+// position writes the offsets of the vertices between its predecessor's key and its own, the last one the tail
+__global__ __launch_bounds__(256) void bounds_kernel(const uint32_t* __restrict__ key, size_t e, uint32_t n,
+                                                     unsigned long long* __restrict__ off)
+{
+    const size_t p = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (p > e) return;
+    const uint32_t lo = p == 0 ? 0u : key[p - 1] + 1u;  // vertices lo .. hi start at position p
+    const uint32_t hi = p == e ? n : key[p];
+    for (uint32_t v = lo; v <= hi; ++v) off[v] = p;
 }
 
 __global__ __launch_bounds__(256) void widen_kernel(const uint32_t* __restrict__ off32, uint32_t n1,
@@ -99,7 +110,7 @@ size_t vgpu_roadmap_assemble_bytes(uint32_t n, size_t m)
         return 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, tc, (uint32_t*)nullptr, (uint32_t*)nullptr, (int)n + 1) != hipSuccess)
         return 0;
-    return 3 * al256(2 * m * 4) + 2 * al256(((size_t)n + 1) * 4) + al256(16) + al256(std::max(ts, tc));
+    return 3 * al256(2 * m * 4) + 2 * al256(((size_t)n + 1) * 4) + al256(16) + al256(std::max(ts, tc));  // (cnt unused)
 }
 
 // pairs[m][2], offsets[n + 1], adj[2m], component[n] (optional): device memory.  *flags (host) gets
@@ -129,11 +140,12 @@ hipError_t vgpu_launch_roadmap_assemble(uint32_t n, const uint32_t* pairs, size_
     void* work = t;
     const size_t work_bytes = tmp_bytes - (size_t)(t - (char*)tmp);
     hipError_t err;
-    if ((err = hipMemsetAsync(cnt, 0, ((size_t)n + 1) * 4, st)) != hipSuccess) return err;
+    (void)cnt;
+    (void)off32;
     if ((err = hipMemsetAsync(dflag, 0, 16, st)) != hipSuccess) return err;
     if (m) {
         hipLaunchKernelGGL(expand_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, pairs, m, n, key, val,
-                           cnt, dflag);
+                           dflag);
         if ((err = hipGetLastError()) != hipSuccess) return err;
         uint32_t bad = 0;  // an index >= n would send the hooking below out of bounds: fail first
         if ((err = hipMemcpyAsync(&bad, dflag, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return err;
@@ -147,9 +159,7 @@ hipError_t vgpu_launch_roadmap_assemble(uint32_t n, const uint32_t* pairs, size_
             hipSuccess)
             return err;
     }
-    size_t wb = work_bytes;
-    if ((err = hipcub::DeviceScan::ExclusiveSum(work, wb, cnt, off32, (int)n + 1, st)) != hipSuccess) return err;
-    hipLaunchKernelGGL(widen_kernel, dim3((n + 256) / 256), dim3(256), 0, st, off32, n + 1, offsets);
+    hipLaunchKernelGGL(bounds_kernel, dim3((unsigned)((e + 1 + 255) / 256)), dim3(256), 0, st, key2, e, n, offsets);
     if ((err = hipGetLastError()) != hipSuccess) return err;
     if (component) {
         hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, n, component);
