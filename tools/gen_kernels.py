@@ -58,6 +58,8 @@ MID_SELF_LINKS = {"panda_link1": 2, "panda_link2": 2, "panda_link5": 4,
                   # whose children almost never confirm (tools/hitstats.py --fetch, profiles/r04n_hitstats_fetch.json)
                   "head_pan_link": 4, "upperarm_roll_link": 2, "elbow_flex_link": 2, "forearm_roll_link": 2,
                   "base_link": 3, "torso_lift_link": 2, "torso_fixed_link": 2}
+# (finer Fetch clusters -- head 8, upper arm 4, elbow 3, forearm 3, base 6 -- measured slower on MI355X: edge-stage
+# validation 297 -> 346 ms at 2.68M vertices, profiles/r05p_ab.log; the extra mid tests cost more than they filter)
 MID_SELF_CHECKS = [("panda_link1", "panda_link5"), ("panda_link2", "panda_link5"),
                    ("head_pan_link", "upperarm_roll_link"), ("head_pan_link", "elbow_flex_link"),
                    ("head_pan_link", "forearm_roll_link"), ("base_link", "elbow_flex_link"),
