@@ -896,6 +896,7 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
             hd[PC_GNZF] = (float)g.nz;
             hd[PC_GUNIT] = g.unit;
             hd[PC_GCELLS] = hdr_u(g.cells_off);
+            hd[PC_GBRICK] = hdr_u(g.brick);
         }
         if (device) e->pc_grid.push_back(g);
     }

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cmath>
 #include <limits>
 #include <numeric>
@@ -187,6 +188,12 @@ bool capt_grid_plan(const CaptTree& t, size_t cells, CaptGridArgs& g)
         if (ok) break;
         h *= 1.25;
     }
+    // VGPU_CAPT_BRICK=1: cells in 4 x 4 x 4 bricks (counts rounded up to multiples of 4: the grid box grows by < 4
+    // cells per axis; cells beyond the cloud get their bounds like any other)
+    const char* bv = std::getenv("VGPU_CAPT_BRICK");
+    g.brick = (bv && std::atoi(bv) != 0) ? 1u : 0u;
+    if (g.brick)
+        for (int k = 0; k < 3; ++k) n[k] = (n[k] + 3u) & ~3u;
     g.x0 = (float)lo[0];
     g.y0 = (float)lo[1];
     g.z0 = (float)lo[2];

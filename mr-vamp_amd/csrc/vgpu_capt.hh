@@ -35,6 +35,7 @@ struct CaptGridArgs {
     uint32_t nx, ny, nz;
     float unit;
     uint32_t cells_off;
+    uint32_t brick;  // cells in 4 x 4 x 4 bricks (vgpu_device.hh capt_cell_index; counts rounded up to 4)
 };
 
 // Sizes the grid of tree t: the top box grown by r_max + r_point, cubic cells, about `cells`

@@ -67,7 +67,17 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
     const uint32_t cell = blockIdx.x * (uint32_t)kGridBlock + threadIdx.x;
     const uint32_t n_cells = g.nx * g.ny * g.nz;
     if (cell >= n_cells) return;
-    const uint32_t ix = cell % g.nx, iy = (cell / g.nx) % g.ny, iz = cell / (g.nx * g.ny);
+    uint32_t ix, iy, iz;  // the cell whose bounds this thread writes at storage index `cell`
+    if (g.brick) {
+        const uint32_t b = cell >> 6, l = cell & 63u, nbx = g.nx >> 2, nby = g.ny >> 2;
+        ix = (b % nbx) * 4u + (l & 3u);
+        iy = ((b / nbx) % nby) * 4u + ((l >> 2) & 3u);
+        iz = (b / (nbx * nby)) * 4u + (l >> 4);
+    } else {
+        ix = cell % g.nx;
+        iy = (cell / g.nx) % g.ny;
+        iz = cell / (g.nx * g.ny);
+    }
     const double h = 1.0 / (double)g.inv_h;
     const double o[3] = {(double)g.x0, (double)g.y0, (double)g.z0};
     const uint32_t ic[3] = {ix, iy, iz};

@@ -252,8 +252,18 @@ enum : int { HF_X = 0, HF_Y, HF_Z, HF_XS, HF_YS, HF_ZS, HF_XD, HF_YD, HF_XD2, HF
 // float), the bound unit, and cells_off (0 = no grid; one uint2 per cell, x-fastest).
 enum : int {
     PC_TOP = 0, PC_RPOINT = 6, PC_NLOG2 = 7, PC_TESTS, PC_AABBS, PC_STARTS, PC_AFF,
-    PC_GX = 12, PC_GY, PC_GZ, PC_GINVH, PC_GNX, PC_GNY, PC_GNZ, PC_GNXF, PC_GNYF, PC_GNZF, PC_GUNIT, PC_GCELLS
+    PC_GX = 12, PC_GY, PC_GZ, PC_GINVH, PC_GNX, PC_GNY, PC_GNZ, PC_GNXF, PC_GNYF, PC_GNZF, PC_GUNIT, PC_GCELLS,
+    PC_GBRICK  // 1: cells stored in 4 x 4 x 4 bricks (capt_cell_index), 0: x-fastest rows
 };
+// storage index of cell (ix, iy, iz): x-fastest rows, or 4 x 4 x 4 bricks of 64 consecutive cells (brick-major,
+// x-fastest bricks; every count a multiple of 4) -- a sphere's next children fall in the same or a nearby brick
+__host__ __device__ __forceinline__ uint32_t capt_cell_index(uint32_t ix, uint32_t iy, uint32_t iz, uint32_t nx,
+                                                             uint32_t ny, bool brick)
+{
+    if (!brick) return (iz * ny + iy) * nx + ix;
+    return ((((iz >> 2) * (ny >> 2) + (iy >> 2)) * (nx >> 2) + (ix >> 2)) << 6) | ((iz & 3u) << 4) | ((iy & 3u) << 2) |
+           (ix & 3u);
+}
 // Cell bounds are scaled by these before they decide a query (vgpu_capt_grid.hip: the float
 // rounding of the distance and of the bound itself is < 1e-6 relative)
 constexpr float kGridLoFac = 0.9999f, kGridHiFac = 1.0001f;
@@ -522,7 +532,8 @@ __device__ __forceinline__ int capt_decide(const VGPU_CONST float* h, float x, f
         const float fy = (y - h[PC_GY]) * h[PC_GINVH];
         const float fz = (z - h[PC_GZ]) * h[PC_GINVH];
         if (fx >= 0.0f && fy >= 0.0f && fz >= 0.0f && fx < h[PC_GNXF] && fy < h[PC_GNYF] && fz < h[PC_GNZF]) {
-            uint32_t cell = ((uint32_t)fz * hdr_u(h, PC_GNY) + (uint32_t)fy) * hdr_u(h, PC_GNX) + (uint32_t)fx;
+            uint32_t cell = capt_cell_index((uint32_t)fx, (uint32_t)fy, (uint32_t)fz, hdr_u(h, PC_GNX), hdr_u(h, PC_GNY),
+                                            hdr_u(h, PC_GBRICK) != 0u);
             cell = VGPU_DCLAMP(base, cell, hdr_u(h, PC_GNX) * hdr_u(h, PC_GNY) * hdr_u(h, PC_GNZ), DBG_CAPT_CELL);
             const uint2 rec = ((const uint2*)(base + goff))[cell];
             const float rr = r + h[PC_RPOINT];
