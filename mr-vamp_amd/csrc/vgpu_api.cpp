@@ -883,7 +883,9 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
             g.starts_off = (uint32_t)o_starts;
             g.aff_off = (uint32_t)o_aff;
             g.cells_off = (uint32_t)dpos();
-            const size_t hole = (2 * (size_t)g.nx * g.ny * g.nz + 15) & ~(size_t)15;
+            const size_t n_cells = (size_t)g.nx * g.ny * g.nz;
+            g.nodes_off = g.split ? (uint32_t)(g.cells_off + ((n_cells + 15) & ~(size_t)15)) : 0u;
+            const size_t hole = 2 * ((n_cells + 15) & ~(size_t)15);
             if (holes) holes->push_back({blob.size(), hole});
             shift += hole;
             const float gv[] = {g.x0, g.y0, g.z0, g.inv_h};
@@ -897,6 +899,7 @@ static void build_prefix(vgpu_env* e, vgpu_env::Layout& L, std::vector<float>& b
             hd[PC_GUNIT] = g.unit;
             hd[PC_GCELLS] = hdr_u(g.cells_off);
             hd[PC_GBRICK] = hdr_u(g.brick);
+            hd[PC_GNODES] = hdr_u(g.nodes_off);
         }
         if (device) e->pc_grid.push_back(g);
     }

@@ -188,12 +188,18 @@ bool capt_grid_plan(const CaptTree& t, size_t cells, CaptGridArgs& g)
         if (ok) break;
         h *= 1.25;
     }
-    // VGPU_CAPT_BRICK=1: cells in 4 x 4 x 4 bricks (counts rounded up to multiples of 4: the grid box grows by < 4
-    // cells per axis; cells beyond the cloud get their bounds like any other)
+    // cells in 4 x 4 x 4 bricks (counts rounded up to multiples of 4: the grid box grows by < 4 cells per axis;
+    // cells beyond the cloud get their bounds like any other).  A wave of the grid build then walks 64 neighbouring
+    // cells, which reach the same few leaves: 1.75 -> 1.06 ms for the bench cloud's grid, queries unchanged
+    // (profiles/r05q_capt.log).  VGPU_CAPT_BRICK=0 keeps plain x-fastest rows.
     const char* bv = std::getenv("VGPU_CAPT_BRICK");
-    g.brick = (bv && std::atoi(bv) != 0) ? 1u : 0u;
+    g.brick = (bv && std::atoi(bv) == 0) ? 0u : 1u;
     if (g.brick)
         for (int k = 0; k < 3; ++k) n[k] = (n[k] + 3u) & ~3u;
+    // the 16-bit bounds in a plane of their own, the start nodes (read only by undecided queries) in another: half
+    // the cache footprint for the decided queries.  VGPU_CAPT_SPLIT=0 keeps one uint2 per cell.
+    const char* sv = std::getenv("VGPU_CAPT_SPLIT");
+    g.split = (sv && std::atoi(sv) == 0) ? 0u : 1u;
     g.x0 = (float)lo[0];
     g.y0 = (float)lo[1];
     g.z0 = (float)lo[2];

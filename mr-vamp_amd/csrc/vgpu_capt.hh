@@ -36,10 +36,12 @@ struct CaptGridArgs {
     float unit;
     uint32_t cells_off;
     uint32_t brick;  // cells in 4 x 4 x 4 bricks (vgpu_device.hh capt_cell_index; counts rounded up to 4)
+    uint32_t split;      // bounds and nodes in separate planes (PC_GNODES)
+    uint32_t nodes_off;  // the node plane (split), else 0
 };
 
 // Sizes the grid of tree t: the top box grown by r_max + r_point, cubic cells, about `cells`
-// of them (0 = default: 128 per leaf, within [2^12, 2^22]; 8 B each).  false: no grid (empty cloud).
+// of them (0 = default: 128 per leaf, within [2^12, 2^22]; 8 B each: bounds + start node).  false: no grid (empty cloud).
 bool capt_grid_plan(const CaptTree& t, size_t cells, CaptGridArgs& g);
 
 struct Heightfield {

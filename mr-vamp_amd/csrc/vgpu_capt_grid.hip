@@ -30,7 +30,6 @@ namespace vgpu {
 constexpr double kSlack = 1e-3;
 constexpr int kMaxLeaves = 64;
 constexpr int kGridBlock = 256;
-constexpr int kStackDepth = 32;  // a depth-first walk of a tree of depth nlog2 <= 26 holds <= nlog2 + 1 nodes
 
 // the float next to finite f toward -inf / +inf
 __device__ __forceinline__ float next_down(float f)
@@ -61,6 +60,9 @@ __device__ __forceinline__ float round_up(double x)
 // of a few metres) only loosens bounds that are then rounded by a further whole unit (h / 256) -- every
 // bound stays conservative.  The descent and the choice of leaves compare the split values with the
 // double cell bounds, as before.
+// kStackDepth: a depth-first walk of a tree of depth nlog2 holds <= nlog2 + 1 nodes; the launcher takes the 16-deep
+// stack (16 KB of LDS per block instead of 32 KB) for trees of depth < 16.
+template <int kStackDepth>
 __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict__ base, CaptGridArgs g)
 {
     __shared__ uint32_t stk[kStackDepth][kGridBlock];
@@ -163,7 +165,12 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
         lq = lo >= 65535.0 ? 65535u : (uint32_t)fmax(floor(lo) - 1.0, 0.0);
         hq = hi + 1.0 < 65535.0 ? (uint32_t)ceil(hi) + 1u : 0xFFFFu;
     }
-    ((uint2*)(base + g.cells_off))[cell] = make_uint2(lq | (hq << 16), node);
+    if (g.nodes_off) {
+        ((uint32_t*)(base + g.cells_off))[cell] = lq | (hq << 16);
+        ((uint32_t*)(base + g.nodes_off))[cell] = node;
+    } else {
+        ((uint2*)(base + g.cells_off))[cell] = make_uint2(lq | (hq << 16), node);
+    }
 }
 
 }  // namespace vgpu
@@ -173,7 +180,10 @@ extern "C" hipError_t vgpu_launch_capt_grid(float* base, const vgpu::CaptGridArg
     const uint64_t n = (uint64_t)g->nx * g->ny * g->nz;
     if (n == 0) return hipSuccess;
     if (n >= ((uint64_t)1 << 31)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(vgpu::capt_grid_kernel, dim3((unsigned)((n + vgpu::kGridBlock - 1) / vgpu::kGridBlock)),
-                       dim3(vgpu::kGridBlock), 0, st, base, *g);
+    const dim3 grid((unsigned)((n + vgpu::kGridBlock - 1) / vgpu::kGridBlock)), block(vgpu::kGridBlock);
+    if (g->nlog2 < 16)
+        hipLaunchKernelGGL(vgpu::capt_grid_kernel<16>, grid, block, 0, st, base, *g);
+    else
+        hipLaunchKernelGGL(vgpu::capt_grid_kernel<32>, grid, block, 0, st, base, *g);
     return hipGetLastError();
 }

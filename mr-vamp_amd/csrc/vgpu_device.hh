@@ -249,11 +249,13 @@ enum : int { HF_X = 0, HF_Y, HF_Z, HF_XS, HF_YS, HF_ZS, HF_XD, HF_YD, HF_XD2, HF
 // point-cloud (CAPT) header: top lower xyz, top upper xyz, r_point | nlog2, tests_off, aabbs_off,
 // starts_off, aff_off (uint32 bits).  aff = [n_aff][3][8] floats (x8 y8 z8), 16-B aligned.
 // Device copies add the cell grid (vgpu_capt_grid.hip): origin xyz, 1/h, cell counts (uint32 and
-// float), the bound unit, and cells_off (0 = no grid; one uint2 per cell, x-fastest).
+// float), the bound unit, and cells_off (0 = no grid; the cell bounds, see PC_GNODES and capt_cell_index).
 enum : int {
     PC_TOP = 0, PC_RPOINT = 6, PC_NLOG2 = 7, PC_TESTS, PC_AABBS, PC_STARTS, PC_AFF,
     PC_GX = 12, PC_GY, PC_GZ, PC_GINVH, PC_GNX, PC_GNY, PC_GNZ, PC_GNXF, PC_GNYF, PC_GNZF, PC_GUNIT, PC_GCELLS,
-    PC_GBRICK  // 1: cells stored in 4 x 4 x 4 bricks (capt_cell_index), 0: x-fastest rows
+    PC_GBRICK,  // 1: cells stored in 4 x 4 x 4 bricks (capt_cell_index), 0: x-fastest rows
+    PC_GNODES   // 0: one uint2 {bounds, node} per cell; else the offset of a separate node plane (one uint32 per
+                // cell) and cells_off holds the bounds alone, one uint32 per cell
 };
 // storage index of cell (ix, iy, iz): x-fastest rows, or 4 x 4 x 4 bricks of 64 consecutive cells (brick-major,
 // x-fastest bricks; every count a multiple of 4) -- a sphere's next children fall in the same or a nearby brick
@@ -535,15 +537,16 @@ __device__ __forceinline__ int capt_decide(const VGPU_CONST float* h, float x, f
             uint32_t cell = capt_cell_index((uint32_t)fx, (uint32_t)fy, (uint32_t)fz, hdr_u(h, PC_GNX), hdr_u(h, PC_GNY),
                                             hdr_u(h, PC_GBRICK) != 0u);
             cell = VGPU_DCLAMP(base, cell, hdr_u(h, PC_GNX) * hdr_u(h, PC_GNY) * hdr_u(h, PC_GNZ), DBG_CAPT_CELL);
-            const uint2 rec = ((const uint2*)(base + goff))[cell];
+            const uint32_t noff = hdr_u(h, PC_GNODES);
+            const uint32_t rec = noff ? ((const uint32_t*)(base + goff))[cell] : ((const uint2*)(base + goff))[cell].x;
             const float rr = r + h[PC_RPOINT];
             const float rc = rr * rr;
-            const float lo = (float)(rec.x & 0xFFFFu) * h[PC_GUNIT];
+            const float lo = (float)(rec & 0xFFFFu) * h[PC_GUNIT];
             if (rc < lo * lo * kGridLoFac) return 0;
-            const uint32_t hq = rec.x >> 16;
+            const uint32_t hq = rec >> 16;
             const float hi = (float)hq * h[PC_GUNIT];
             if (hq != 0xFFFFu && rc > hi * hi * kGridHiFac) return 1;
-            node = rec.y;
+            node = noff ? ((const uint32_t*)(base + noff))[cell] : ((const uint2*)(base + goff))[cell].y;
         }
     }
     return 2;
