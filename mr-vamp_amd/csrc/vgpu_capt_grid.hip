@@ -126,14 +126,15 @@ __global__ __launch_bounds__(kGridBlock) void capt_grid_kernel(float* __restrict
                 const float* v = aff + 24u * j;
 #pragma unroll
                 for (int l = 0; l < 8; ++l) {
+                    // no finiteness test: the +inf padding gives dn = df = +inf (no effect on either min), and a
+                    // NaN coordinate gives dn = 0 (max ignores NaN: lo only shrinks) and df = NaN (min ignores it)
                     const float p[3] = {v[l], v[8 + l], v[16 + l]};
-                    if (!(__builtin_isfinite(p[0]) && __builtin_isfinite(p[1]) && __builtin_isfinite(p[2]))) continue;
                     float dn = 0.0f, df = 0.0f;
 #pragma unroll
                     for (int k = 0; k < 3; ++k) {
                         const float a = Lf[k] - p[k], b = p[k] - Uf[k];
-                        const float near = fmaxf(fmaxf(a, b), 0.0f);
-                        const float far = fmaxf(fabsf(p[k] - Lf[k]), fabsf(p[k] - Uf[k]));
+                        const float near = fmaxf(fmaxf(a, b), 0.0f);  // v_max3
+                        const float far = fmaxf(fabsf(a), fabsf(b));   // |p - Lf|, |p - Uf|: abs source modifiers
                         dn = __builtin_fmaf(near, near, dn);
                         df = __builtin_fmaf(far, far, df);
                     }
