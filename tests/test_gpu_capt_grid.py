@@ -44,24 +44,29 @@ def boundary_queries(pts, n, seed):
     return np.concatenate([c, c, c]), np.concatenate([r, r2, big])
 
 
-def check(vamp, oracle, pts, c, r, cells=None):
-    old = os.environ.get("VGPU_CAPT_GRID_CELLS")
+def check(vamp, oracle, pts, c, r, cells=None, layout=None):
+    """layout: {"VGPU_CAPT_BRICK": "0"|"1", "VGPU_CAPT_SPLIT": "0"|"1"} (None: the defaults, bricks + split)"""
+    sets = {"VGPU_CAPT_GRID_CELLS": None if cells is None else str(cells), **(layout or {})}
+    old = {k: os.environ.get(k) for k in sets}
     try:
-        if cells is None:
-            os.environ.pop("VGPU_CAPT_GRID_CELLS", None)
-        else:
-            os.environ["VGPU_CAPT_GRID_CELLS"] = str(cells)
+        for k, v in sets.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         env = vamp.Environment()
         env.add_pointcloud(pts, R_MIN, R_MAX, R_POINT)
         got = env.pointcloud_collides(c, r, simd=True)
     finally:
-        if old is None:
-            os.environ.pop("VGPU_CAPT_GRID_CELLS", None)
-        else:
-            os.environ["VGPU_CAPT_GRID_CELLS"] = old
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     want = oracle.Capt(pts, R_MIN, R_MAX, R_POINT).collides(c, r, simd=True)
     bad = np.nonzero(got != want)[0]
-    assert len(bad) == 0, f"cells={cells}: {len(bad)} mismatches, first {bad[:5]} c={c[bad[:3]]} r={r[bad[:3]]}"
+    assert len(bad) == 0, (f"cells={cells} layout={layout}: {len(bad)} mismatches, first {bad[:5]} "
+                           f"c={c[bad[:3]]} r={r[bad[:3]]}")
     return got
 
 
@@ -100,3 +105,28 @@ def test_grid_degenerate_clouds(vamp, oracle, shape):
     c, r = boundary_queries(pts, 4096, seed=2)
     check(vamp, oracle, pts, c, r)
     check(vamp, oracle, pts, c, r, cells=0)
+
+
+# the grid's storage layouts (vgpu_capt.cpp capt_grid_plan): x-fastest rows or 4 x 4 x 4 bricks, one uint2
+# {bounds, node} per cell or separate bound / node planes -- the same answers under each
+@pytest.mark.parametrize("brick,split", [("0", "0"), ("0", "1"), ("1", "0"), ("1", "1")])
+def test_grid_layouts(vamp, oracle, brick, split):
+    layout = {"VGPU_CAPT_BRICK": brick, "VGPU_CAPT_SPLIT": split}
+    pts = cage_points()
+    c, r = boundary_queries(pts, 1 << 14, seed=13)
+    check(vamp, oracle, pts, c, r, layout=layout)
+    check(vamp, oracle, pts, c, r, cells=4096, layout=layout)
+    far = (cage_points(2000, seed=4) + np.array([1000.0, -700.0, 30.0], F)).astype(F)
+    c, r = boundary_queries(far, 4096, seed=2)
+    check(vamp, oracle, far, c, r, layout=layout)
+
+
+def test_grid_deep_tree(vamp, oracle):
+    """40k points: a tree of depth 16, whose grid build walks with the 32-deep LDS stack (trees of depth < 16
+    take the 16-deep one)"""
+    pts = cage_points(40000, seed=21)
+    c, r = boundary_queries(pts, 1 << 14, seed=17)
+    got = check(vamp, oracle, pts, c, r)
+    assert 0.05 < got.mean() < 0.99
+    c2, r2 = raw_queries(1 << 15, seed=19)
+    check(vamp, oracle, pts, c2, r2)
