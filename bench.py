@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--base", default="000", choices=["000", "220"],
                     help="validate: PandaBase<0,0,0> (the headline) or the fork's default Panda (2,2,0) "
                          "(robots/panda_grid.hh:39)")
+    ap.add_argument("--robot", default="panda", choices=["panda", "panda_pair"],
+                    help="rrtc: the Panda on the MBM table_pick problems (configs[0]) or the two-Panda composite "
+                         "(configs[4]'s planner half)")
     ap.add_argument("--scene", default="cage", choices=["cage", "table_pick"],
                     help="validate: the 14-sphere cage (the headline) or MotionBenchMaker table_pick_panda scene0001 "
                          "(tests/golden/panda_table_pick.npz)")
@@ -369,7 +372,6 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     qs = op.robot_scale("fetch", op.halton(8, ks))
     _, _, _, fl = op.robot_fkcc("fetch", oenv, qs, stats=True)
     f_sample = float(fl.mean())
-    achieved = f_sample * n / (kern_ms * 1e-3) / 1e12
     cpu = None
     parity = None
     if not a.no_cpu and world == 1:
@@ -413,13 +415,13 @@ def run_fetch_prm(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                    "robot": "Fetch", "draws_total": a.draws, "vertices": int(n_vertices),
                    "parallelism": f"dp{world} (contiguous draw ranges, one all-gather)"},
         "roofline": {"kernel": "vgpu_sample_fkcc: staged Halton + scale + fkcc (bound / queue / children kernels)",
-                     "bound": "valu", "achieved": achieved,
-                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
-                     **traffic_fields("fetch_prm", n), "kernel_ms": kern_ms, "algorithmic_flops_per_sample": f_sample,
+                     "bound": "valu", "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     **utilisation("fetch_prm" if world == 1 else None, n, step_ev_ms, f_sample * n),
+                     **traffic_fields("fetch_prm", n), "kernel_ms": step_ev_ms, "sample_fkcc_kernel_ms": kern_ms,
+                     "algorithmic_flops_per_sample": f_sample,
                      "algorithmic_bytes_per_sample": 8 * 4 + 1, "step_ms_events": step_ev_ms,
-                     "frac_meaning": FRAC_MEANING,
-                     "executed": executed_record("fetch_prm", n, step_ev_ms) if world == 1 else None,
-                     "executed_note": "over the whole step (fused sample + fkcc, compaction, index conversion)"},
+                     "utilisation_note": "over the whole step (fused sample + fkcc, compaction, index conversion), the "
+                                         "span the step profile covers"},
         "cpu_baseline": cpu,
         "parity": parity,
     }
@@ -657,12 +659,15 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                    "parallelism": f"dp{world} (query ranges of equal prefix work, one all-gather)"},
         "roofline": {"kernel": "validate_motion of the step's candidate edges: the Fetch staged bound / queue / "
                                "children kernels (rank 0's candidates)", "bound": "valu",
-                     "achieved": val_tflops, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": val_tflops / FP32_PEAK_TFLOPS, "kernel_ms": validate_ms,
+                     "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", **utilisation(prof_w, n, step_ev_ms),
+                     "reference_work_achieved": val_tflops, "reference_work_frac": val_tflops / FP32_PEAK_TFLOPS,
+                     "reference_work_note": "the candidate validation's reference float ops over its own kernel time "
+                                            "(validate_ms); `frac` is the executed FP32 of the whole step",
+                     "kernel_ms": step_ev_ms, "validate_kernel_ms": validate_ms,
                      "algorithmic_flops_per_candidate_edge": f_cand, "candidate_edges": candidates,
                      "algorithmic_bytes_per_candidate_edge": 2 * dim * 4 + 1, **traffic_fields(prof_w, n),
                      "traffic_note": "traffic = HBM bytes of the whole step (all its kernels) from the committed profile",
-                     "step_kernel_ms_events": step_ev_ms, "frac_meaning": FRAC_MEANING,
+                     "step_kernel_ms_events": step_ev_ms,
                      "knn_index": knn_roof,
                      "knn_brute": {"ms": knn_ms, "achieved_tflops": knn_brute_tflops,
                                    "algorithmic_flops_per_vertex_pair": 24, "vertex_pairs_rank0": pairs_scanned,
@@ -670,8 +675,7 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
                                            "from 65536 vertices), timed for the index == brute force check"},
                      "knn_ms": knn, "knn_mode_in_step": "index" if n >= 65536 else "brute",
                      "index_equals_brute": index_equals_brute,
-                     "executed": executed_record(prof_w, n, step_ev_ms),
-                     "executed_note": "over the whole step"},
+                     "utilisation_note": "frac / executed over the whole step (every kernel the step profile holds)"},
         "cpu_baseline": cpu,
         "parity": parity,
         "phases": phases,
@@ -769,9 +773,56 @@ def executed_record(workload, units, kernel_ms):
                              "this run's kernel time)"}
 
 
-FRAC_MEANING = ("reference-work throughput: the float ops the reference executes for these inputs (its early exits "
-                "included, counted by the instrumented oracle) / kernel time / FP32 peak -- work the GPU skips (the "
-                "wrist gate, bounding-first inter-arm tests) still counts; `executed` is the hardware utilisation")
+FRAC_MEANING = ("executed FP32 utilisation: 64 x (ADD + MUL + 2 FMA) FP32 VALU instructions per unit from the committed PMC "
+                "record of this workload's step (profiles/rNN_prof_<workload>.json, same build) x this run's units / this "
+                "run's kernel time / the FP32 peak -- what the hardware executed, bounded by 1.  The reference's own work "
+                "(its float ops for these inputs, early exits included, counted by the instrumented oracle) over the same "
+                "time is `reference_work_frac`: it counts work the GPU legitimately skips (mid spheres, the wrist gate, "
+                "never-firing self checks, the obstacle prefilter), so it measures algorithmic savings plus speed and may "
+                "exceed 1")
+
+
+def utilisation(workload, units, kernel_ms, ref_flops=None):
+    """The roofline's rate fields: `achieved` / `frac` = EXECUTED FP32 (bounded by 1) from the
+    committed PMC record of the same workload's step over this run's kernel time; `frac_at_profile_time` = the same
+    count over the record's own kernel time (what the record alone recomputes to); `reference_work_achieved` /
+    `reference_work_frac` = the reference's float ops (ref_flops per launch) over this run's kernel time."""
+    ex = executed_record(workload, units, kernel_ms) if workload else None
+    _, rec = prof_record(workload) if workload else (None, None)
+    out = {"achieved": None, "frac": None, "frac_at_profile_time": None}
+    if ex:
+        out["frac"] = ex["fp32_exec_frac"]
+        out["achieved"] = ex["fp32_exec_frac"] * FP32_PEAK_TFLOPS
+        if rec and rec.get("kernel_ms_per_call"):
+            out["frac_at_profile_time"] = rec["fp32_ops_per_call"] / (rec["kernel_ms_per_call"] * 1e-3) / 1e12 / \
+                FP32_PEAK_TFLOPS
+    if ref_flops is not None and kernel_ms:
+        ra = ref_flops / (kernel_ms * 1e-3) / 1e12
+        out["reference_work_achieved"] = ra
+        out["reference_work_frac"] = ra / FP32_PEAK_TFLOPS
+    out["frac_meaning"] = FRAC_MEANING
+    out["executed"] = ex
+    return out
+
+
+def phase_utilisation(workload, units, phase_ms):
+    """executed FP32 fraction per validate phase: the record's per-kernel FP32 counts split by source kind (head:
+    the lead, bound, children, count and queue kernels of SrcHeadT; tail: those of SrcTailT), scaled to this run's
+    units, over this run's phase times (HIP events inside the library).  Bounded by 1 like `frac`."""
+    _, rec = prof_record(workload)
+    if not rec or not rec.get("kernels"):
+        return None
+    fp = {"head": 0.0, "tail": 0.0}
+    for name, k in rec["kernels"].items():
+        ops = 64.0 * (k.get("SQ_INSTS_VALU_ADD_F32", 0) + k.get("SQ_INSTS_VALU_MUL_F32", 0) +
+                      2 * k.get("SQ_INSTS_VALU_FMA_F32", 0))
+        if "SrcHeadT" in name:
+            fp["head"] += ops
+        elif "SrcTailT" in name:
+            fp["tail"] += ops
+    scale = units / rec["units_per_call"]
+    return {p: (fp[p] * scale / (phase_ms[p] * 1e-3) / 1e12 / FP32_PEAK_TFLOPS if phase_ms.get(p) else None)
+            for p in fp}
 
 
 def contract_line(a, world, wall_max, units_all, metric, unit, scaling, data, config, roofline, cpu):
@@ -860,8 +911,6 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     s_np, g_np = starts[:256].cpu().numpy(), goals[:256].cpu().numpy()
     fl = op.pair_validate_flops(oenv, s_np, g_np)  # executed float ops per edge, reference semantics
     f_edge = float(np.mean(fl))
-    kern_s = kern_ms * 1e-3
-    achieved = f_edge * E / kern_s / 1e12
     cpu = None
     parity = None
     if not a.no_cpu and world == 1:
@@ -897,10 +946,10 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
          "edge_valid_fraction": float(okd.float().mean().item()),
          "parallelism": f"dp{world} (independent edge shards, no collective)"},
         {"kernel": "pair_validate_head/tail kernels (one validate_motions call)", "bound": "valu",
-         "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS,
+         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", **utilisation("pair" if not strong else None, E, kern_ms,
+                                                                     f_edge * E),
          **traffic_fields("pair", E), "algorithmic_flops_per_edge": f_edge, "kernel_ms": kern_ms,
-         "step_ms_wall": wall / a.steps * 1e3, "frac_meaning": FRAC_MEANING,
-         "executed": executed_record("pair", E, kern_ms) if not strong else None},
+         "step_ms_wall": wall / a.steps * 1e3},
         cpu)
     line["counting"] = "rake_early_exit (8 x rake blocks the reference evaluates)"
     line["value_full_mask_count"] = units_full_all * a.steps / wall_max
@@ -908,15 +957,30 @@ def run_pair(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     emit(line)
 
 
-def run_rrtc(a, torch, dist, rank, world, dev, stream, ctx, vamp):
-    """BASELINE configs[0] (SURVEY §8(d) config 1): Panda RRT-Connect (planning/rrtc.hh) on the
-    MotionBenchMaker table_pick problems (scene + request 1..16, resolved into
-    tests/golden/panda_table_pick_problems.npz), CPU only -- the planner and its validate_vector
-    checks on the CPU rake, one core, RRTCSettings range 1.0 / 1e6 iterations, Halton<7> reset per
-    problem (scripts/evaluate_mbm.py:95-96), PandaBase<0,0,0> (the scenes are origin-centred) and
-    the fork's default Panda (2,2,0) on problem 1.  One step = one solve of every problem; the
-    value is the median planning time (PlanningResult.nanoseconds).  Every solved path's segments
-    are re-checked on the GPU (vgpu_validate_motions) against the CPU rake.  N ranks = replicas."""
+def RRTC_SETTINGS(vamp):
+    """RRTCSettings of the MBM runs: range 1.0, 1e6 iterations / samples (src/vamp/constants.py:1,49-55)"""
+    return vamp.RRTCSettings(range=1.0, max_iterations=1000000, max_samples=1000000)
+
+
+def rrtc_problems(vamp, robot_name):
+    """(environments, starts, goals, robot, description) of the rrtc workload.
+    panda: the 16 MotionBenchMaker table_pick problems (scene + request 1..16, resolved into
+    tests/golden/panda_table_pick_problems.npz), one environment each, PandaBase<0,0,0>.
+    panda_pair: configs[4]'s planner half -- 16 composite problems on configs[4]'s scene (a table and three spheres,
+    pair_scene_env), start and goal collision-free composite configurations whose straight edge is invalid, drawn
+    from a seeded uniform stream and filtered by the CPU rake (the same draws as tests/test_rrtc.py pair_problems)."""
+    if robot_name == "panda_pair":
+        env, _ = pair_scene_env(vamp)
+        robot = vamp.panda_pair
+        rng = np.random.default_rng(41)
+        q = robot.scale_configuration(rng.random((40 * 16, 14), dtype=np.float32))
+        q = q[robot.cpu_fkcc_batch(q, env)]
+        s, g = q[0::2][:8 * 16], q[1::2][:8 * 16]
+        m = min(len(s), len(g))
+        ok, _, _ = robot.cpu_validate_batch(s[:m], g[:m], env)
+        hard = np.nonzero(~ok)[0][:16]
+        return [env] * 16, list(s[hard]), list(g[hard]), robot, \
+            "configs[4] composite: 16 problems on the table + 3 spheres scene (straight edge invalid)"
     fx = np.load(os.path.join(ROOT, "tests", "golden", "panda_table_pick_problems.npz"), allow_pickle=False)
     P = int(fx["n_problems"])
     envs, starts, goals = [], [], []
@@ -932,8 +996,25 @@ def run_rrtc(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         envs.append(env)
         starts.append(fx[f"p{k}_start"])
         goals.append(fx[f"p{k}_goal"])
-    settings = vamp.RRTCSettings(range=1.0, max_iterations=1000000, max_samples=1000000)
-    runs = [(vamp.panda_0_0, k) for k in range(P)] + [(vamp.panda, 0)]
+    return envs, starts, goals, vamp.panda_0_0, "MBM table_pick_panda scene/request 0001-0016"
+
+
+def run_rrtc(a, torch, dist, rank, world, dev, stream, ctx, vamp):
+    """BASELINE configs[0] (SURVEY §8(d) config 1): Panda RRT-Connect (planning/rrtc.hh) on the
+    MotionBenchMaker table_pick problems (scene + request 1..16, resolved into
+    tests/golden/panda_table_pick_problems.npz), CPU only -- the planner and its validate_vector
+    checks on the CPU rake, one core, RRTCSettings range 1.0 / 1e6 iterations, Halton<7> reset per
+    problem (scripts/evaluate_mbm.py:95-96), PandaBase<0,0,0> (the scenes are origin-centred) and
+    the fork's default Panda (2,2,0) on problem 1.  One step = one solve of every problem; the
+    value is the median planning time (PlanningResult.nanoseconds).  Every solved path's segments
+    are re-checked on the GPU (vgpu_validate_motions) against the CPU rake -- that batch is the line's
+    roofline (HIP events, its step profile profiles/rNN_prof_rrtc.json).  N ranks = replicas.
+    --robot panda_pair: configs[4]'s planner half, RRT-Connect on the two-Panda composite (rrtc_problems)."""
+    pair = a.robot == "panda_pair"
+    envs, starts, goals, robot0, desc = rrtc_problems(vamp, a.robot)
+    P = len(starts)
+    settings = RRTC_SETTINGS(vamp)
+    runs = [(robot0, k) for k in range(P)] + ([] if pair else [(vamp.panda, 0)])
     results = []
 
     def step():
@@ -953,35 +1034,68 @@ def run_rrtc(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     owner = np.concatenate([np.full(len(r.path) - 1, i) for i, r in enumerate(results[:P]) if r.solved])
     gpu_ok = np.zeros(len(seg_s), bool)
     cpu_ok = np.zeros(len(seg_s), bool)
-    for i in range(P):
-        m = owner == i
+    groups = [np.ones(len(seg_s), bool)] if pair else [owner == i for i in range(P)]
+    for i, m in enumerate(groups):
         if m.any():
-            gpu_ok[m] = vamp.panda_0_0.validate_batch(seg_s[m], seg_g[m], envs[i], ctx)[0]
-            cpu_ok[m] = vamp.panda_0_0.cpu_validate_batch(seg_s[m], seg_g[m], envs[i], threads=1)[0]
+            gpu_ok[m] = robot0.validate_batch(seg_s[m], seg_g[m], envs[i], ctx)[0]
+            cpu_ok[m] = robot0.cpu_validate_batch(seg_s[m], seg_g[m], envs[i], threads=1)[0]
+    # the roofline: the GPU leg's batch (all segments of the composite; problem 1's for the Panda, one scene per
+    # problem) resident in HBM, HIP events on the launch stream
+    m0 = groups[0]
+    ds, dg = torch.from_numpy(seg_s[m0]).to(dev), torch.from_numpy(seg_g[m0]).to(dev)
+    E = int(m0.sum())
+    okd = torch.empty(E, dtype=torch.uint8, device=dev)
+    nbd = torch.empty(E, dtype=torch.int32, device=dev)
+    for _ in range(3):
+        robot0.validate_device(ds.data_ptr(), dg.data_ptr(), E, envs[0], okd.data_ptr(), nbd.data_ptr(), ctx)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(20):
+        robot0.validate_device(ds.data_ptr(), dg.data_ptr(), E, envs[0], okd.data_ptr(), nbd.data_ptr(), ctx)
+    e1.record(stream)
+    torch.cuda.synchronize(dev)
+    seg_ms = e0.elapsed_time(e1) / 20
+    prof_w = "rrtc_pair" if pair else "rrtc"
+    roof = {"kernel": "vgpu_validate_motions of the solved paths' segments (the line's GPU leg), "
+                      + ("all 16 problems' segments, one batch" if pair else "problem 1's segments"),
+            "bound": "latency (a few hundred edges: far below one wave per CU)", "peak": FP32_PEAK_TFLOPS,
+            "unit": "TFLOP/s", **utilisation(prof_w, E, seg_ms), **traffic_fields(prof_w, E), "kernel_ms": seg_ms,
+            "segments": E, "algorithmic_bytes_per_segment": 2 * robot0.dimension() * 4 + 1 + 4}
     med_us = float(np.median(ns)) / 1e3
-    b220 = results[P]
     line = {
-        "metric": "Panda MBM RRT-Connect planning time, median (CPU rake)", "value": med_us, "unit": "us",
+        "metric": ("2x Panda composite RRT-Connect planning time, median (CPU rake)" if pair else
+                   "Panda MBM RRT-Connect planning time, median (CPU rake)"), "value": med_us, "unit": "us",
         "n_gpus": world, "steps": a.steps, "warmup": a.warmup, "ms_per_step": wall_max / a.steps * 1e3,
-        "higher_is_better": False, "scaling": "replicas", "vs_baseline": med_us / 35.0, "dtype": "f32",
-        "data": "MotionBenchMaker table_pick_panda scene/request 0001-0016 (resources/panda/problems.tar.bz2, resolved "
-                "into tests/golden/panda_table_pick_problems.npz)",
-        "config": {"workload": f"BASELINE configs[0]: Panda 7-DOF RRT-Connect, {P} MBM table_pick problems, CPU only",
-                   "robot": "PandaBase<0,0,0> (+ Panda (2,2,0) on problem 1)", "planner": "RRTC<Panda, 8, 32>",
-                   "settings": "range 1.0, dynamic domain, balanced, 1e6 iterations/samples, Halton<7> reset per problem",
-                   "parallelism": "one core per problem (replicas over ranks)"},
-        "baseline_note": "vs_baseline = median / 35 us, the reference README's median over all MBM problems on one "
-                         "desktop core (BASELINE.md); this run: table_pick only, GPU box host core",
+        "higher_is_better": False, "scaling": "replicas", "vs_baseline": None if pair else med_us / 35.0,
+        "dtype": "f32",
+        "data": ("synthetic (seeded uniform composite configurations on configs[4]'s scene)" if pair else
+                 "MotionBenchMaker table_pick_panda scene/request 0001-0016 (resources/panda/problems.tar.bz2, resolved "
+                 "into tests/golden/panda_table_pick_problems.npz)"),
+        "config": ({"workload": f"BASELINE configs[4] planner: 2x Panda composite (14-DOF) RRT-Connect, {desc}",
+                    "robot": "panda_pair (PandaBase<0,0,0> + PandaBase<100,0,0>)", "planner": "RRTC<PandaPair, 8, 32>",
+                    "settings": "range 1.0, dynamic domain, balanced, 1e6 iterations/samples, Halton<14> reset per problem",
+                    "parallelism": "one core per problem (replicas over ranks)"} if pair else
+                   {"workload": f"BASELINE configs[0]: Panda 7-DOF RRT-Connect, {P} MBM table_pick problems, CPU only",
+                    "robot": "PandaBase<0,0,0> (+ Panda (2,2,0) on problem 1)", "planner": "RRTC<Panda, 8, 32>",
+                    "settings": "range 1.0, dynamic domain, balanced, 1e6 iterations/samples, Halton<7> reset per problem",
+                    "parallelism": "one core per problem (replicas over ranks)"}),
         "problems": [{"problem": k + 1, "solved": bool(r.solved), "ns": int(r.nanoseconds), "iterations": int(r.iterations),
                       "path_len": int(len(r.path)), "cost": float(r.cost), "trees": list(r.size)}
                      for k, r in enumerate(results[:P])],
-        "panda_2_2_0_problem1": {"solved": bool(b220.solved), "ns": int(b220.nanoseconds),
-                                  "iterations": int(b220.iterations)},
         "solved": int(sum(r.solved for r in results[:P])), "iterations_median": float(np.median(its)),
         "path_segments": {"count": int(len(seg_s)), "gpu_valid": int(gpu_ok.sum()),
                           "gpu_vs_cpu_rake_mismatches": int((gpu_ok != cpu_ok).sum())},
+        "roofline": roof,
         "cpu_baseline": None, "cpu_model": cpu_model(),
     }
+    if pair:
+        line["baseline_note"] = "no reference counterpart (the reference has no composite robot, SURVEY §0 finding 10)"
+    else:
+        line["baseline_note"] = ("vs_baseline = median / 35 us, the reference README's median over all MBM problems on one "
+                                 "desktop core (BASELINE.md); this run: table_pick only, GPU box host core")
+        b220 = results[P]
+        line["panda_2_2_0_problem1"] = {"solved": bool(b220.solved), "ns": int(b220.nanoseconds),
+                                        "iterations": int(b220.iterations)}
     emit(line)
 
 
@@ -1060,8 +1174,6 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     qs = q[:2048].cpu().numpy()
     _, _, _, fl = op.fkcc(oenv, qs, (0, 0, 0), stats=True)
     f_cfg = float(fl.mean())
-    kern_s = kern_ms * 1e-3
-    achieved = f_cfg * N / kern_s / 1e12
     cpu = None
     parity = None
     if not a.no_cpu and world == 1:
@@ -1092,11 +1204,10 @@ def run_capt(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         {"workload": f"BASELINE configs[2]: Panda 7-DOF vs 10k-point CAPT, {N} configurations per GPU",
          "robot": "PandaBase<0,0,0>", "configs_per_gpu": N, "valid_fraction": float(ok.float().mean().item()),
          "parallelism": f"dp{world} (independent shards, no collective)"},
-        {"kernel": "fkcc (staged, point-cloud ext path)", "bound": "valu", "achieved": achieved,
-         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": achieved / FP32_PEAK_TFLOPS, **tf,
+        {"kernel": "fkcc (staged, point-cloud ext path)", "bound": "valu",
+         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s", **utilisation("capt", N, kern_ms, f_cfg * N), **tf,
          "algorithmic_bytes_per_config": 7 * 4 + 1, "algorithmic_flops_per_config": f_cfg, "kernel_ms": kern_ms,
-         "step_ms_wall": wall / a.steps * 1e3, "frac_meaning": FRAC_MEANING,
-         "executed": executed_record("capt", N, kern_ms),
+         "step_ms_wall": wall / a.steps * 1e3,
          "note": "latency-bound gathers, not FLOPs: the cell grid (vgpu_capt_grid.hip) decides most sphere queries "
                  "with one dependent 8-B load after the sphere's FK; undecided ones are queued per wave in LDS and "
                  "resolved a full wave at a time (descent from the cell's node, leaf box, affordance scan: "
@@ -1291,9 +1402,8 @@ def main():
         tail_items = c_ok_head_items(c_nb, c_ne)
         backstep_ops = 56.0 * float((tail_items * (tail_items + 1) // 2).sum()) / max(1, len(c_nb))  # 7 rows x 8 lanes
         achieved = f_head * E / (head_ms * 1e-3) / 1e12
-        achieved_step = (f_head + f_tail) * E / (kern_ms * 1e-3) / 1e12
-        prof_w = {("B", "000", "cage"): "validate", ("A", "000", "cage"): "validate_setA"}.get((a.edge_set, a.base,
-                                                                                                a.scene))
+        prof_w = {("B", "000", "cage"): "validate", ("A", "000", "cage"): "validate_setA",
+                  ("B", "000", "table_pick"): "validate_table_pick"}.get((a.edge_set, a.base, a.scene))
         tf = traffic_fields(prof_w, E) if prof_w and not strong else {"traffic": None, "traffic_source": None}
         cpu = None
         parity = None
@@ -1343,10 +1453,9 @@ def main():
                 "kernel": "validate_motions step: staged bound/queue/children kernels of head and tail "
                           "(vgpu_staged.hip), one call",
                 "bound": "valu",
-                "achieved": achieved_step,
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
-                "frac": achieved_step / FP32_PEAK_TFLOPS,
+                **utilisation(prof_w if not strong else None, E, kern_ms, (f_head + f_tail) * E),
                 **tf,
                 "traffic_measured_in_run": False,
                 "algorithmic_flops_per_launch": (f_head + f_tail) * E,
@@ -1358,10 +1467,10 @@ def main():
                 "backstep_subtract_flops_per_edge": backstep_ops,
                 "backstep_frac_of_tail": backstep_ops / max(f_tail, 1e-9),
                 "phase_ms": {"head": head_ms, "scan_and_count": scan_ms, "tail": tail_ms},
-                "phase_frac": {"head": achieved / FP32_PEAK_TFLOPS,
-                               "tail": f_tail * E / (max(tail_ms, 1e-9) * 1e-3) / 1e12 / FP32_PEAK_TFLOPS},
-                "frac_meaning": FRAC_MEANING,
-                "executed": executed_record(prof_w, E, kern_ms) if prof_w and not strong else None,
+                "phase_frac": phase_utilisation(prof_w, E, {"head": head_ms, "tail": tail_ms})
+                if prof_w and not strong else None,
+                "phase_reference_work_frac": {"head": achieved / FP32_PEAK_TFLOPS,
+                                              "tail": f_tail * E / (max(tail_ms, 1e-9) * 1e-3) / 1e12 / FP32_PEAK_TFLOPS},
             },
             "roofline_hbm_fk": fk_leg,
             "full_mask": full_mask,

@@ -42,6 +42,7 @@ extern "C" {
 #define VGPU_ERR_OOM (-3)
 #define VGPU_ERR_UNSUPPORTED (-4)
 #define VGPU_ERR_RSQRT (-5)
+#define VGPU_ERR_INTERNAL (-6) /* an unexpected C++ exception inside the library (none crosses this ABI) */
 
 typedef struct vgpu_ctx vgpu_ctx;
 typedef struct vgpu_env vgpu_env;

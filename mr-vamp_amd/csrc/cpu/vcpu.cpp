@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "../vgpu_host_env.hh"
+#include "../vgpu_abi.hh"
 #include "vcpu_robot.hh"
 
 namespace vcpu {
@@ -161,12 +162,19 @@ void parallel_for(size_t n, int threads, Fn fn)
         fn(0, n);
         return;
     }
+    // a chunk whose thread cannot be started (std::system_error) runs on the calling thread: the started
+    // threads are always joined, so no exception leaves through a joinable std::thread
     std::vector<std::thread> pool;
     pool.reserve(T);
-    for (size_t t = 0; t < T; ++t) {
-        const size_t lo = n * t / T, hi = n * (t + 1) / T;
-        pool.emplace_back([=] { fn(lo, hi); });
+    size_t t = 0;
+    try {
+        for (; t < T; ++t) {
+            const size_t lo = n * t / T, hi = n * (t + 1) / T;
+            pool.emplace_back([=] { fn(lo, hi); });
+        }
+    } catch (...) {
     }
+    if (t < T) fn(n * t / T, n);
     for (auto& th : pool) th.join();
 }
 
@@ -217,7 +225,7 @@ extern "C" float vgpu_l2_norm(const float* v, int dim)
 }
 
 extern "C" int vgpu_robot_scale_params(const vgpu_robot* robot, float* s_m, float* s_a, float* d_m)
-{
+try {
     Bound b;
     if (int rc = bind(robot, b)) return rc;
     for (int j = 0; j < b.R->dim; ++j) {
@@ -226,10 +234,10 @@ extern "C" int vgpu_robot_scale_params(const vgpu_robot* robot, float* s_m, floa
         if (d_m) d_m[j] = b.R->d_m[j];
     }
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_eefk(const vgpu_robot* robot, const float* q, size_t n, float* pose)
-{
+try {
     if (!robot || (n && (!q || !pose))) return VGPU_ERR_INVALID_ARG;
     Bound b;
     if (int rc = bind(robot, b)) return rc;
@@ -278,10 +286,10 @@ extern "C" int vgpu_cpu_eefk(const vgpu_robot* robot, const float* q, size_t n, 
         o[3] = (float)qe[1], o[4] = (float)qe[2], o[5] = (float)qe[3], o[6] = (float)qe[0];
     }
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_fkcc_block(const vgpu_robot* robot, vgpu_env* env, const float* block, int* valid)
-{
+try {
     Bound b;
     Env e;
     if (!block || !valid) return VGPU_ERR_INVALID_ARG;
@@ -291,10 +299,10 @@ extern "C" int vgpu_cpu_fkcc_block(const vgpu_robot* robot, vgpu_env* env, const
     for (int j = 0; j < b.R->dim; ++j) q[j] = V(_mm256_loadu_ps(block + 8 * j));
     *valid = b.R->fkcc(q, e.v, b.base, e.ext) ? 1 : 0;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_fkcc_attach_block(const vgpu_robot* robot, vgpu_env* env, const float* block, int* valid)
-{
+try {
     Bound b;
     Env e;
     if (!block || !valid) return VGPU_ERR_INVALID_ARG;
@@ -306,10 +314,10 @@ extern "C" int vgpu_cpu_fkcc_attach_block(const vgpu_robot* robot, vgpu_env* env
     for (int j = 0; j < b.R->dim; ++j) q[j] = V(_mm256_loadu_ps(block + 8 * j));
     *valid = b.R->fkcc_attach(q, e.v, b.base, e.ext) ? 1 : 0;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_sphere_fk_block(const vgpu_robot* robot, const float* block, float* out)
-{
+try {
     Bound b;
     if (!block || !out) return VGPU_ERR_INVALID_ARG;
     if (int rc = bind(robot, b)) return rc;
@@ -319,11 +327,11 @@ extern "C" int vgpu_cpu_sphere_fk_block(const vgpu_robot* robot, const float* bl
     b.R->sphere_fk(q, b.base, o.data());
     for (size_t i = 0; i < o.size(); ++i) _mm256_storeu_ps(out + 8 * i, o[i].v);
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_validate_motion(const vgpu_robot* robot, vgpu_env* env, const float* start,
                                         const float* goal, int* valid)
-{
+try {
     Bound b;
     Env e;
     if (!start || !goal || !valid) return VGPU_ERR_INVALID_ARG;
@@ -332,11 +340,11 @@ extern "C" int vgpu_cpu_validate_motion(const vgpu_robot* robot, vgpu_env* env, 
     if (e.attached && !b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
     *valid = validate_one(b, e, start, goal, nullptr, nullptr) ? 1 : 0;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_validate_vector(const vgpu_robot* robot, vgpu_env* env, const float* start,
                                         const float* vector, float distance, int* valid)
-{
+try {
     Bound b;
     Env e;
     if (!start || !vector || !valid) return VGPU_ERR_INVALID_ARG;
@@ -345,11 +353,11 @@ extern "C" int vgpu_cpu_validate_vector(const vgpu_robot* robot, vgpu_env* env, 
     if (e.attached && !b.R->fkcc_attach) return VGPU_ERR_UNSUPPORTED;
     *valid = validate_vector_one(b, e, start, vector, distance, nullptr, nullptr) ? 1 : 0;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_fkcc(const vgpu_robot* robot, vgpu_env* env, const float* q, size_t n, uint8_t* valid,
                              int threads)
-{
+try {
     Bound b;
     Env e;
     if ((n && (!q || !valid))) return VGPU_ERR_INVALID_ARG;
@@ -364,11 +372,11 @@ extern "C" int vgpu_cpu_fkcc(const vgpu_robot* robot, vgpu_env* env, const float
         }
     });
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_fkcc_attach(const vgpu_robot* robot, vgpu_env* env, const float* q, size_t n,
                                     uint8_t* valid, int threads)
-{
+try {
     Bound b;
     Env e;
     if ((n && (!q || !valid))) return VGPU_ERR_INVALID_ARG;
@@ -385,12 +393,12 @@ extern "C" int vgpu_cpu_fkcc_attach(const vgpu_robot* robot, vgpu_env* env, cons
         }
     });
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_validate_motions_mask(const vgpu_robot* robot, vgpu_env* env, const float* starts,
                                               const float* goals, size_t n, uint8_t* ok, int32_t* n_blocks,
                                               uint8_t* block_ok, size_t block_cap, size_t* n_total, int threads)
-{
+try {
     Bound b;
     Env e;
     if (!n_total || (n && (!starts || !goals || !ok))) return VGPU_ERR_INVALID_ARG;
@@ -415,12 +423,12 @@ extern "C" int vgpu_cpu_validate_motions_mask(const vgpu_robot* robot, vgpu_env*
         }
     });
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_cpu_validate_motions(const vgpu_robot* robot, vgpu_env* env, const float* starts,
                                          const float* goals, size_t n, uint8_t* ok, int32_t* n_blocks,
                                          int32_t* n_evaluated, int threads)
-{
+try {
     Bound b;
     Env e;
     if (n && (!starts || !goals || !ok)) return VGPU_ERR_INVALID_ARG;
@@ -437,4 +445,4 @@ extern "C" int vgpu_cpu_validate_motions(const vgpu_robot* robot, vgpu_env* env,
         }
     });
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH

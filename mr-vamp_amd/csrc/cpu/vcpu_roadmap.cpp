@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../../include/vamp_gpu.h"
+#include "../vgpu_abi.hh"
 #include "vcpu_robot.hh"
 
 namespace {
@@ -155,7 +156,7 @@ void query(const KdTree& T, uint32_t q, uint32_t k, float r, std::vector<Key>& h
 extern "C" int vgpu_cpu_roadmap_knn(int dim, const float* V, size_t n, const uint32_t* queries, size_t m,
                                     const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr, float* dist,
                                     uint32_t* cnt, int threads)
-{
+try {
     if (dim < 1 || dim > kMaxD || n >= 0x7FFFFFFFu || kmax < 1) return VGPU_ERR_INVALID_ARG;
     if (m == 0) return VGPU_OK;
     if (!V || !queries || !k || !r || !nbr || !dist || !cnt) return VGPU_ERR_INVALID_ARG;
@@ -190,9 +191,12 @@ extern "C" int vgpu_cpu_roadmap_knn(int dim, const float* V, size_t n, const uin
             }
         }
     };
-    std::vector<std::thread> pool;
-    for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
+    std::vector<std::thread> pool;  // workers take rows from a shared counter: fewer threads only take longer
+    try {
+        for (unsigned t = 1; t < nt; ++t) pool.emplace_back(work);
+    } catch (...) {
+    }
     work();
     for (auto& th : pool) th.join();
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH

@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "vcpu_robot.hh"
+#include "../vgpu_abi.hh"
 
 namespace vcpu {
 namespace {
@@ -69,7 +70,7 @@ using namespace vcpu;
 extern "C" int vgpu_cpu_rrtc(const vgpu_robot* robot, vgpu_env* env, const float* start, const float* goals,
                              size_t n_goals, const vgpu_rrtc_settings* settings, uint64_t* rng_index, float* path,
                              size_t path_cap, vgpu_plan_result* result)
-{
+try {
     Bound b;
     Env e;
     if (!start || (n_goals && !goals) || !settings || !rng_index || !result || (path_cap && !path))
@@ -241,4 +242,4 @@ extern "C" int vgpu_cpu_rrtc(const vgpu_robot* robot, vgpu_env* env, const float
     if (result->path_len > path_cap) return VGPU_ERR_INVALID_ARG;
     std::copy(out_path.begin(), out_path.end(), path);
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH

@@ -20,6 +20,7 @@
 #include <vector>
 
 #include "../../include/vamp_gpu.h"
+#include "vgpu_abi.hh"
 #include "vgpu_capt.hh"
 #include "vgpu_device.hh"
 #include "vgpu_host_env.hh"
@@ -332,7 +333,7 @@ static int fail(vgpu_ctx* ctx, int code, const char* msg)
 // context
 // ---------------------------------------------------------------------------------------
 extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
-{
+try {
     if (!out) return VGPU_ERR_INVALID_ARG;
     *out = nullptr;
     auto* c = new (std::nothrow) vgpu_ctx();
@@ -378,21 +379,21 @@ extern "C" int vgpu_ctx_create(int device, vgpu_ctx** out)
     }
     *out = c;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_debug_build(void)
-{
+try {
 #ifdef VGPU_DEBUG
     return 1;
 #else
     return 0;
 #endif
-}
+} VGPU_ABI_CATCH
 
 // The debug-check words (VGPU_DCHECK, debug builds): the context's (kNN index) and, when env is given, the
 // environment copy's (staged and CAPT kernels).  out[0] = violations, out[1] = first site id; read and reset.
 extern "C" int vgpu_debug_violations(vgpu_ctx* c, vgpu_env* e, uint32_t out[2])
-{
+try {
     if (!c || !out) return VGPU_ERR_INVALID_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->cur));
@@ -406,7 +407,7 @@ extern "C" int vgpu_debug_violations(vgpu_ctx* c, vgpu_env* e, uint32_t out[2])
     out[0] = a[0] + b[0];
     out[1] = a[1] ? a[1] : b[1];
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
 {
@@ -437,29 +438,29 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
 extern "C" const char* vgpu_last_error(const vgpu_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
 extern "C" int vgpu_ctx_set_stream(vgpu_ctx* c, void* s)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     c->cur = s ? (hipStream_t)s : c->own;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_ctx_device(const vgpu_ctx* c, int* device)
-{
+try {
     if (!c || !device) return VGPU_ERR_INVALID_ARG;
     *device = c->device;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_sync(vgpu_ctx* c)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_ctx_set_profiling(vgpu_ctx* c, int enable)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     HIPCHK(c, hipSetDevice(c->device));
     for (auto& ev : c->ev)
@@ -467,28 +468,28 @@ extern "C" int vgpu_ctx_set_profiling(vgpu_ctx* c, int enable)
     c->prof = enable != 0;
     for (float& a : c->acc) a = 0.0f;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_phase_times(vgpu_ctx* c, float ms[4])
-{
+try {
     if (!c || !ms) return VGPU_ERR_INVALID_ARG;
     for (int i = 0; i < 4; ++i) {
         ms[i] = c->acc[i];
         c->acc[i] = 0.0f;
     }
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_rsqrt_table(const vgpu_ctx* c, int* kbits, const uint32_t** table)
-{
+try {
     if (!c || !kbits || !table) return VGPU_ERR_INVALID_ARG;
     *kbits = c->kbits;
     *table = c->lut.data();
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_rsqrt_table_set(vgpu_ctx* c, const uint32_t* table, int kbits)
-{
+try {
     if (!c || !table || kbits < 1 || kbits > 23) return fail(c, VGPU_ERR_INVALID_ARG, "bad rsqrt table");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->cur));
@@ -499,7 +500,7 @@ extern "C" int vgpu_rsqrt_table_set(vgpu_ctx* c, const uint32_t* table, int kbit
     HIPCHK(c, hipMemcpy(c->lut_dev, c->lut.data(), c->lut.size() * 4, hipMemcpyHostToDevice));
     c->kbits = kbits;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // ---------------------------------------------------------------------------------------
 // environment: shapes.hh / factory.hh restated on the host (float, no contraction)
@@ -569,14 +570,14 @@ static void euler_xyz_matrix(const float e[3], float R[3][3])
 
 // c may be NULL: a host-only environment (build and inspect; it cannot be uploaded or used)
 extern "C" int vgpu_env_create(vgpu_ctx* c, vgpu_env** out)
-{
+try {
     if (!out) return VGPU_ERR_INVALID_ARG;
     auto* e = new (std::nothrow) vgpu_env();
     if (!e) return fail(c, VGPU_ERR_OOM, "out of host memory");
     e->ctx = c;
     *out = e;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" void vgpu_env_destroy(vgpu_env* e)
 {
@@ -592,16 +593,16 @@ extern "C" void vgpu_env_destroy(vgpu_env* e)
 static bool finite3(const float* v) { return std::isfinite(v[0]) && std::isfinite(v[1]) && std::isfinite(v[2]); }
 
 extern "C" int vgpu_env_add_sphere(vgpu_env* e, const float c[3], float r)
-{
+try {
     if (!e || !c || !finite3(c) || !std::isfinite(r)) return VGPU_ERR_INVALID_ARG;
     e->spheres.push_back({c[0], c[1], c[2], r, sphere_min_distance(c[0], c[1], c[2], r)});
     e->dirty = e->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_add_cuboid_axes(vgpu_env* e, const float c[3], const float a1[3], const float a2[3],
                                         const float a3[3], const float h[3])
-{
+try {
     if (!e || !c || !a1 || !a2 || !a3 || !h) return VGPU_ERR_INVALID_ARG;
     std::array<float, 16> row{c[0],  c[1],  c[2],  a1[0], a1[1], a1[2], a2[0], a2[1],
                               a2[2], a3[0], a3[1], a3[2], h[0],  h[1],  h[2],  0.0f};
@@ -612,10 +613,10 @@ extern "C" int vgpu_env_add_cuboid_axes(vgpu_env* e, const float c[3], const flo
         e->cuboids.push_back(row);
     e->dirty = e->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_add_cuboid_euler(vgpu_env* e, const float c[3], const float euler[3], const float h[3])
-{
+try {
     if (!e || !c || !euler || !h) return VGPU_ERR_INVALID_ARG;
     float R[3][3];
     euler_xyz_matrix(euler, R);
@@ -623,10 +624,10 @@ extern "C" int vgpu_env_add_cuboid_euler(vgpu_env* e, const float c[3], const fl
     const float a2[3] = {R[0][1], R[1][1], R[2][1]};
     const float a3[3] = {R[0][2], R[1][2], R[2][2]};
     return vgpu_env_add_cuboid_axes(e, c, a1, a2, a3, h);
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_add_capsule_endpoints(vgpu_env* e, const float p1[3], const float p2[3], float r)
-{
+try {
     if (!e || !p1 || !p2) return VGPU_ERR_INVALID_ARG;
     const float xv = p2[0] - p1[0], yv = p2[1] - p1[1], zv = p2[2] - p1[2];  // factory.hh:113-116
     const float dot = (xv * xv + yv * yv) + zv * zv;
@@ -639,10 +640,10 @@ extern "C" int vgpu_env_add_capsule_endpoints(vgpu_env* e, const float p1[3], co
         e->capsules.push_back(row);
     e->dirty = e->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_add_capsule_euler(vgpu_env* e, const float c[3], const float euler[3], float r, float len)
-{
+try {
     if (!e || !c || !euler) return VGPU_ERR_INVALID_ARG;
     float R[3][3];
     euler_xyz_matrix(euler, R);
@@ -650,10 +651,10 @@ extern "C" int vgpu_env_add_capsule_euler(vgpu_env* e, const float c[3], const f
     const float p1[3] = {c[0] + R[0][2] * h, c[1] + R[1][2] * h, c[2] + R[2][2] * h};
     const float p2[3] = {c[0] - R[0][2] * h, c[1] - R[1][2] * h, c[2] - R[2][2] * h};
     return vgpu_env_add_capsule_endpoints(e, p1, p2, r);
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_counts(const vgpu_env* e, int32_t counts[5])
-{
+try {
     if (!e || !counts) return VGPU_ERR_INVALID_ARG;
     counts[0] = (int32_t)e->spheres.size();
     counts[1] = (int32_t)e->capsules.size();
@@ -661,12 +662,12 @@ extern "C" int vgpu_env_counts(const vgpu_env* e, int32_t counts[5])
     counts[3] = (int32_t)e->cuboids.size();
     counts[4] = (int32_t)e->zcuboids.size();
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // HeightField via factory::heightfield::array / flat (factory.hh:365-423): reciprocal scales
 extern "C" int vgpu_env_add_heightfield(vgpu_env* e, const float center[3], const float scale[3], size_t xd,
                                         size_t yd, const float* data)
-{
+try {
     if (!e || !center || !scale || (xd * yd && !data)) return VGPU_ERR_INVALID_ARG;
     if (xd == 0 || yd == 0 || xd * yd >= (1u << 24)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "heightfield size");
     vgpu::Heightfield h;
@@ -682,12 +683,12 @@ extern "C" int vgpu_env_add_heightfield(vgpu_env* e, const float center[3], cons
     e->heightfields.push_back(std::move(h));
     e->dirty = e->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // Environment::add_pointcloud (bindings/environment.cc:148-158): builds the CAPT on the host
 extern "C" int vgpu_env_add_pointcloud(vgpu_env* e, const float* points, size_t n, float r_min, float r_max,
                                        float r_point, int64_t* build_ns)
-{
+try {
     if (!e || (n && !points)) return VGPU_ERR_INVALID_ARG;
     if (n == 0 || n > ((size_t)1 << 26)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "point cloud size");
     for (size_t i = 0; i < 3 * n; ++i)
@@ -697,7 +698,7 @@ extern "C" int vgpu_env_add_pointcloud(vgpu_env* e, const float* points, size_t 
     if (build_ns) *build_ns = e->pointclouds.back().build_ns;
     e->dirty = e->pc_dirty = e->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 namespace vgpu {
 hipError_t capt_build_device(const float* points, size_t n, float r_min, float r_max, float r_point, hipStream_t st,
@@ -706,7 +707,7 @@ hipError_t capt_build_device(const float* points, size_t n, float r_min, float r
 
 extern "C" int vgpu_env_add_pointcloud_device(vgpu_ctx* c, vgpu_env* e, const float* points, size_t n, float r_min,
                                               float r_max, float r_point, int64_t* build_ns)
-{
+try {
     // env: this context's, or a host-only one (ctx NULL); the build runs on ctx's device and stream
     if (!c || !e || (e->ctx && e->ctx != c) || (n && !points))
         return fail(c, VGPU_ERR_INVALID_ARG, "bad add_pointcloud_device");
@@ -718,12 +719,12 @@ extern "C" int vgpu_env_add_pointcloud_device(vgpu_ctx* c, vgpu_env* e, const fl
     e->pointclouds.push_back(std::move(t));
     e->dirty = e->pc_dirty = e->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // A deep copy of src's obstacles, point clouds and attachment bound to context c (or host-only for NULL):
 // the per-device environments of a multi-device batch (vgpu_multi.cpp)
 extern "C" int vgpu_env_clone(const vgpu_env* src, vgpu_ctx* c, vgpu_env** out)
-{
+try {
     if (!src || !out) return VGPU_ERR_INVALID_ARG;
     *out = nullptr;
     auto* e = new (std::nothrow) vgpu_env();
@@ -741,10 +742,10 @@ extern "C" int vgpu_env_clone(const vgpu_env* src, vgpu_ctx* c, vgpu_env** out)
     e->att_spheres = src->att_spheres;
     *out = e;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_copy_pointcloud(vgpu_env* dst, const vgpu_env* src, int index)
-{
+try {
     if (!dst || !src || index < 0 || (size_t)index >= src->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
     if (dst == src) {
         vgpu::CaptTree t = src->pointclouds[index];  // copy before the vector may reallocate
@@ -754,29 +755,29 @@ extern "C" int vgpu_env_copy_pointcloud(vgpu_env* dst, const vgpu_env* src, int 
     }
     dst->dirty = dst->pc_dirty = dst->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_ext_counts(const vgpu_env* e, int32_t counts[2])
-{
+try {
     if (!e || !counts) return VGPU_ERR_INVALID_ARG;
     counts[0] = (int32_t)e->heightfields.size();
     counts[1] = (int32_t)e->pointclouds.size();
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_pointcloud_info(const vgpu_env* e, int index, int32_t* nlog2, size_t* n_aff, float top[6])
-{
+try {
     if (!e || index < 0 || (size_t)index >= e->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
     const auto& t = e->pointclouds[index];
     if (nlog2) *nlog2 = t.nlog2;
     if (n_aff) *n_aff = t.n_aff();
     if (top) std::copy(t.top, t.top + 6, top);
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_pointcloud_arrays(const vgpu_env* e, int index, float* tests, float* aabbs,
                                           uint32_t* aff_starts, float* aff)
-{
+try {
     if (!e || index < 0 || (size_t)index >= e->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
     const auto& t = e->pointclouds[index];
     if (tests) std::copy(t.tests.begin(), t.tests.end(), tests);
@@ -784,7 +785,7 @@ extern "C" int vgpu_env_pointcloud_arrays(const vgpu_env* e, int index, float* t
     if (aff_starts) std::copy(t.aff_starts.begin(), t.aff_starts.end(), aff_starts);
     if (aff) std::copy(t.aff.begin(), t.aff.end(), aff);
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 template <size_t W>
 static void sort_md(std::vector<std::array<float, W>>& v)  // environment.hh:40-66
@@ -795,7 +796,7 @@ static void sort_md(std::vector<std::array<float, W>>& v)  // environment.hh:40-
 // Device layout of EnvView (vgpu_device.hh): per type, records sorted by min_distance
 // (environment.hh:40-66) followed by kObsPad sentinels with min_distance = +inf.
 extern "C" int vgpu_env_attach(vgpu_env* e, const float tf[7], const float* spheres, size_t n)
-{
+try {
     if (!e || !tf || (n && !spheres)) return VGPU_ERR_INVALID_ARG;
     if (n > ((size_t)1 << 20)) return fail(e->ctx, VGPU_ERR_INVALID_ARG, "too many attached spheres");
     for (int i = 0; i < 7; ++i)
@@ -807,16 +808,16 @@ extern "C" int vgpu_env_attach(vgpu_env* e, const float tf[7], const float* sphe
     e->attached = true;
     e->dirty = e->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_detach(vgpu_env* e)
-{
+try {
     if (!e) return VGPU_ERR_INVALID_ARG;
     e->attached = false;
     e->att_spheres.clear();
     e->dirty = e->host_dirty = true;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // The environment as one float blob: per obstacle type, records sorted by min_distance
 // (environment.hh:40-66) followed by kObsPad sentinels (md = +inf), then heightfield / point-cloud
@@ -1047,7 +1048,7 @@ static int build_blob(vgpu_env* e, std::vector<float>& blob, std::vector<std::pa
 }
 
 extern "C" int vgpu_env_upload(vgpu_env* e)
-{
+try {
     if (!e) return VGPU_ERR_INVALID_ARG;
     vgpu_ctx* c = e->ctx;
     if (!c) return VGPU_ERR_INVALID_ARG;  // host-only environment
@@ -1102,12 +1103,12 @@ extern "C" int vgpu_env_upload(vgpu_env* e)
     e->dirty = e->pc_dirty = false;
     ++e->n_full;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // The cell grid of point cloud `index` as its DEVICE header records it: out = {nx, ny, nz, cells_off} (all 0:
 // no grid).  Reads the uploaded header back, so a layout slip that drops the grid shows up in a test.
 extern "C" int vgpu_env_pointcloud_grid(vgpu_env* e, int index, uint32_t out[4])
-{
+try {
     if (!e || !out || !e->ctx || index < 0 || (size_t)index >= e->pointclouds.size()) return VGPU_ERR_INVALID_ARG;
     if (int rc = vgpu_env_upload(e)) return rc;
     vgpu_ctx* c = e->ctx;
@@ -1118,16 +1119,16 @@ extern "C" int vgpu_env_pointcloud_grid(vgpu_env* e, int index, uint32_t out[4])
     const int f[4] = {PC_GNX, PC_GNY, PC_GNZ, PC_GCELLS};
     for (int k = 0; k < 4; ++k) std::memcpy(&out[k], &hd[f[k]], 4);
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_env_upload_stats(const vgpu_env* e, uint64_t out[3])
-{
+try {
     if (!e || !out) return VGPU_ERR_INVALID_ARG;
     out[0] = e->n_full;
     out[1] = e->n_tail;
     out[2] = e->n_grids;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // Host view for the CPU rake (csrc/cpu/vcpu.cpp): the same blob in host memory, rebuilt when the
 // environment changed.  Offsets are identical to the device copy's.
@@ -1183,7 +1184,7 @@ static const RobotOps* generic_ops(int32_t kind);
 static size_t dim_of(const vgpu_robot* r);
 
 extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t* ns)
-{
+try {
     if (const RobotOps* g = generic_ops(kind)) {
         if (dim) *dim = g->dim;
         if (res) *res = g->resolution;
@@ -1207,7 +1208,7 @@ extern "C" int vgpu_robot_info(int32_t kind, int32_t* dim, int32_t* res, int32_t
     if (res) *res = kPandaResolution;
     if (ns) *ns = kPandaSpheres;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // both arms' bases of a VGPU_ROBOT_PANDA_PAIR, metres (panda/fk.hh:109-111 per arm)
 static void pair_bases(const vgpu_robot* r, float pb[6])
@@ -1239,7 +1240,7 @@ static int check_robot(vgpu_ctx* c, const vgpu_robot* r, float base[3])
 }
 
 extern "C" int vgpu_sphere_fk(vgpu_ctx* c, const vgpu_robot* r, const float* q, size_t n, float* xyz, size_t ld)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     float b[3];
     int rc = check_robot(c, r, b);
@@ -1258,7 +1259,7 @@ extern "C" int vgpu_sphere_fk(vgpu_ctx* c, const vgpu_robot* r, const float* q, 
         return fail(c, VGPU_ERR_UNSUPPORTED, "sphere_fk of the composite: call it per arm (VGPU_ROBOT_PANDA)");
     HIPCHK(c, vgpu_launch_panda_sphere_fk(q, n, b[0], b[1], b[2], xyz, ld, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // One staged pass (vgpu_staged.hip) over n groups of a source kind (0 configurations, 1 Halton
 // samples, 2 validate head, 3 validate tail): bound -> counts to host -> queue -> children.
@@ -1509,7 +1510,7 @@ static int pair_staged(vgpu_ctx* c, int kind, const void* s0, const void* s1, co
 }
 
 extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n, uint8_t* valid)
-{
+try {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
     float b[3];
     int rc = check_robot(c, r, b);
@@ -1539,11 +1540,11 @@ extern "C" int vgpu_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const fl
     if (c->staged) return staged_pass(c, kPandaStaged, 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_fkcc(q, n, &v, b[0], b[1], b[2], valid, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_fkcc_attach(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n,
                                 uint8_t* valid)
-{
+try {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
     float b[3];
     int rc = check_robot(c, r, b);
@@ -1562,7 +1563,7 @@ extern "C" int vgpu_fkcc_attach(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, c
     else
         HIPCHK(c, vgpu_launch_panda_fkcc_attach(q, n, &v, b[0], b[1], b[2], valid, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // The back-step item count of a validate call (cnt[0 .. n_edges) scanned into off): read back once,
 // with its 64-bit sum -- the scan and the item indices are 32-bit, so a batch whose rake blocks do not
@@ -1607,7 +1608,7 @@ static int ensure_ws(vgpu_ctx* c, size_t n_edges, uint32_t** cnt, uint32_t** off
 
 extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* starts,
                                      const float* goals, size_t n_edges, uint8_t* ok, int32_t* n_blocks)
-{
+try {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
     float b[3];
     int rc = check_robot(c, r, b);
@@ -1716,14 +1717,14 @@ extern "C" int vgpu_validate_motions(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
         c->acc[3] += 1.0f;
     }
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // Full-mask mode (SURVEY §8(d) "full-mask: every interpolant evaluated"): every rake block of every
 // edge is evaluated -- no early exit across an edge's blocks -- and each block's result is kept.
 extern "C" int vgpu_validate_motions_mask(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* starts,
                                           const float* goals, size_t n_edges, uint8_t* ok, int32_t* n_blocks,
                                           uint8_t* block_ok, size_t block_cap, size_t* n_total)
-{
+try {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
     float b[3];
     int rc = check_robot(c, r, b);
@@ -1763,13 +1764,13 @@ extern "C" int vgpu_validate_motions_mask(vgpu_ctx* c, const vgpu_robot* r, vgpu
     }
     HIPCHK(c, vgpu_launch_mask_finish(n_edges, off, ok, block_ok, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // CAPT::collides (simd = 0, capt.hh:403-443) or one lane of CAPT::collides_simd (simd = 1,
 // capt.hh:457-541) for n raw spheres against point cloud `index` of the environment.
 extern "C" int vgpu_pointcloud_collides(vgpu_ctx* c, vgpu_env* e, int index, const float* centers,
                                         const float* radii, size_t n, int simd, uint8_t* out)
-{
+try {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
     if (index < 0 || (size_t)index >= e->pointclouds.size()) return fail(c, VGPU_ERR_INVALID_ARG, "bad index");
     if (n == 0) return VGPU_OK;
@@ -1780,13 +1781,13 @@ extern "C" int vgpu_pointcloud_collides(vgpu_ctx* c, vgpu_env* e, int index, con
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, vgpu_launch_capt_query(centers, radii, n, &v, index, simd, out, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // filter_pointcloud (collision/filter.hh:175-268) on the device (vgpu_filter.hip)
 extern "C" int vgpu_filter_pointcloud(vgpu_ctx* c, const float* pc, size_t n, float min_dist, float max_range,
                                       const float origin[3], const float ws_min[3], const float ws_max[3], int cull,
                                       uint32_t* out_idx, size_t* count)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (!count || !origin || !ws_min || !ws_max) return fail(c, VGPU_ERR_INVALID_ARG, "null argument");
     *count = 0;
@@ -1796,7 +1797,7 @@ extern "C" int vgpu_filter_pointcloud(vgpu_ctx* c, const float* pc, size_t n, fl
     HIPCHK(c, vgpu_filter_pointcloud_run(pc, n, min_dist, max_range, origin, ws_min, ws_max, cull, out_idx, count,
                                          c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // filter_robot_from_pointcloud<Robot> (bindings/common.hh:36-87): sphere_fk<1> of the configuration
 // (the robot's own sphere_fk kernel on one row), then one lane per point (vgpu_query.hip)
@@ -1813,7 +1814,7 @@ static const float* sphere_radii(int32_t kind, int* S)
 
 extern "C" int vgpu_filter_robot_pointcloud(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* configuration,
                                             const float* pc, size_t n, float point_radius, uint8_t* keep)
-{
+try {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
     float b[3];
     int rc = check_robot(c, r, b);
@@ -1839,11 +1840,11 @@ extern "C" int vgpu_filter_robot_pointcloud(vgpu_ctx* c, const vgpu_robot* r, vg
     if ((rc = vgpu_sphere_fk(c, r, c->small, 1, c->small + 16, 1))) return rc;
     HIPCHK(c, vgpu_launch_filter_robot(pc, n, point_radius, c->small + 16, S, &v, keep, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // ---- sampling (rng::Halton, Robot::scale_configuration) and compaction --------------------------
 extern "C" int vgpu_halton(vgpu_ctx* c, int dim, uint64_t first, size_t n, float* out)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (dim < 1 || dim > 16 || first == 0) return fail(c, VGPU_ERR_INVALID_ARG, "dim must be 1..16, first >= 1");
     if (n == 0) return VGPU_OK;
@@ -1851,10 +1852,10 @@ extern "C" int vgpu_halton(vgpu_ctx* c, int dim, uint64_t first, size_t n, float
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, vgpu_launch_halton(dim, first, n, out, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_sample_configurations(vgpu_ctx* c, const vgpu_robot* r, uint64_t first, size_t n, float* q)
-{
+try {
     float b[3];
     int rc = check_robot(c, r, b);
     if (rc) return rc;
@@ -1870,11 +1871,11 @@ extern "C" int vgpu_sample_configurations(vgpu_ctx* c, const vgpu_robot* r, uint
     else
         HIPCHK(c, vgpu_launch_panda_sample(first, n, q, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, uint64_t first, size_t n, float* q,
                                 uint8_t* valid)
-{
+try {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
     float b[3];
     int rc = check_robot(c, r, b);
@@ -1906,11 +1907,11 @@ extern "C" int vgpu_sample_fkcc(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, u
     if (c->staged) return staged_pass(c, kPandaStaged, 1, q, nullptr, nullptr, nullptr, first, n, &v, b, valid);
     HIPCHK(c, vgpu_launch_panda_sample_fkcc(first, n, &v, b[0], b[1], b[2], q, valid, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_compact(vgpu_ctx* c, const float* rows, const uint8_t* valid, size_t n, int dim, float* rows_out,
                             uint32_t* index_out, size_t* count)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (dim < 1 || !count || n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "bad compaction args");
     *count = 0;
@@ -1936,7 +1937,7 @@ extern "C" int vgpu_compact(vgpu_ctx* c, const float* rows, const uint8_t* valid
     HIPCHK(c, hipStreamSynchronize(c->cur));
     *count = *c->total_host;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // ---- host conveniences ------------------------------------------------------------------
 // Also makes the context's device current for the calling thread: the staging buffer and everything the
@@ -1976,7 +1977,7 @@ static size_t spheres_of(const vgpu_robot* r)
 }
 
 extern "C" int vgpu_sphere_fk_host(vgpu_ctx* c, const vgpu_robot* r, const float* q, size_t n, float* xyz)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
@@ -1989,11 +1990,11 @@ extern "C" int vgpu_sphere_fk_host(vgpu_ctx* c, const vgpu_robot* r, const float
     HIPCHK(c, hipMemcpyAsync(xyz, d + qb, ob, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n,
                               uint8_t* valid)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
@@ -2006,11 +2007,11 @@ extern "C" int vgpu_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, con
     HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_fkcc_attach_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* q, size_t n,
                                      uint8_t* valid)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
@@ -2023,11 +2024,11 @@ extern "C" int vgpu_fkcc_attach_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_validate_motions_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, const float* starts,
                                           const float* goals, size_t n, uint8_t* ok, int32_t* n_blocks)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
@@ -2045,12 +2046,12 @@ extern "C" int vgpu_validate_motions_host(vgpu_ctx* c, const vgpu_robot* r, vgpu
     if (n_blocks) HIPCHK(c, hipMemcpyAsync(n_blocks, nbd, n * 4, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_filter_pointcloud_host(vgpu_ctx* c, const float* pc, size_t n, float min_dist, float max_range,
                                            const float origin[3], const float ws_min[3], const float ws_max[3],
                                            int cull, uint32_t* out_idx, size_t* count)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (!count) return fail(c, VGPU_ERR_INVALID_ARG, "null count");
     *count = 0;
@@ -2068,11 +2069,11 @@ extern "C" int vgpu_filter_pointcloud_host(vgpu_ctx* c, const float* pc, size_t 
     HIPCHK(c, hipMemcpyAsync(out_idx, d + pb, *count * 4, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_pointcloud_collides_host(vgpu_ctx* c, vgpu_env* e, int index, const float* centers,
                                              const float* radii, size_t n, int simd, uint8_t* out)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
@@ -2088,10 +2089,10 @@ extern "C" int vgpu_pointcloud_collides_host(vgpu_ctx* c, vgpu_env* e, int index
     HIPCHK(c, hipMemcpyAsync(out, d + cb + rb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_halton_host(vgpu_ctx* c, int dim, uint64_t first, size_t n, float* out)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
@@ -2101,11 +2102,11 @@ extern "C" int vgpu_halton_host(vgpu_ctx* c, int dim, uint64_t first, size_t n, 
     HIPCHK(c, hipMemcpyAsync(out, d, n * (size_t)dim * 4, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_sample_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e, uint64_t first, size_t n,
                                      float* q, uint8_t* valid)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n == 0) return VGPU_OK;
     char* d;
@@ -2117,7 +2118,7 @@ extern "C" int vgpu_sample_fkcc_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env*
     HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // ---------------------------------------------------------------------------------------
 // PRM roadmap edge stage (planning/prm.hh:235-299; vgpu_roadmap.hip)
@@ -2134,7 +2135,7 @@ extern "C" hipError_t vgpu_launch_edge_gather(const float* V, uint32_t q_first, 
 // PRMStarNeighborParams (roadmap.hh:42-77) for roadmap sizes 0 .. n-1, in double as the reference
 extern "C" int vgpu_prm_neighbor_params(int dim, double space_measure, double gamma_scale, size_t n, uint32_t* k,
                                         float* r)
-{
+try {
     if (dim <= 0 || (n && (!k || !r))) return VGPU_ERR_INVALID_ARG;
     const double E = 2.718281828459045235360287471352662498;  // constants.hh:6
     const double PI = 3.141592653589793238462643383279502884;
@@ -2164,11 +2165,19 @@ extern "C" int vgpu_prm_neighbor_params(int dim, double space_measure, double ga
         fill(0, n);
         return VGPU_OK;
     }
+    // a thread that cannot be started (std::system_error) leaves its range and every later one to this thread:
+    // no exception crosses the C ABI, and the table is complete either way
     std::vector<std::thread> th;
-    for (size_t t = 0; t < nt; ++t) th.emplace_back(fill, n * t / nt, n * (t + 1) / nt);
+    size_t done = 0;  // ranges [0, done) have a thread
+    try {
+        th.reserve(nt);
+        for (; done < nt; ++done) th.emplace_back(fill, n * done / nt, n * (done + 1) / nt);
+    } catch (...) {
+    }
+    fill(n * done / nt, n);
     for (auto& x : th) x.join();
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" size_t vgpu_knn_index_bytes(int dim, uint32_t n, uint32_t q_count);
 extern "C" hipError_t vgpu_launch_knn_index(int dim, const float* V, uint32_t n, uint32_t q_first, uint32_t q_count,
@@ -2184,16 +2193,16 @@ static bool knn_dim_ok(int dim) { return dim == 6 || dim == 7 || dim == 8 || dim
 static constexpr size_t kKnnIndexMin = 65536;  // group-query index: 3.6 vs 11.8 ms (brute) at 100k Fetch vertices
 
 extern "C" int vgpu_set_knn_mode(vgpu_ctx* c, int mode)
-{
+try {
     if (!c || mode < 0 || mode > 2) return VGPU_ERR_INVALID_ARG;
     c->knn_mode = mode;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_roadmap_knn_range(vgpu_ctx* c, int dim, const float* V, size_t n, size_t q_first, size_t q_count,
                                       const uint32_t* k, const float* r, uint32_t kmax, uint32_t* nbr, float* dist,
                                       uint32_t* cnt)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (q_first > n || q_count > n - q_first) return fail(c, VGPU_ERR_INVALID_ARG, "query range outside the vertices");
     if (!knn_dim_ok(dim)) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap kNN: dimension 6, 7, 8 or 14");
@@ -2223,18 +2232,18 @@ extern "C" int vgpu_roadmap_knn_range(vgpu_ctx* c, int dim, const float* V, size
     HIPCHK(c, vgpu_launch_roadmap_knn(dim, V, (uint32_t)n, (uint32_t)q_first, (uint32_t)q_count, k, r, kmax, S,
                                       (uint32_t)C, pd, pi, pc, nbr, dist, cnt, c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_roadmap_knn(vgpu_ctx* c, int dim, const float* V, size_t n, const uint32_t* k, const float* r,
                                 uint32_t kmax, uint32_t* nbr, float* dist, uint32_t* cnt)
-{
+try {
     return vgpu_roadmap_knn_range(c, dim, V, n, 0, n, k, r, kmax, nbr, dist, cnt);
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_roadmap_edge_gather(vgpu_ctx* c, int dim, const float* V, size_t q_first, size_t q_count,
                                         const uint32_t* nbr, uint32_t kmax, const uint32_t* cnt, const uint32_t* off,
                                         float* starts, float* goals)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (q_count && (!V || !nbr || !cnt || !off || !starts || !goals))
         return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
@@ -2242,7 +2251,7 @@ extern "C" int vgpu_roadmap_edge_gather(vgpu_ctx* c, int dim, const float* V, si
     HIPCHK(c, vgpu_launch_edge_gather(V, (uint32_t)q_first, (uint32_t)q_count, dim, nbr, kmax, cnt, off, starts, goals,
                                       c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 namespace {
 struct DevBufs {  // call-scoped device allocations
@@ -2269,7 +2278,7 @@ struct DevBufs {  // call-scoped device allocations
 // then the later vertices that connected to it, ascending.  Union-find for the components.
 extern "C" int vgpu_roadmap_assemble(size_t n, const uint32_t* pairs, size_t m, size_t* offsets, uint32_t* adj,
                                      uint32_t* component)
-{
+try {
     if (!offsets || (m && (!pairs || !adj))) return VGPU_ERR_INVALID_ARG;
     for (size_t p = 0; p < 2 * m; ++p)
         if (pairs[p] >= n) return VGPU_ERR_INVALID_ARG;
@@ -2297,7 +2306,7 @@ extern "C" int vgpu_roadmap_assemble(size_t n, const uint32_t* pairs, size_t m, 
         for (size_t i = 0; i < n; ++i) component[i] = find((uint32_t)i);
     }
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" size_t vgpu_roadmap_assemble_bytes(uint32_t n, size_t m);
 extern "C" hipError_t vgpu_launch_roadmap_assemble(uint32_t n, const uint32_t* pairs, size_t m, unsigned long long* offsets,
@@ -2306,7 +2315,7 @@ extern "C" hipError_t vgpu_launch_roadmap_assemble(uint32_t n, const uint32_t* p
 
 extern "C" int vgpu_roadmap_assemble_device(vgpu_ctx* c, size_t n, const uint32_t* pairs, size_t m, uint64_t* offsets,
                                             uint32_t* adj, uint32_t* component)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many vertices");
     if (2 * m >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many pairs (2m must be < 2^31)");
@@ -2327,12 +2336,12 @@ extern "C" int vgpu_roadmap_assemble_device(vgpu_ctx* c, size_t n, const uint32_
                                            c->knn_idx, c->knn_idx_cap * 4, &flags, c->cur));
     if (flags & 1u) return fail(c, VGPU_ERR_INVALID_ARG, "pair index out of range");
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_build_roadmap_host(vgpu_ctx* c, const vgpu_robot* robot, vgpu_env* e, const float* V, size_t n,
                                        double space_measure, double gamma_scale, size_t* offsets, uint32_t* adj,
                                        size_t adj_cap, size_t* n_adj, uint32_t* component)
-{
+try {
     if (!c || !e || e->ctx != c) return fail(c, VGPU_ERR_INVALID_ARG, "bad context/environment");
     float b[3];
     int rc = check_robot(c, robot, b);
@@ -2405,12 +2414,12 @@ extern "C" int vgpu_build_roadmap_host(vgpu_ctx* c, const vgpu_robot* robot, vgp
     if ((rc = vgpu_roadmap_assemble(n, pairs.data(), pairs.size() / 2, offsets, adj, component)))
         return fail(c, rc, "roadmap assembly");
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_filter_robot_pointcloud_host(vgpu_ctx* c, const vgpu_robot* r, vgpu_env* e,
                                                  const float* configuration, const float* pc, size_t n,
                                                  float point_radius, float* out, size_t* count)
-{
+try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (!count) return fail(c, VGPU_ERR_INVALID_ARG, "null count");
     *count = 0;
@@ -2431,4 +2440,4 @@ extern "C" int vgpu_filter_robot_pointcloud_host(vgpu_ctx* c, const vgpu_robot* 
     HIPCHK(c, hipMemcpyAsync(out, d + pb + kb, *count * 12, hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH

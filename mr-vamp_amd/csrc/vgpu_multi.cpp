@@ -33,19 +33,20 @@
 #include <vector>
 
 #include "../../include/vamp_gpu.h"
+#include "vgpu_abi.hh"
 
 extern "C" int vgpu_env_clone(const vgpu_env* src, vgpu_ctx* c, vgpu_env** out);
 
 // ---- shard ranges ---------------------------------------------------------------------------------
 extern "C" int vgpu_shard_range(size_t n, int rank, int world, size_t* first, size_t* count)
-{
+try {
     if (world < 1 || rank < 0 || rank >= world || !first || !count) return VGPU_ERR_INVALID_ARG;
     const unsigned __int128 lo = (unsigned __int128)n * (unsigned)rank / (unsigned)world;
     const unsigned __int128 hi = (unsigned __int128)n * (unsigned)(rank + 1) / (unsigned)world;
     *first = (size_t)lo;
     *count = (size_t)(hi - lo);
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // ---- one process, several devices -------------------------------------------------------------------
 struct vgpu_multi {
@@ -55,7 +56,7 @@ struct vgpu_multi {
 };
 
 extern "C" int vgpu_multi_create(const int* devices, int n, vgpu_multi** out)
-{
+try {
     if (!out || n < 1 || !devices) return VGPU_ERR_INVALID_ARG;
     *out = nullptr;
     auto* m = new (std::nothrow) vgpu_multi();
@@ -73,7 +74,7 @@ extern "C" int vgpu_multi_create(const int* devices, int n, vgpu_multi** out)
     }
     *out = m;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" void vgpu_multi_destroy(vgpu_multi* m)
 {
@@ -93,7 +94,7 @@ extern "C" const char* vgpu_multi_last_error(const vgpu_multi* m) { return m ? m
 
 // envs[i] = src realised on device i (destroy each with vgpu_env_destroy)
 extern "C" int vgpu_multi_env_create(vgpu_multi* m, const vgpu_env* src, vgpu_env** envs)
-{
+try {
     if (!m || !src || !envs) return VGPU_ERR_INVALID_ARG;
     for (size_t i = 0; i < m->ctx.size(); ++i) {
         const int rc = vgpu_env_clone(src, m->ctx[i], &envs[i]);
@@ -103,7 +104,7 @@ extern "C" int vgpu_multi_env_create(vgpu_multi* m, const vgpu_env* src, vgpu_en
         }
     }
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // Runs fn(i) on one host thread per device; the first failure's code and message are returned.
 template <class Fn>
@@ -111,16 +112,25 @@ static int per_device(vgpu_multi* m, Fn fn)
 {
     std::vector<int> rc(m->ctx.size(), VGPU_OK);
     std::vector<std::thread> th;
+    th.reserve(m->ctx.size());
     // HIP's current device is per thread and a new thread starts on device 0: select the context's device
-    // before fn allocates or launches anything
-    for (size_t i = 0; i < m->ctx.size(); ++i)
-        th.emplace_back([&, i] {
-            if (hipSetDevice(m->device[i]) != hipSuccess) {
-                rc[i] = VGPU_ERR_HIP;
-                return;
-            }
-            rc[i] = fn((int)i);
-        });
+    // before fn allocates or launches anything.  No exception leaves a worker (it would terminate the process),
+    // and a device whose thread cannot be started runs on this thread after the others have been started
+    auto body = [&](size_t i) {
+        try {
+            rc[i] = hipSetDevice(m->device[i]) != hipSuccess ? VGPU_ERR_HIP : fn((int)i);
+        } catch (const std::bad_alloc&) {
+            rc[i] = VGPU_ERR_OOM;
+        } catch (...) {
+            rc[i] = VGPU_ERR_INTERNAL;
+        }
+    };
+    size_t started = 0;
+    try {
+        for (; started < m->ctx.size(); ++started) th.emplace_back(body, started);
+    } catch (...) {
+    }
+    for (size_t i = started; i < m->ctx.size(); ++i) body(i);
     for (auto& t : th) t.join();
     for (size_t i = 0; i < rc.size(); ++i)
         if (rc[i] != VGPU_OK) {
@@ -140,7 +150,7 @@ static int robot_dim(const vgpu_robot* r)
 extern "C" int vgpu_multi_validate_motions_host(vgpu_multi* m, const vgpu_robot* r, vgpu_env* const* envs,
                                                 const float* starts, const float* goals, size_t n, uint8_t* ok,
                                                 int32_t* n_blocks)
-{
+try {
     if (!m || !envs || (n && (!starts || !goals || !ok))) return VGPU_ERR_INVALID_ARG;
     const int dim = robot_dim(r);
     if (dim < 1) return VGPU_ERR_INVALID_ARG;
@@ -152,14 +162,14 @@ extern "C" int vgpu_multi_validate_motions_host(vgpu_multi* m, const vgpu_robot*
         return vgpu_validate_motions_host(m->ctx[i], r, envs[i], starts + lo * dim, goals + lo * dim, cnt, ok + lo,
                                           n_blocks ? n_blocks + lo : nullptr);
     });
-}
+} VGPU_ABI_CATCH
 
 // The PRM vertex stage over the devices: draws first .. first + n_draws - 1 split into contiguous ranges,
 // each device's valid rows compacted on the device and copied back; rows_out[*count][dim] and draws_out
 // (1-based draw indices) in draw order (capacity n_draws each).
 extern "C" int vgpu_multi_sample_fkcc_host(vgpu_multi* m, const vgpu_robot* r, vgpu_env* const* envs, uint64_t first,
                                            size_t n_draws, float* rows_out, uint64_t* draws_out, size_t* count)
-{
+try {
     if (!m || !envs || !count || (n_draws && (!rows_out || !draws_out)) || first == 0) return VGPU_ERR_INVALID_ARG;
     *count = 0;
     const int dim = robot_dim(r);
@@ -205,7 +215,7 @@ extern "C" int vgpu_multi_sample_fkcc_host(vgpu_multi* m, const vgpu_robot* r, v
     }
     *count = at;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // ---- one process per GPU: the exchange a communicator runs its all-gathers over -----------------------
 // The sharded stages below need exactly one collective: an all-gather of equal-sized device blocks in rank
@@ -277,10 +287,14 @@ struct vgpu_loopback {
     std::vector<size_t> bytes;
     int members = 0;  // communicators created on the hub and not yet destroyed
     int timeout_s = 120;
+    // set for good by the first barrier that times out: a late rank arriving afterwards must not pair up with
+    // its peers' NEXT exchange (same sizes, other data), so every later barrier fails at once
+    bool failed = false;
 
     bool barrier()
     {
         std::unique_lock<std::mutex> lk(mu);
+        if (failed) return false;
         const uint64_t g = gen;
         if (++arrived == world) {
             arrived = 0;
@@ -288,8 +302,9 @@ struct vgpu_loopback {
             cv.notify_all();
             return true;
         }
-        if (!cv.wait_for(lk, std::chrono::seconds(timeout_s), [&] { return gen != g; })) {
-            --arrived;  // leave: the peers that did arrive time out as well
+        if (!cv.wait_for(lk, std::chrono::seconds(timeout_s), [&] { return gen != g || failed; }) || gen == g) {
+            failed = true;  // the hub is unusable from here on; wake the peers still waiting
+            cv.notify_all();
             return false;
         }
         return true;
@@ -358,7 +373,7 @@ struct vgpu_comm {
 static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id is 128 bytes");
 
 extern "C" int vgpu_comm_unique_id(uint8_t id[128])
-{
+try {
     if (!id) return VGPU_ERR_INVALID_ARG;
     Rccl& R = rccl();
     if (!R.ok) return VGPU_ERR_UNSUPPORTED;
@@ -366,7 +381,7 @@ extern "C" int vgpu_comm_unique_id(uint8_t id[128])
     if (R.get_id(&u) != ncclSuccess) return VGPU_ERR_HIP;
     std::memcpy(id, &u, 128);
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // RCCL may print a version banner on stdout while a communicator is created.  With VGPU_RCCL_QUIET=1 the
 // caller's stdout (bench.py's one JSON line) stays clean: fd 1 is pointed at stderr for the duration of
@@ -392,24 +407,73 @@ struct StdoutToStderr {
     }
 };
 
-// the communicator's stream and word buffer on its device (before the exchange itself exists)
+// exchange 1's word buffer layout: [0, W) the gathered words, [W] this rank's word, [W + 1] the selection
+// count, [W + 2] a pre-set failure word (kFailTag | -VGPU_ERR_HIP): the word a rank sends when even the copy of
+// its own word to the device fails, so it still enters the all-gather
+constexpr uint64_t kFailTagC = 0xFFFFFFFF00000000ull;
+size_t words_len(int world) { return 2 * (size_t)world + 3; }
+
+// the communicator's word buffer (first: the status exchange below needs it) and stream on its device, before
+// the exchange itself exists.  Returns the first failure; c->words is non-null whenever that allocation worked
 int comm_alloc(vgpu_comm* c, int dev, int world)
 {
     c->device = dev;
     c->world = world;
-    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) return VGPU_ERR_HIP;
-    if (hipMalloc(&c->words, (2 * (size_t)world + 2) * sizeof(uint64_t)) != hipSuccess) {
+    if (hipMalloc(&c->words, words_len(world) * sizeof(uint64_t)) != hipSuccess) {
         c->words = nullptr;
         return VGPU_ERR_OOM;
+    }
+    const uint64_t fail = kFailTagC | (uint32_t)(-VGPU_ERR_HIP);
+    if (hipMemcpy(c->words + world + 2, &fail, 8, hipMemcpyHostToDevice) != hipSuccess) return VGPU_ERR_HIP;
+    if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+        c->st = nullptr;
+        return VGPU_ERR_HIP;
     }
     return VGPU_OK;
 }
 }  // namespace
 
 extern "C" void vgpu_comm_destroy(vgpu_comm* c);
+static bool injected(const vgpu_comm* c, const char* site);
+
+// The last step of communicator creation, on every rank alike: one all-gather of each rank's creation status
+// (0, or kFailTag | -code), so that when ANY rank failed -- an allocation, the exchange, an injected fault --
+// EVERY rank destroys its communicator and returns the same code (the lowest failing rank's) instead of leaving
+// its peers to block in their first stage's all-gather.  A rank without a word buffer (its 24-byte allocation
+// failed) cannot take part: it returns at once, and its peers' status all-gather fails in RCCL (or times out on
+// the loopback hub) -- the one case this cannot turn into a clean error.
+static int comm_status_exchange(vgpu_comm* c, int local_rc, vgpu_comm** out)
+{
+    if (local_rc == VGPU_OK && injected(c, "comm_init")) local_rc = VGPU_ERR_HIP, c->err = "injected failure";
+    if (!c->words) {
+        vgpu_comm_destroy(c);
+        return local_rc != VGPU_OK ? local_rc : VGPU_ERR_OOM;
+    }
+    const int W = c->world;
+    const uint64_t mine = local_rc != VGPU_OK ? (kFailTagC | (uint32_t)(-local_rc)) : 0;
+    std::vector<uint64_t> all(W, kFailTagC | (uint32_t)(-VGPU_ERR_HIP));
+    const hipStream_t st = c->st;  // null stream when the stream could not be created
+    const bool put = hipMemcpy(c->words + W, &mine, 8, hipMemcpyHostToDevice) == hipSuccess;
+    bool ok = c->x && c->x->allgather(c->words + (put ? W : W + 2), c->words, 8, st);
+    ok = ok && hipMemcpyAsync(all.data(), c->words, W * 8, hipMemcpyDeviceToHost, st) == hipSuccess &&
+         hipStreamSynchronize(st) == hipSuccess;
+    int rc = ok ? VGPU_OK : VGPU_ERR_HIP;
+    for (int k = 0; ok && k < W; ++k)
+        if (all[k] >= kFailTagC) {
+            rc = -(int)(uint32_t)(all[k] & 0xFFFFFFFFu);
+            break;
+        }
+    if (rc == VGPU_OK && !put) rc = VGPU_ERR_HIP;  // (the pre-set word already told the peers)
+    if (rc != VGPU_OK) {
+        vgpu_comm_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return VGPU_OK;
+}
 
 extern "C" int vgpu_comm_init(vgpu_ctx* ctx, int rank, int world, const uint8_t id[128], vgpu_comm** out)
-{
+try {
     if (!ctx || !id || !out || world < 1 || rank < 0 || rank >= world) return VGPU_ERR_INVALID_ARG;
     *out = nullptr;
     Rccl& R = rccl();
@@ -419,27 +483,44 @@ extern "C" int vgpu_comm_init(vgpu_ctx* ctx, int rank, int world, const uint8_t 
     auto* c = new (std::nothrow) vgpu_comm();
     if (!c) return VGPU_ERR_OOM;
     c->rank = rank;
-    // a local allocation failure here still joins ncclCommInitRank (itself collective), then fails
-    const int arc = comm_alloc(c, dev, world);
-    auto* x = new (std::nothrow) RcclExchange();
+    // the word buffer comes first; a later local failure (the stream, the exchange object, an injected
+    // "comm_init:alloc") still joins ncclCommInitRank -- itself collective, into a stack handle that needs no
+    // allocation -- and then reports through the status exchange
+    int lrc = comm_alloc(c, dev, world);
+    if (lrc == VGPU_OK && injected(c, "comm_init:alloc")) lrc = VGPU_ERR_OOM, c->err = "injected failure";
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
+    ncclComm_t comm = nullptr;
     ncclResult_t ir;
     {
         StdoutToStderr quiet;
-        ir = x ? R.init(&x->comm, world, u, rank) : ncclSystemError;
+        ir = R.init(&comm, world, u, rank);
     }
-    c->x.reset(x);
-    if (ir != ncclSuccess || arc != VGPU_OK) {
+    if (ir != ncclSuccess) {  // no communicator to exchange over: RCCL reports its own failure per rank
         vgpu_comm_destroy(c);
-        return ir != ncclSuccess ? VGPU_ERR_HIP : arc;
+        return VGPU_ERR_HIP;
     }
-    *out = c;
-    return VGPU_OK;
-}
+    auto* x = new (std::nothrow) RcclExchange();
+    if (!x) {
+        // nothing to run the status exchange through but the raw handle: a throwaway exchange on the stack
+        RcclExchange tmp;
+        tmp.comm = comm;
+        c->x.reset();
+        if (c->words) {
+            const uint64_t* src = c->words + world + 2;  // the pre-set failure word
+            (void)tmp.allgather(src, c->words, 8, c->st);
+            (void)hipStreamSynchronize(c->st);
+        }
+        vgpu_comm_destroy(c);
+        return VGPU_ERR_OOM;  // tmp's destructor destroys the RCCL communicator
+    }
+    x->comm = comm;
+    c->x.reset(x);
+    return comm_status_exchange(c, lrc, out);
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_loopback_create(int world, vgpu_loopback** out)
-{
+try {
     if (!out || world < 1) return VGPU_ERR_INVALID_ARG;
     *out = nullptr;
     auto* h = new (std::nothrow) vgpu_loopback();
@@ -450,10 +531,10 @@ extern "C" int vgpu_loopback_create(int world, vgpu_loopback** out)
     if (const char* t = std::getenv("VGPU_LOOPBACK_TIMEOUT_S")) h->timeout_s = std::max(1, std::atoi(t));
     *out = h;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_loopback_destroy(vgpu_loopback* h)
-{
+try {
     if (!h) return VGPU_OK;
     {
         std::lock_guard<std::mutex> lk(h->mu);
@@ -461,10 +542,10 @@ extern "C" int vgpu_loopback_destroy(vgpu_loopback* h)
     }
     delete h;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" int vgpu_comm_init_loopback(vgpu_ctx* ctx, int rank, vgpu_loopback* hub, vgpu_comm** out)
-{
+try {
     if (!ctx || !hub || !out || rank < 0 || rank >= hub->world) return VGPU_ERR_INVALID_ARG;
     *out = nullptr;
     int dev = 0;
@@ -484,14 +565,11 @@ extern "C" int vgpu_comm_init_loopback(vgpu_ctx* ctx, int rank, vgpu_loopback* h
     }
     c->x.reset(x);
     c->rank = rank;
-    const int rc = comm_alloc(c, dev, hub->world);
-    if (rc != VGPU_OK) {
-        vgpu_comm_destroy(c);
-        return rc;
-    }
-    *out = c;
-    return VGPU_OK;
-}
+    // the same status exchange as vgpu_comm_init: a failing rank fails every rank's creation
+    int lrc = comm_alloc(c, dev, hub->world);
+    if (lrc == VGPU_OK && injected(c, "comm_init:alloc")) lrc = VGPU_ERR_OOM, c->err = "injected failure";
+    return comm_status_exchange(c, lrc, out);
+} VGPU_ABI_CATCH
 
 extern "C" void vgpu_comm_destroy(vgpu_comm* c)
 {
@@ -555,8 +633,10 @@ static int exchange_counts(vgpu_comm* c, int local_rc, uint64_t count, std::vect
     uint64_t* dev_words = c->words;
     const uint64_t mine = local_rc != VGPU_OK ? (kFailTag | (uint32_t)(-local_rc)) : count;
     all.assign(W, 0);
-    if (hipMemcpyAsync(dev_words + W, &mine, 8, hipMemcpyHostToDevice, c->st) != hipSuccess ||
-        !c->x->allgather(dev_words + W, dev_words, 8, c->st) ||
+    // the all-gather is entered whatever happens to this rank's word: when its copy to the device fails, the
+    // pre-set failure word (comm_alloc) is sent instead, so the peers fail with this rank instead of waiting
+    const bool put = hipMemcpyAsync(dev_words + W, &mine, 8, hipMemcpyHostToDevice, c->st) == hipSuccess;
+    if (!c->x->allgather(dev_words + (put ? W : W + 2), dev_words, 8, c->st) || !put ||
         hipMemcpyAsync(all.data(), dev_words, W * 8, hipMemcpyDeviceToHost, c->st) != hipSuccess ||
         hipStreamSynchronize(c->st) != hipSuccess) {
         c->err = "count exchange (all-gather) failed";
@@ -632,7 +712,7 @@ static int comm_enter(vgpu_ctx* ctx, vgpu_comm* comm)
 extern "C" int vgpu_prm_vertices_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const vgpu_robot* r, vgpu_env* e,
                                            uint64_t first, size_t n_draws_total, float* rows, uint64_t* draws,
                                            size_t cap, size_t* count)
-{
+try {
     if (!comm) return VGPU_ERR_INVALID_ARG;  // no communicator: nothing to enter (a caller bug on this rank)
     comm->err.clear();
     if (count) *count = 0;
@@ -685,12 +765,12 @@ extern "C" int vgpu_prm_vertices_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const
     if ((rc = gather_padded(comm, pad_draws, all_d, cnts, sizeof(uint64_t), draws)) != VGPU_OK) return rc;
     *count = (size_t)total;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 // Query ranges of equal prefix work: query i scans i candidates, so rank k takes [n sqrt(k/W), n sqrt((k+1)/W))
 // rounded half up (vamp_amd.roadmap.query_split is the same expression).
 extern "C" int vgpu_query_split(size_t n, int rank, int world, size_t* first, size_t* count)
-{
+try {
     if (world < 1 || rank < 0 || rank >= world || !first || !count) return VGPU_ERR_INVALID_ARG;
     auto bound = [&](int k) -> size_t {
         if (k <= 0) return 0;
@@ -701,7 +781,7 @@ extern "C" int vgpu_query_split(size_t n, int rank, int world, size_t* first, si
     *first = bound(rank);
     *count = bound(rank + 1) - *first;
     return VGPU_OK;
-}
+} VGPU_ABI_CATCH
 
 extern "C" hipError_t vgpu_launch_valid_pairs(uint32_t q_first, uint32_t q_count, const uint32_t* nbr, uint32_t kmax,
                                               const uint32_t* cnt, const uint32_t* off, const uint8_t* ok, size_t E,
@@ -719,7 +799,7 @@ extern "C" int vgpu_prm_edges_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const vg
                                         const float* V, size_t n, double space_measure, double gamma_scale,
                                         uint64_t* offsets, uint32_t* adj, size_t adj_cap, size_t* n_adj,
                                         uint32_t* component)
-{
+try {
     if (!comm) return VGPU_ERR_INVALID_ARG;  // no communicator: nothing to enter (a caller bug on this rank)
     comm->err.clear();
     if (n_adj) *n_adj = 0;
@@ -824,4 +904,4 @@ extern "C" int vgpu_prm_edges_allgather(vgpu_ctx* ctx, vgpu_comm* comm, const vg
     return rank_fail(comm, ctx,
                      vgpu_roadmap_assemble_device(ctx, n, (const uint32_t*)pairs, (size_t)m, offsets, adj, component),
                      "roadmap assembly");
-}
+} VGPU_ABI_CATCH

@@ -19,7 +19,7 @@ VGPU_ROBOT_FETCH = 2
 VGPU_ROBOT_PANDA_PAIR = 3
 VGPU_ROBOT_UR5 = 4
 VGPU_ROBOT_BAXTER = 5
-ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of memory", -4: "unsupported", -5: "host rsqrt probe"}
+ERRORS = {-1: "invalid argument", -2: "HIP error", -3: "out of memory", -4: "unsupported", -5: "host rsqrt probe", -6: "internal (C++ exception inside the library)"}
 
 F32P = C.POINTER(C.c_float)
 U8P = C.POINTER(C.c_uint8)

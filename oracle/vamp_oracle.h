@@ -195,6 +195,8 @@ void vo_panda_validate_motions(const vo_env *env, const float *starts, const flo
  * fkcc_A && fkcc_B && no A-B sphere overlap (link-bounding pairs first, then their spheres). */
 int vo_pair_fkcc_block(const vo_env *env, const float *q, int G, const int ba100[3], const int bb100[3],
                        vo_stats *stats);
+int vo_pair_validate_vector(const vo_env *env, const float start[14], const float v[14], float distance,
+                            const int ba100[3], const int bb100[3], int *n_out, vo_stats *st);
 int vo_pair_validate_motion(const vo_env *env, const float start[14], const float goal[14], const int ba100[3],
                             const int bb100[3], int *n_out, vo_stats *stats);
 void vo_pair_fkcc_configs(const vo_env *env, const float *q, size_t n, const int ba100[3], const int bb100[3],

@@ -553,6 +553,24 @@ def pair_validate_motions(env: Env, starts, goals, ba=(0, 0, 0), bb=(100, 0, 0),
     return ok.astype(bool), n
 
 
+def pair_validate_vector(env_c, start, vector, distance, ba=(0, 0, 0), bb=(100, 0, 0)):
+    """validate_vector<Composite, 8, 32>(start, vector, distance) (planning/validate.hh:23-65, oracle
+    vo_pair_validate_vector); env_c is Env.c() (kept alive by the caller across calls)"""
+    s = np.ascontiguousarray(start, np.float32)
+    v = np.ascontiguousarray(vector, np.float32)
+    L = lib()
+    L.vo_pair_validate_vector.argtypes = [C.c_void_p, F32P, F32P, C.c_float, C.c_void_p, C.c_void_p, C.c_void_p,
+                                          C.c_void_p]
+    return bool(L.vo_pair_validate_vector(C.byref(env_c), fp(s), fp(v), float(distance), _i3(ba), _i3(bb), None,
+                                          None))
+
+
+def pair_scale(u):
+    """the composite's scale_configuration: each arm's seven joints by the Panda's limits"""
+    u = np.ascontiguousarray(u, np.float32).reshape(-1, 14)
+    return np.concatenate([robot_scale("panda", u[:, :7]), robot_scale("panda", u[:, 7:])], axis=1)
+
+
 def pair_scene() -> Env:
     """Config-5 scene: a table surface under both arms plus three spheres between them."""
     e = Env()

@@ -14,11 +14,37 @@ F = np.float32
 FMAX = np.finfo(np.float32).max
 
 
+def fma_sq(a, c):
+    """float32 fma(a, a, c), correctly rounded (one rounding of a*a + c), vectorised: a*a is exact in float64,
+    TwoSum gives the float64 sum's error, and a sum that sits exactly on a float32 rounding midpoint is nudged
+    toward the error's sign so the float32 conversion rounds the exact value"""
+    a64 = np.asarray(a, np.float64)
+    c64 = np.asarray(c, np.float64)
+    p = a64 * a64
+    s = p + c64
+    bv = s - p
+    e = (p - (s - bv)) + (c64 - bv)
+    r = s.astype(F)
+    other = np.nextafter(r, np.where(s > r, np.inf, -np.inf).astype(F)).astype(F)
+    mid = (r.astype(np.float64) + other.astype(np.float64)) / 2
+    tie = (s == mid) & (e != 0)
+    if tie.any():
+        s = np.where(tie, np.nextafter(s, s + e), s)
+        r = s.astype(F)
+    return r
+
+
 def l2_rows(d):
-    """FloatVector<dim>::l2_norm of each row (dim <= 8: one register, hsum order of avx.hh:441-452)"""
+    """FloatVector<dim>::l2_norm of each row (hsum order of avx.hh:441-452; dim <= 8: one register; dim 9-16:
+    two, combined lane-wise as fma(lo, lo, hi * hi) by the release build -- ref_probe l2norm)"""
     d = np.asarray(d, F)
     s = np.zeros((d.shape[0], 8), F)
-    s[:, :d.shape[1]] = d * d
+    if d.shape[1] <= 8:
+        s[:, :d.shape[1]] = d * d
+    else:
+        hi = np.zeros((d.shape[0], 8), F)
+        hi[:, :d.shape[1] - 8] = d[:, 8:]
+        s[:] = fma_sq(d[:, :8], (hi * hi).astype(F))
     a = (s[:, 0] + s[:, 4]) + (s[:, 2] + s[:, 6])
     b = (s[:, 1] + s[:, 5]) + (s[:, 3] + s[:, 7])
     return np.sqrt(a + b).astype(F)
@@ -35,7 +61,12 @@ def rrtc(robot, oenv, start, goals, settings, rng_index, base100=(0, 0, 0)):
     goals = np.asarray(goals, F).reshape(-1, dim)
 
     def vv(s, v, d):
+        if robot == "pair":  # the configs[4] composite: base100 = (arm A's base, arm B's base)
+            return op.pair_validate_vector(ec, s, v, d, *base100)
         return op.robot_validate_vector(robot, ec, s, v, d, base100)
+
+    def scale(u):
+        return op.pair_scale(u) if robot == "pair" else op.robot_scale(robot, u)
 
     for g in goals:  # rrtc.hh:61-73
         if vv(start, (g - start).astype(F), l2_rows((g - start)[None])[0]):
@@ -73,7 +104,7 @@ def rrtc(robot, oenv, start, goals, settings, rng_index, base100=(0, 0, 0)):
         if (not S["balance"]) or ratio < F(S["tree_ratio"]):
             ta, tb = tb, ta
             tree_a_is_start = not tree_a_is_start
-        temp = op.robot_scale(robot, op.halton(dim, [rng_index]))[0]
+        temp = scale(op.halton(dim, [rng_index]))[0]
         rng_index += 1
         nn, nd = nearest(ta, temp)
         nr = radii[nn]

@@ -52,6 +52,31 @@ def test_exports_are_c_abi():
         assert name in exported, f"{name} not exported unmangled"
 
 
+def test_no_exception_crosses_the_abi():
+    """Every multi-statement int entry point of the host runtime is a function-try-block ending in
+    VGPU_ABI_CATCH (mr-vamp_amd/csrc/vgpu_abi.hh): a C++ exception inside the library comes back as
+    VGPU_ERR_OOM / VGPU_ERR_INTERNAL instead of terminating the caller's process."""
+    csrc = os.path.join(ROOT, "mr-vamp_amd", "csrc")
+    files = ["vgpu_api.cpp", "vgpu_multi.cpp", "cpu/vcpu.cpp", "cpu/vcpu_roadmap.cpp", "cpu/vcpu_rrtc.cpp"]
+    seen = 0
+    for f in files:
+        lines = open(os.path.join(csrc, f)).read().split("\n")
+        for i, l in enumerate(lines):
+            if not l.startswith('extern "C" int ') or l.rstrip().endswith(";") or "{" in l:
+                continue
+            j = i
+            while lines[j] not in ("{", "try {"):
+                assert not lines[j].rstrip().endswith(";"), (f, i)
+                j += 1
+            assert lines[j] == "try {", f"{f}:{i + 1}: {l.strip()} is not a function-try-block"
+            k = j + 1
+            while not lines[k].startswith("}"):
+                k += 1
+            assert lines[k] == "} VGPU_ABI_CATCH", f"{f}:{k + 1}"
+            seen += 1
+    assert seen >= 80
+
+
 def test_errors_without_context(lib):
     # argument validation paths need no device
     assert lib.vgpu_sync(None) == -1

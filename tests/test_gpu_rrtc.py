@@ -84,3 +84,30 @@ def test_table_pick_straight_lines_gpu(vamp, oracle):
         ref.append(fx[f"p{k}_ok"][0])
         keep.append(stable(fx[f"p{k}_test_margin"], fx[f"p{k}_cull_margin"], same)[0])
     fixture_check("panda table_pick start->goal (GPU)", np.array(got), np.array(ref), np.array(keep), same, 0.5)
+
+
+def test_pair_rrtc_paths_revalidated_on_gpu(vamp, oracle):
+    """configs[4] "2x Panda composite RRT-Connect with inter-robot collision": 16 composite problems on the
+    configs[4] scene whose straight edge fails (tests/test_rrtc.py pair_problems) planned on the CPU rake
+    (vamp_amd.panda_pair.rrtc, rrtc.hh:33-248), and every segment of every path then validated as one edge batch
+    through the HIP path (vgpu_validate_motions, the composite's chained staged passes) == the oracle's composite
+    validate_motion == the CPU rake, and valid."""
+    from test_rrtc import PAIR_BASES, pair_problems
+    o, S, G = pair_problems(oracle, 16)
+    env = gpu_env_from_oracle(vamp, o)
+    robot = vamp.panda_pair
+    segs_a, segs_b = [], []
+    for k in range(16):
+        res = robot.rrtc(S[k], G[k], env, vamp.RRTCSettings(**SETTINGS), robot.halton())
+        assert res.solved, f"composite problem {k} unsolved"
+        segs_a.append(res.path[:-1])
+        segs_b.append(res.path[1:])
+    a, b = np.concatenate(segs_a), np.concatenate(segs_b)
+    ok_gpu, n_gpu = robot.validate_batch(a, b, env)
+    ok_cpu, n_cpu, _ = robot.cpu_validate_batch(a, b, env)
+    ok_ora, n_ora = oracle.pair_validate_motions(o, a, b, *PAIR_BASES)
+    assert np.array_equal(n_gpu, n_ora) and np.array_equal(n_cpu, n_ora)
+    assert np.array_equal(ok_gpu, ok_ora.astype(bool)) and np.array_equal(ok_cpu, ok_gpu)
+    assert ok_gpu.all()
+    print(f"configs[4] composite RRT-Connect: 16/16 solved, {len(a)} path segments re-validated on the GPU, "
+          f"0 mismatches vs oracle and CPU rake")

@@ -424,3 +424,78 @@ def test_loopback_rank_failure_reaches_every_rank(loopback_ranks, monkeypatch, w
         assert _run_ranks(world, call) == [-1] * world, key
         null[key] = False
     assert _run_ranks(world, call) == [0] * world
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("site", ["comm_init", "comm_init:alloc"])
+def test_loopback_comm_init_failure_reaches_every_rank(monkeypatch, world, site):
+    """Communicator creation ends in a status all-gather (vgpu_multi.cpp comm_status_exchange): a failure on
+    rank 1 only -- after every allocation, or its stream / exchange allocation -- makes EVERY rank's
+    vgpu_comm_init_loopback return the same code and hand back no communicator, at once (no rank is left to
+    block in its first stage's all-gather; the loopback timeout is set far above the test's limit)."""
+    import time
+
+    import vamp_amd as vamp
+    from vamp_amd import roadmap
+    from vamp_amd._lib import load
+    lib = load()
+    monkeypatch.setenv("VGPU_LOOPBACK_TIMEOUT_S", "600")
+    ctxs = [vamp.Context(0) for _ in range(world)]
+    hub = roadmap.Loopback(world)
+    code = -2 if site == "comm_init" else -3
+    monkeypatch.setenv("VGPU_FAULT_INJECT", f"{site}@1")
+    handles = [C.c_void_p() for _ in range(world)]
+    t = time.perf_counter()
+    got = _run_ranks(world, lambda r: lib.vgpu_comm_init_loopback(ctxs[r].h, r, hub.h, C.byref(handles[r])))
+    assert time.perf_counter() - t < 30
+    assert got == [code] * world, got
+    assert not any(h.value for h in handles)
+    monkeypatch.delenv("VGPU_FAULT_INJECT")
+    comms = _run_ranks(world, lambda r: roadmap.Comm(ctxs[r], r, world, hub=hub))  # the hub is still usable
+    for c in comms:
+        c.close()
+    hub.close()
+
+
+@pytest.mark.gpu
+def test_loopback_rank_that_never_arrives_fails_the_hub_for_good(monkeypatch):
+    """a peer that never enters an exchange makes the waiting ranks fail after
+    VGPU_LOOPBACK_TIMEOUT_S, and the hub stays failed -- a late rank cannot pair up with the next call's
+    exchange -- so every later stage call on it fails at once instead of mixing data of different calls."""
+    import time
+
+    import torch
+
+    import vamp_amd as vamp
+    from vamp_amd import roadmap
+    from vamp_amd._lib import load
+    lib = load()
+    monkeypatch.setenv("VGPU_LOOPBACK_TIMEOUT_S", "2")
+    world = 2
+    ctxs = [vamp.Context(0) for _ in range(world)]
+    hub = roadmap.Loopback(world)
+    comms = _run_ranks(world, lambda r: roadmap.Comm(ctxs[r], r, world, hub=hub))
+    env = vamp.Environment()
+    env.add_sphere(vamp.Sphere([0.5, 0.0, 0.5], 0.3))
+    for c in ctxs:
+        env.handle(c)
+    robot = vamp.panda_0_0
+    n = 4000
+    bufs = [(torch.zeros((n, 7), dtype=torch.float32, device="cuda"), torch.zeros(n, dtype=torch.int64, device="cuda"))
+            for _ in range(world)]
+    torch.cuda.synchronize()
+
+    def call(r):
+        cnt = C.c_size_t()
+        return _vertices_call(lib, vamp, ctxs[r], comms[r], robot, env, 1, n, bufs[r][0], bufs[r][1], n, cnt)
+
+    t = time.perf_counter()
+    assert call(0) != 0  # rank 1 never arrives: rank 0 times out instead of hanging
+    assert time.perf_counter() - t < 20
+    t = time.perf_counter()
+    assert _run_ranks(world, call) == [-2, -2]
+    assert time.perf_counter() - t < 20  # failed hub: no further waiting
+    for c in comms:
+        c.close()
+    hub.close()

@@ -122,3 +122,43 @@ def test_rrtc_rng_and_settings(vamp, oracle):
     blocked.add_sphere(vamp.Sphere([0.0, 0.0, 0.4], 0.6))
     r = robot.rrtc(s, g, blocked, vamp.RRTCSettings(range=1.0, max_iterations=200, max_samples=1000), robot.halton())
     assert not r.solved and r.path.shape == (0, 7) and r.iterations == 201
+
+
+# ---- BASELINE configs[4]'s planner half: RRT-Connect on the two-Panda composite -------------------------------
+PAIR_BASES = ((0, 0, 0), (100, 0, 0))  # vamp_amd.panda_pair: arm A at the origin, arm B 1 m along x
+
+
+def pair_problems(oracle, n, seed=41):
+    """configs[4]'s scene (oracle_py.pair_scene: a table under both arms, three spheres between them) and n
+    start/goal composite configurations, collision-free, whose straight validate_motion FAILS (so the planner
+    has to search), from seeded uniform draws -- no reference counterpart (SURVEY §0 finding 10): the anchor is
+    rrtc.hh:33-248 over the composed validity"""
+    o = oracle.pair_scene()
+    rng = np.random.default_rng(seed)
+    q = oracle.pair_scale(rng.random((40 * n, 14), dtype=F))
+    q = q[oracle.pair_fkcc_threads(o, q, *PAIR_BASES)]
+    s, g = q[0::2][:8 * n], q[1::2][:8 * n]
+    m = min(len(s), len(g))
+    ok, _ = oracle.pair_validate_motions(o, s[:m], g[:m], *PAIR_BASES)
+    hard = np.nonzero(~ok.astype(bool))[0][:n]
+    assert len(hard) == n
+    return o, s[hard], g[hard]
+
+
+@pytest.mark.parametrize("k", range(6))
+def test_pair_rrtc_matches_restatement(vamp, oracle, k):
+    """vamp_amd.panda_pair.rrtc == the Python restatement over the oracle's composite validate_vector
+    (oracle vo_pair_validate_vector), Halton<14> and the two-register l2_norm: path bit for bit, cost,
+    iterations, tree sizes, sampler index; every segment of the path passes the oracle's validate_motion."""
+    o, S, G = pair_problems(oracle, 6)
+    env = gpu_env_from_oracle(vamp, o)
+    robot = vamp.panda_pair
+    rng = robot.halton()
+    res = robot.rrtc(S[k], G[k], env, vamp.RRTCSettings(**SETTINGS), rng)
+    p, cost, it, sizes, idx = rrtc_py.rrtc("pair", o, S[k], G[k], SETTINGS, 1, PAIR_BASES)
+    assert res.solved and len(p) > 2
+    assert res.iterations == it and res.size == sizes and rng.index == idx
+    assert np.array_equal(res.path.view(np.uint32), p.view(np.uint32))
+    assert np.float32(res.cost).view(np.uint32) == np.float32(cost).view(np.uint32)
+    ok, _ = oracle.pair_validate_motions(o, res.path[:-1], res.path[1:], *PAIR_BASES)
+    assert ok.all(), np.nonzero(~ok.astype(bool))[0]

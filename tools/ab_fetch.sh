@@ -20,8 +20,10 @@ run() {  # spec, command...
   env VAMP_AMD_LIB=$(lib $v) $(echo $envs | tr ',' ' ') "$@"
 }
 for s in "$@"; do
-  run $s timeout -k 10 300 python -u -m pytest tests/test_gpu_fetch.py tests/test_gpu_roadmap.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/abf_${T}_parity.log 2>&1 || { tail -30 gpurun_out/abf_${T}_parity.log; exit 1; }
-  echo "$s parity: $(tail -n 1 gpurun_out/abf_${T}_parity.log)"
+  # one parity log per spec (round 5's single log was overwritten per spec, so an abort did not say whose it was)
+  P=gpurun_out/abf_${T}_parity_$(echo $s | tr ':,=' '___').log
+  run $s timeout -k 10 300 python -u -m pytest tests/test_gpu_fetch.py tests/test_gpu_roadmap.py -m gpu -x -v --timeout 200 --timeout-method thread > $P 2>&1 || { echo "spec $s failed: $P"; tail -30 $P; exit 1; }
+  echo "$s parity: $(tail -n 1 $P)"
 done
 for r in 1 2; do
   for s in "$@"; do

@@ -9,7 +9,8 @@ not the contract bench).
 `run` loads the inputs, builds the environment (its upload kernels -- the CAPT cell grid -- are
 excluded from the summaries by kernel name), runs one warm-up call and C measured calls of the
 workload's step, and writes $TMPDIR/vamp_pmc_inputs/W.meta.json (units per call, calls) for
-tools/pmc_report.py.  Workloads: validate (configs[1] set B, 2^20 edges), validate_setA, capt
+tools/pmc_report.py.  Workloads: validate (configs[1] set B, 2^20 edges), validate_setA, validate_table_pick (set B edges on the MBM
+table_pick scene), rrtc / rrtc_pair (configs[0] / configs[4]'s planner: the solved paths' segments as one batch), capt
 (configs[2], 2^20 configurations), fetch_prm (configs[3] vertex stage, 4M draws: the fused
 sample+fkcc and the compaction), prm_edges (configs[3] edge stage: kNN + gather + validation +
 pair selection + device assembly through vgpu_prm_edges_allgather at world size 1; prm_edges_full: at
@@ -31,16 +32,36 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 import bench  # noqa: E402
 
 OUT = os.path.join(os.environ.get("TMPDIR", "/tmp"), "vamp_pmc_inputs")  # large inputs: outside gpurun_out
-WORKLOADS = ("validate", "validate_setA", "capt", "fetch_prm", "prm_edges", "prm_edges_full", "pair")
+WORKLOADS = ("validate", "validate_setA", "validate_table_pick", "capt", "fetch_prm", "prm_edges", "prm_edges_full",
+             "pair", "rrtc", "rrtc_pair")
 
 
 def setup(torch, vamp, w, dev, ctx, prep, inp, a):
     """(step(), units per call, unit name, extra meta) of workload w; prep=True builds and saves inputs"""
     path = os.path.join(OUT, f"{w}.npz")
-    if w in ("validate", "validate_setA"):
-        env = vamp.Environment()
-        for c in bench.CAGE:
-            env.add_sphere(vamp.Sphere(c, 0.2))
+    if w in ("rrtc", "rrtc_pair"):  # the bench line's GPU leg: every solved path's segments, one validate batch
+        if prep:
+            return None
+        envs, S, G, robot, _ = bench.rrtc_problems(vamp, "panda_pair" if w == "rrtc_pair" else "panda")
+        if w == "rrtc":  # one scene per problem: the first problem's segments (the bench line's largest batch)
+            envs, S, G = envs[:1], S[:1], G[:1]
+        res = [robot.rrtc(S[k], G[k], envs[k], bench.RRTC_SETTINGS(vamp), robot.halton()) for k in range(len(S))]
+        a_ = torch.from_numpy(np.concatenate([r.path[:-1] for r in res])).to(dev)
+        b_ = torch.from_numpy(np.concatenate([r.path[1:] for r in res])).to(dev)
+        E = a_.shape[0]
+        ok = torch.empty(E, dtype=torch.uint8, device=dev)
+        nb = torch.empty(E, dtype=torch.int32, device=dev)
+        env = envs[0]
+        env.handle(ctx)
+        return (lambda: robot.validate_device(a_.data_ptr(), b_.data_ptr(), E, env, ok.data_ptr(), nb.data_ptr(), ctx),
+                E, "path segments", {})
+    if w in ("validate", "validate_setA", "validate_table_pick"):
+        if w == "validate_table_pick":
+            env, _, _ = bench.scene_envs(vamp, "table_pick")
+        else:
+            env = vamp.Environment()
+            for c in bench.CAGE:
+                env.add_sphere(vamp.Sphere(c, 0.2))
         robot = vamp.panda_0_0
         E = a.edges
         if prep:
