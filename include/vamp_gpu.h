@@ -413,7 +413,11 @@ int vgpu_multi_sample_fkcc_host(vgpu_multi *m, const vgpu_robot *robot, vgpu_env
                                 size_t n_draws, float *rows_out, uint64_t *draws_out, size_t *count);
 /* One process per GPU: RCCL communicators (librccl.so.1 loaded at run time; VGPU_ERR_UNSUPPORTED without
  * it).  Rank 0 makes the 128-byte id, the caller ships it to the other ranks (any side channel), every
- * rank calls vgpu_comm_init with its own context current. */
+ * rank calls vgpu_comm_init with its own context current.  Creation is collective and ends in a status
+ * all-gather: when any rank fails (its stream or exchange allocation, RCCL, or VGPU_FAULT_INJECT=comm_init
+ * [:alloc][@rank]), EVERY rank destroys its communicator and returns the same code (the lowest failing rank's),
+ * *comm stays NULL -- no rank is left to block in its first stage's all-gather.  (A rank whose 24-byte word
+ * buffer cannot be allocated cannot join that exchange; its peers then fail inside RCCL.) */
 typedef struct vgpu_comm vgpu_comm;
 int vgpu_comm_unique_id(uint8_t id[128]);
 int vgpu_comm_init(vgpu_ctx *ctx, int rank, int world, const uint8_t id[128], vgpu_comm **out);
@@ -424,8 +428,10 @@ const char *vgpu_comm_last_error(const vgpu_comm *comm);
  * its own context (on one device or several); the stages' all-gathers become a barrier plus device copies
  * from every peer.  Same stage semantics as RCCL -- it runs the multi-rank logic (rank-order concatenation,
  * count padding, failure words) at world size > 1 without a multi-GPU job.  A rank that does not arrive
- * within VGPU_LOOPBACK_TIMEOUT_S seconds (default 120) makes its peers' exchange fail instead of hang.
- * vgpu_loopback_destroy fails (VGPU_ERR_INVALID_ARG) while communicators still use the hub. */
+ * within VGPU_LOOPBACK_TIMEOUT_S seconds (default 120) makes its peers' exchange fail instead of hang, and
+ * the hub stays failed (every later exchange on it fails at once: a late rank never pairs with a later call).
+ * vgpu_comm_init_loopback is collective like vgpu_comm_init (one call per rank, from one thread each; the same
+ * status exchange).  vgpu_loopback_destroy fails (VGPU_ERR_INVALID_ARG) while communicators still use the hub. */
 typedef struct vgpu_loopback vgpu_loopback;
 int vgpu_loopback_create(int world, vgpu_loopback **out);
 int vgpu_loopback_destroy(vgpu_loopback *hub);

@@ -314,6 +314,11 @@ struct vgpu_env {
     size_t dev_floats = 0;
 };
 
+// A context's device made current for this thread, and the thread's last HIP error cleared: a HANDLED failure of an
+// earlier call (e.g. vgpu_ctx_create on a device that does not exist) must not be read back by this call's first
+// hipGetLastError() after a kernel launch and reported as this call's failure
+#define ctx_device(c) (hipSetDevice((c)->device) == hipSuccess ? ((void)hipGetLastError(), hipSuccess) \
+                                                                 : hipSetDevice((c)->device))
 #define HIPCHK(ctx, expr)                                                                          \
     do {                                                                                           \
         hipError_t e_ = (expr);                                                                    \
@@ -345,6 +350,7 @@ try {
     }
     c->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        (void)hipGetLastError();  // handled here: not a later call's failure
         delete c;
         return VGPU_ERR_HIP;
     }
@@ -395,7 +401,7 @@ try {
 extern "C" int vgpu_debug_violations(vgpu_ctx* c, vgpu_env* e, uint32_t out[2])
 try {
     if (!c || !out) return VGPU_ERR_INVALID_ARG;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     uint32_t a[2] = {0, 0}, b[2] = {0, 0};
     HIPCHK(c, hipMemcpy(a, c->dbg, 8, hipMemcpyDeviceToHost));
@@ -454,7 +460,7 @@ try {
 extern "C" int vgpu_sync(vgpu_ctx* c)
 try {
     if (!c) return VGPU_ERR_INVALID_ARG;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     return VGPU_OK;
 } VGPU_ABI_CATCH
@@ -462,7 +468,7 @@ try {
 extern "C" int vgpu_ctx_set_profiling(vgpu_ctx* c, int enable)
 try {
     if (!c) return VGPU_ERR_INVALID_ARG;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     for (auto& ev : c->ev)
         if (!ev) HIPCHK(c, hipEventCreate(&ev));
     c->prof = enable != 0;
@@ -491,7 +497,7 @@ try {
 extern "C" int vgpu_rsqrt_table_set(vgpu_ctx* c, const uint32_t* table, int kbits)
 try {
     if (!c || !table || kbits < 1 || kbits > 23) return fail(c, VGPU_ERR_INVALID_ARG, "bad rsqrt table");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     c->lut.assign(table, table + ((size_t)2 << kbits));
     if (c->lut_dev) (void)hipFree(c->lut_dev);
@@ -712,7 +718,7 @@ try {
     if (!c || !e || (e->ctx && e->ctx != c) || (n && !points))
         return fail(c, VGPU_ERR_INVALID_ARG, "bad add_pointcloud_device");
     if (n == 0 || n > ((size_t)1 << 26)) return fail(c, VGPU_ERR_INVALID_ARG, "point cloud size");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     vgpu::CaptTree t;
     HIPCHK(c, vgpu::capt_build_device(points, n, r_min, r_max, r_point, c->cur, t));
     if (build_ns) *build_ns = t.build_ns;
@@ -1054,7 +1060,7 @@ try {
     if (!c) return VGPU_ERR_INVALID_ARG;  // host-only environment
     if (!e->dirty && !e->pc_dirty && e->dev) return VGPU_OK;
     std::lock_guard<std::mutex> lock(e->host_mu);  // the builds re-sort the host rows
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (e->dev && !e->pc_dirty) {  // the tail alone, in place, when it still fits the allocation
         std::vector<float> tail;
         build_tail(e, e->dev_lay, tail, e->tail_off);
@@ -1113,7 +1119,7 @@ try {
     if (int rc = vgpu_env_upload(e)) return rc;
     vgpu_ctx* c = e->ctx;
     float hd[kExtHdr];
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     HIPCHK(c, hipMemcpy(hd, e->dev + e->dev_lay.pc_off + (size_t)kExtHdr * index, sizeof(hd), hipMemcpyDeviceToHost));
     const int f[4] = {PC_GNX, PC_GNY, PC_GNZ, PC_GCELLS};
@@ -1246,7 +1252,7 @@ try {
     int rc = check_robot(c, r, b);
     if (rc) return rc;
     if (n && (!q || !xyz || ld < n)) return fail(c, VGPU_ERR_INVALID_ARG, "bad sphere_fk arguments");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (r->kind == VGPU_ROBOT_FETCH) {
         HIPCHK(c, vgpu_launch_fetch_sphere_fk(q, n, xyz, ld, c->cur));
         return VGPU_OK;
@@ -1518,7 +1524,7 @@ try {
     if (n && (!q || !valid)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (const RobotOps* g = generic_ops(r->kind)) {
         if (c->staged && g->staged)
             return chain_pass(c, generic_chain(r->kind), 0, q, nullptr, nullptr, nullptr, 0, n, &v, b, valid);
@@ -1555,7 +1561,7 @@ try {
     if (r->kind == VGPU_ROBOT_BAXTER) return vgpu_fkcc(c, r, e, q, n, valid);  // Baxter::fkcc_attach = fkcc
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (r->kind == VGPU_ROBOT_FETCH)
         HIPCHK(c, vgpu_launch_fetch_fkcc_attach(q, n, &v, valid, c->cur));
     else if (r->kind == VGPU_ROBOT_UR5)
@@ -1623,7 +1629,7 @@ try {
         return fail(c, VGPU_ERR_UNSUPPORTED, "attachments: no fkcc_attach for the composite");
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     uint32_t *cnt, *off;
     void* tmp;
     size_t tmp_bytes;
@@ -1738,7 +1744,7 @@ try {
     if (n_edges >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many edges in one call (< 2^31)");
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     uint32_t *cnt, *off;
     void* tmp;
     size_t tmp_bytes;
@@ -1778,7 +1784,7 @@ try {
     int rc = vgpu_env_upload(e);
     if (rc) return rc;
     const EnvView v = make_view(e);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, vgpu_launch_capt_query(centers, radii, n, &v, index, simd, out, c->cur));
     return VGPU_OK;
 } VGPU_ABI_CATCH
@@ -1793,7 +1799,7 @@ try {
     *count = 0;
     if (n == 0) return VGPU_OK;
     if (!pc || !out_idx || n > 0x7fffffffu) return fail(c, VGPU_ERR_INVALID_ARG, "bad filter_pointcloud arguments");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, vgpu_filter_pointcloud_run(pc, n, min_dist, max_range, origin, ws_min, ws_max, cull, out_idx, count,
                                          c->cur));
     return VGPU_OK;
@@ -1827,7 +1833,7 @@ try {
     if (!pc || !keep) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     constexpr int kSmallFloats = 16 + 4 * 128;
     if (!c->small) HIPCHK(c, hipMalloc((void**)&c->small, kSmallFloats * sizeof(float)));
     // [0, 16) configuration, [16, 16 + 3S) sphere_fk centres (ld = 1), then the radii
@@ -1849,7 +1855,7 @@ try {
     if (dim < 1 || dim > 16 || first == 0) return fail(c, VGPU_ERR_INVALID_ARG, "dim must be 1..16, first >= 1");
     if (n == 0) return VGPU_OK;
     if (!out) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, vgpu_launch_halton(dim, first, n, out, c->cur));
     return VGPU_OK;
 } VGPU_ABI_CATCH
@@ -1862,7 +1868,7 @@ try {
     if (first == 0) return fail(c, VGPU_ERR_INVALID_ARG, "draw indices start at 1");
     if (n == 0) return VGPU_OK;
     if (!q) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (r->kind == VGPU_ROBOT_PANDA_PAIR) return fail(c, VGPU_ERR_UNSUPPORTED, "no sampler for the composite");
     if (const RobotOps* g = generic_ops(r->kind))
         HIPCHK(c, g->sample(first, n, q, c->cur));
@@ -1885,7 +1891,7 @@ try {
     if (!valid) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
     if ((rc = vgpu_env_upload(e))) return rc;
     const EnvView v = make_view(e);
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (r->kind == VGPU_ROBOT_PANDA_PAIR) return fail(c, VGPU_ERR_UNSUPPORTED, "no sampler for the composite");
     if (c->staged && !q) {  // the children stage reads the bound stage's samples back
         int32_t dim = 0;
@@ -1919,7 +1925,7 @@ try {
     if (!valid || !index_out || (rows_out && !rows)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffer");
     const size_t tmp = vgpu_compact_bytes(n);
     const size_t need = 256 + tmp;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (need > c->aux_bytes) {
         if (c->aux) {
             HIPCHK(c, hipStreamSynchronize(c->cur));
@@ -1944,7 +1950,7 @@ try {
 // *_host entry point enqueues after it belong to that device (HIP's current device is per thread).
 static int stage(vgpu_ctx* c, size_t bytes, char** p)
 {
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (bytes > c->stage_bytes) {
         if (c->stage) {
             HIPCHK(c, hipStreamSynchronize(c->cur));
@@ -1984,7 +1990,7 @@ try {
     const size_t qb = al(n * dim_of(r) * 4), ob = (size_t)3 * spheres_of(r) * n * 4;
     int rc = stage(c, qb + ob, &d);
     if (rc) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipMemcpyAsync(d, q, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     if ((rc = vgpu_sphere_fk(c, r, (const float*)d, n, (float*)(d + qb), n))) return rc;
     HIPCHK(c, hipMemcpyAsync(xyz, d + qb, ob, hipMemcpyDeviceToHost, c->cur));
@@ -2001,7 +2007,7 @@ try {
     const size_t qb = al(n * dim_of(r) * 4);
     int rc = stage(c, qb + n, &d);
     if (rc) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipMemcpyAsync(d, q, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     if ((rc = vgpu_fkcc(c, r, e, (const float*)d, n, (uint8_t*)(d + qb)))) return rc;
     HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
@@ -2018,7 +2024,7 @@ try {
     const size_t qb = al(n * dim_of(r) * 4);
     int rc = stage(c, qb + n, &d);
     if (rc) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipMemcpyAsync(d, q, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     if ((rc = vgpu_fkcc_attach(c, r, e, (const float*)d, n, (uint8_t*)(d + qb)))) return rc;
     HIPCHK(c, hipMemcpyAsync(valid, d + qb, n, hipMemcpyDeviceToHost, c->cur));
@@ -2036,7 +2042,7 @@ try {
     const size_t okb = al(n), nbb = al(n * 4);
     int rc = stage(c, 2 * qb + okb + nbb, &d);
     if (rc) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipMemcpyAsync(d, starts, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     HIPCHK(c, hipMemcpyAsync(d + qb, goals, n * dim_of(r) * 4, hipMemcpyHostToDevice, c->cur));
     uint8_t* okd = (uint8_t*)(d + 2 * qb);
@@ -2061,7 +2067,7 @@ try {
     const size_t pb = al(n * 12);
     int rc = stage(c, pb + n * 4, &d);
     if (rc) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipMemcpyAsync(d, pc, n * 12, hipMemcpyHostToDevice, c->cur));
     if ((rc = vgpu_filter_pointcloud(c, (const float*)d, n, min_dist, max_range, origin, ws_min, ws_max, cull,
                                      (uint32_t*)(d + pb), count)))
@@ -2080,7 +2086,7 @@ try {
     const size_t cb = al(n * 12), rb = al(n * 4);
     int rc = stage(c, cb + rb + n, &d);
     if (rc) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipMemcpyAsync(d, centers, n * 12, hipMemcpyHostToDevice, c->cur));
     HIPCHK(c, hipMemcpyAsync(d + cb, radii, n * 4, hipMemcpyHostToDevice, c->cur));
     if ((rc = vgpu_pointcloud_collides(c, e, index, (const float*)d, (const float*)(d + cb), n, simd,
@@ -2209,7 +2215,7 @@ try {
     if (kmax == 0 || kmax > 64) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap kNN: 1 <= kmax <= 64");
     if (n >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many vertices");
     if (n && (!V || !k || !r || !nbr || !dist || !cnt)) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     if (q_count == 0) return VGPU_OK;
     int rc;
     const bool index = c->knn_mode == 2 || (c->knn_mode == 0 && n >= kKnnIndexMin);
@@ -2247,7 +2253,7 @@ try {
     if (!c) return VGPU_ERR_INVALID_ARG;
     if (q_count && (!V || !nbr || !cnt || !off || !starts || !goals))
         return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, vgpu_launch_edge_gather(V, (uint32_t)q_first, (uint32_t)q_count, dim, nbr, kmax, cnt, off, starts, goals,
                                       c->cur));
     return VGPU_OK;
@@ -2321,7 +2327,7 @@ try {
     if (2 * m >= ((size_t)1 << 31)) return fail(c, VGPU_ERR_INVALID_ARG, "too many pairs (2m must be < 2^31)");
     if (!offsets || (m && (!pairs || !adj))) return fail(c, VGPU_ERR_INVALID_ARG, "null buffers");
     if (m && n == 0) return fail(c, VGPU_ERR_INVALID_ARG, "pair index out of range");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     const size_t bytes = vgpu_roadmap_assemble_bytes((uint32_t)n, m);
     if (!bytes) return fail(c, VGPU_ERR_HIP, "roadmap assembly: scratch size query failed");
     int rc;
@@ -2362,7 +2368,7 @@ try {
     for (uint32_t v : k) kmax = std::max(kmax, v);
     kmax = std::min<uint32_t>(kmax, (uint32_t)n);
     if (kmax > 64) return fail(c, VGPU_ERR_UNSUPPORTED, "roadmap kNN: more than 64 neighbours per query");
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     DevBufs db;
     float *dV, *dr, *dd;
     uint32_t *dk, *dn, *dc, *doff;
@@ -2430,7 +2436,7 @@ try {
     const size_t pb = al(n * 12), kb = al(n), ib = al(n * 4);
     int rc = stage(c, 2 * pb + kb + ib, &d);
     if (rc) return rc;
-    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, ctx_device(c));
     HIPCHK(c, hipMemcpyAsync(d, pc, n * 12, hipMemcpyHostToDevice, c->cur));
     uint8_t* keep = (uint8_t*)(d + pb);
     if ((rc = vgpu_filter_robot_pointcloud(c, r, e, configuration, (const float*)d, n, point_radius, keep))) return rc;

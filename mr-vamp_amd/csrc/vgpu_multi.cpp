@@ -496,6 +496,7 @@ try {
         StdoutToStderr quiet;
         ir = R.init(&comm, world, u, rank);
     }
+    (void)hipGetLastError();  // RCCL's device probing may leave a handled error as this thread's last one
     if (ir != ncclSuccess) {  // no communicator to exchange over: RCCL reports its own failure per rank
         vgpu_comm_destroy(c);
         return VGPU_ERR_HIP;

@@ -407,7 +407,8 @@ class Comm:
 
 class Loopback:
     """An in-process loopback hub (vgpu_loopback_create): ``world`` ranks as threads of this process, each
-    with its own context and ``Comm(ctx, rank, world, hub=self)``; the C stages' all-gathers become device
+    with its own context and ``Comm(ctx, rank, world, hub=self)`` -- created from one thread per rank, as creation
+    is collective (it ends in a status all-gather, like vgpu_comm_init); the C stages' all-gathers become device
     copies between the ranks' buffers.  Close every Comm on it before closing the hub."""
 
     def __init__(self, world: int):

@@ -281,7 +281,8 @@ def loopback_ranks(monkeypatch):
     def make(world):
         ctxs = [vamp.Context(0) for _ in range(world)]
         hub = roadmap.Loopback(world)
-        comms = [roadmap.Comm(ctxs[r], r, world, hub=hub) for r in range(world)]
+        # creation is collective (it ends in a status all-gather): one thread per rank, like vgpu_comm_init
+        comms = _run_ranks(world, lambda r: roadmap.Comm(ctxs[r], r, world, hub=hub))
         made.append((ctxs, hub, comms))
         return ctxs, comms
 

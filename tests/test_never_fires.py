@@ -85,3 +85,16 @@ def test_generated_guards_match_the_model():
     # one guarded line per check (the 8-lane groups' per-lane form: tools/gen_kernels.py LANE_BITS)
     guarded = sorted(int(x) for x in re.findall(r"<< (\d+);(?: \})?  // proven silent inside", inc))
     assert guarded == [c for c, _ in never(m)]
+
+
+def test_lever_counts_later_prismatic_travel():
+    """a revolute joint's lever includes the travel of every prismatic joint after it in the chain (a
+    point pushed out along a slide moves farther per radian); a prismatic joint itself moves the point 1:1"""
+    import prove_self_checks as P
+    frames = [{"dof": 0, "jtype": "revolute", "t": [0.0, 0.0, 0.0], "axis": [0, 0, 1]},
+              {"dof": 1, "jtype": "prismatic", "t": [0.5, 0.0, 0.0], "axis": [1, 0, 0]},
+              {"dof": -1, "t": [0.0, 0.2, 0.0]}]
+    reach = np.array([3.0, 0.4])
+    lev = P.levers(frames, [0, 1, 2], [0.0, 0.0, 0.1], reach)
+    assert lev[1] == 1.0
+    assert abs(lev[0] - (0.5 + 0.2 + 0.1 + 0.4)) < 1e-12

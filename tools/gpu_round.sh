@@ -2,8 +2,8 @@
 # GPU-box passes (run through gpurun from the repo root).  One script, several modes; every GPU step runs under its
 # own timeout and the script stops at the first failure (no retries).
 #
-#   bash tools/gpu_round.sh suite TAG [SPEC]         the -m gpu suite (SPEC: a library variant, below)
-#                                                   -> gpurun_out/TAG_gputest[_SPEC].log
+#   bash tools/gpu_round.sh suite TAG [SPEC [FILE ...]]  the -m gpu suite, or the given test files (SPEC: a library
+#                                                   variant, below) -> gpurun_out/TAG_gputest[_SPEC].log
 #   bash tools/gpu_round.sh smoke TAG                __graft_entry__.smoke() -> gpurun_out/TAG_smoke.log
 #   bash tools/gpu_round.sh bench TAG W [W ...]      bench lines with CPU baselines -> gpurun_out/TAG_bench_W.json
 #   bash tools/gpu_round.sh prof W [W ...]           step profiles (tools/prof_step.sh -> gpurun_out/prof/W.json)
@@ -41,14 +41,16 @@ bench_args() {  # workload -> bench.py arguments
 summary() {  # bench line -> one summary line on stdout
   python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d.get('roofline') or {}; print(sys.argv[2], '%.4g' % d['value'], d['unit'], 'ms %.4f' % d['ms_per_step'], 'frac', r.get('frac'), 'ref_work_frac', r.get('reference_work_frac'), 'parity', json.dumps(d.get('parity'))[:200])" "$1" "$2"
 }
-suite() {  # TAG [SPEC]
-  local out=gpurun_out/$1_gputest${2:+_${2%%:*}}.log
-  env $(spec_env ${2:-rel}) timeout -k 10 700 python -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $out 2>&1 || { tail -30 $out; exit 1; }
-  echo "suite ${2:-rel}: $(tail -n 1 $out)"
+suite() {  # TAG [SPEC [FILE ...]]
+  local out=gpurun_out/$1_gputest${2:+_${2%%:*}}.log spec=${2:-rel}
+  shift; [ $# -gt 0 ] && shift
+  local files=${*:-tests}
+  env $(spec_env $spec) timeout -k 10 700 python -u -m pytest $files -m gpu -x -v --timeout 200 --timeout-method thread > $out 2>&1 || { echo "suite $spec failed: $out"; tail -30 $out; exit 1; }
+  echo "suite $spec: $(tail -n 1 $out)"
 }
 
 case $MODE in
-suite) suite "$1" "$2" ;;
+suite) suite "$@" ;;
 smoke)
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/$1_smoke.log 2>&1 || { tail -20 gpurun_out/$1_smoke.log; exit 1; }
   tail -n 1 gpurun_out/$1_smoke.log ;;

@@ -109,8 +109,11 @@ def chain_fk(frames, chain, q):
     return out
 
 
-def levers(frames, chain, offset):
-    """{dof: movement bound per unit of that joint} for a point at `offset` in the last frame of chain"""
+def levers(frames, chain, offset, reach):
+    """{dof: movement bound per unit of that joint} for a point at `offset` in the last frame of chain.  A revolute
+    joint's lever is the point's largest distance from its axis: the fixed translations of the later frames, the
+    offset, and the travel of every LATER prismatic joint (reach[dof] = max |q| over the widened limits) -- without
+    that travel the bound is unsound for a chain with a prismatic joint after a revolute one"""
     lev = {}
     for i, f in enumerate(chain):
         fr = frames[f]
@@ -119,7 +122,10 @@ def levers(frames, chain, offset):
         if fr.get("jtype") == "prismatic":
             lev[fr["dof"]] = 1.0
         else:
-            lev[fr["dof"]] = sum(np.linalg.norm(frames[g]["t"]) for g in chain[i + 1:]) + np.linalg.norm(offset)
+            travel = sum(reach[frames[g]["dof"]] for g in chain[i + 1:]
+                         if frames[g]["dof"] >= 0 and frames[g].get("jtype") == "prismatic")
+            lev[fr["dof"]] = sum(np.linalg.norm(frames[g]["t"]) for g in chain[i + 1:]) + np.linalg.norm(offset) + \
+                travel
     return lev
 
 
@@ -145,8 +151,9 @@ def prove(m, ck, margin_q=MARGIN_Q, max_iter=60, verbose=False):
     # per pair and dof: the joint's movement bound for the two spheres
     L = np.zeros((len(pairs), len(dofs)))
     for k, (a, b) in enumerate(pairs):
-        la = levers(frames, pa, spheres[a]["offset"])
-        lb = levers(frames, pb, spheres[b]["offset"])
+        reach = np.maximum(np.abs(lo0), np.abs(hi0))
+        la = levers(frames, pa, spheres[a]["offset"], reach)
+        lb = levers(frames, pb, spheres[b]["offset"], reach)
         for di, d in enumerate(dofs):
             L[k, di] = la.get(d, 0.0) + lb.get(d, 0.0)
     lo = lo0[dofs][None, :].copy()
