@@ -474,9 +474,9 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
     wall = timed_steps(a, torch, dist, dev, world, step, ev)
     step_ev_ms = ev[0]
     wall_max, units_all = reduce_over_ranks(dist, torch, wall, float(n) / world, dev, world)
-    # PCIe-inclusive rate (reported beside value): a few more steps, each ending in the host copy; the parity
-    # checks below read the host Roadmap of the last of them
-    pa = argparse.Namespace(**{**vars(a), "warmup": 0, "steps": min(a.steps, 3)})
+    # PCIe-inclusive rate (reported beside value): the same warm-up and step count as value, each step ending in the
+    # host copy; the parity checks below read the host Roadmap of the last of them
+    pa = argparse.Namespace(**{**vars(a)})
     wall_pcie = timed_steps(pa, torch, dist, dev, world, step_d2h)
     wall_pcie_max, _ = reduce_over_ranks(dist, torch, wall_pcie, float(n) / world, dev, world)
     pcie_ms = wall_pcie_max / pa.steps * 1e3
@@ -633,6 +633,10 @@ def run_prm_edges(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         parity = graph_parity(n, m, qi[ok_c], qj[ok_c], off_h.numpy(), adj_h[:info["n_adj"]].numpy(),
                               comp_h[:n].numpy(), roadmap)
         cpu = {"value": m / dt, "unit": "vertices/s", "cores": threads, "kind": "port",
+               "measurement_boundary": "the CPU path returns a host Roadmap; compare it with "
+                                       "phases.pcie_inclusive_vertices_per_s (the GPU step ending in the Roadmap's copy "
+                                       "to pinned host memory, same warm-up and steps as value) -- `value` leaves the "
+                                       "Roadmap in HBM (inputs and outputs resident, the bench contract)",
                "sample": f"the first {m} vertices of the same sequence: exact k-d tree neighbour queries "
                          f"(vgpu_cpu_roadmap_knn, {t_nn:.2f} s) + validate_motion of the {len(qi)} candidates on the "
                          f"AVX2 rake (mr-vamp_amd/csrc/cpu), {threads} threads, {dt:.1f} s in all; the host graph "
