@@ -1043,25 +1043,27 @@ def run_rrtc(a, torch, dist, rank, world, dev, stream, ctx, vamp):
         if m.any():
             gpu_ok[m] = robot0.validate_batch(seg_s[m], seg_g[m], envs[i], ctx)[0]
             cpu_ok[m] = robot0.cpu_validate_batch(seg_s[m], seg_g[m], envs[i], threads=1)[0]
-    # the roofline: the GPU leg's batch (all segments of the composite; problem 1's for the Panda, one scene per
-    # problem) resident in HBM, HIP events on the launch stream
-    m0 = groups[0]
+    # the roofline: the GPU leg's batch (all segments of the composite; for the Panda, one scene per problem, the
+    # problem with the most segments) resident in HBM, HIP events on the launch stream
+    k0 = 0 if pair else int(np.argmax([m.sum() for m in groups]))
+    m0 = groups[k0]
     ds, dg = torch.from_numpy(seg_s[m0]).to(dev), torch.from_numpy(seg_g[m0]).to(dev)
     E = int(m0.sum())
     okd = torch.empty(E, dtype=torch.uint8, device=dev)
     nbd = torch.empty(E, dtype=torch.int32, device=dev)
     for _ in range(3):
-        robot0.validate_device(ds.data_ptr(), dg.data_ptr(), E, envs[0], okd.data_ptr(), nbd.data_ptr(), ctx)
+        robot0.validate_device(ds.data_ptr(), dg.data_ptr(), E, envs[k0], okd.data_ptr(), nbd.data_ptr(), ctx)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record(stream)
     for _ in range(20):
-        robot0.validate_device(ds.data_ptr(), dg.data_ptr(), E, envs[0], okd.data_ptr(), nbd.data_ptr(), ctx)
+        robot0.validate_device(ds.data_ptr(), dg.data_ptr(), E, envs[k0], okd.data_ptr(), nbd.data_ptr(), ctx)
     e1.record(stream)
     torch.cuda.synchronize(dev)
     seg_ms = e0.elapsed_time(e1) / 20
     prof_w = "rrtc_pair" if pair else "rrtc"
     roof = {"kernel": "vgpu_validate_motions of the solved paths' segments (the line's GPU leg), "
-                      + ("all 16 problems' segments, one batch" if pair else "problem 1's segments"),
+                      + ("all 16 problems' segments, one batch" if pair else
+                         f"problem {k0 + 1}'s segments (the most of the 16; one scene per problem)"),
             "bound": "latency (a few hundred edges: far below one wave per CU)", "peak": FP32_PEAK_TFLOPS,
             "unit": "TFLOP/s", **utilisation(prof_w, E, seg_ms), **traffic_fields(prof_w, E), "kernel_ms": seg_ms,
             "segments": E, "algorithmic_bytes_per_segment": 2 * robot0.dimension() * 4 + 1 + 4}

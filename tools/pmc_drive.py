@@ -43,9 +43,10 @@ def setup(torch, vamp, w, dev, ctx, prep, inp, a):
         if prep:
             return None
         envs, S, G, robot, _ = bench.rrtc_problems(vamp, "panda_pair" if w == "rrtc_pair" else "panda")
-        if w == "rrtc":  # one scene per problem: the first problem's segments (the bench line's largest batch)
-            envs, S, G = envs[:1], S[:1], G[:1]
         res = [robot.rrtc(S[k], G[k], envs[k], bench.RRTC_SETTINGS(vamp), robot.halton()) for k in range(len(S))]
+        if w == "rrtc":  # one scene per problem: the problem with the most segments (the bench line's batch)
+            k = int(np.argmax([len(r.path) for r in res]))
+            envs, res = envs[k:k + 1], res[k:k + 1]
         a_ = torch.from_numpy(np.concatenate([r.path[:-1] for r in res])).to(dev)
         b_ = torch.from_numpy(np.concatenate([r.path[1:] for r in res])).to(dev)
         E = a_.shape[0]
