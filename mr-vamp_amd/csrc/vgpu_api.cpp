@@ -71,7 +71,8 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
     int vgpu_##NAME##_staged_lead_check(void);                                                                       \
     hipError_t vgpu_##NAME##_staged_lead(int kind, const void* s0, const void* s1, const void* s2, const void* s3,   \
                                          uint64_t first, uint32_t n_groups, const EnvView* env, const float* bases,  \
-                                         uint8_t* valid, hipStream_t st);
+                                         uint8_t* valid, hipStream_t st);                                            \
+    int vgpu_##NAME##_staged_head_list(void);
 VGPU_STAGED_DECL(panda_p0)
 VGPU_STAGED_DECL(panda_p1)
 VGPU_STAGED_DECL(panda_p2)
@@ -259,6 +260,9 @@ struct vgpu_ctx {
     std::vector<uint64_t> rounds;  // check sets run in order (staged); empty = chosen per batch
     long one_round = -1;           // A/B: source kinds run as one round (VAMP_AMD_ONE_ROUND), -1 = the robot's
     long lead = -1;                // A/B: source kinds that run the lead pass (VAMP_AMD_LEAD), -1 = the robot's
+    bool head_list = true;         // A/B: validate heads after the lead pass over its compacted list (VAMP_AMD_HEAD_LIST)
+    uint32_t* st_list = nullptr;   // that list (edges still valid, ascending), its count word, the selection's temp
+    size_t st_list_cap = 0;
     uint32_t* st_mask = nullptr;
     size_t st_mask_cap = 0;
     uint32_t* st_q = nullptr;  // staged sampling without a caller buffer: the drawn configurations
@@ -360,6 +364,7 @@ try {
     if (const char* s = std::getenv("VAMP_AMD_STAGED_STATS")) c->stats = std::strcmp(s, "0") != 0;
     if (const char* s = std::getenv("VAMP_AMD_ONE_ROUND")) c->one_round = std::strtol(s, nullptr, 0);
     if (const char* s = std::getenv("VAMP_AMD_LEAD")) c->lead = std::strtol(s, nullptr, 0);
+    if (const char* s = std::getenv("VAMP_AMD_HEAD_LIST")) c->head_list = std::strcmp(s, "0") != 0;
     if (const char* s = std::getenv("VAMP_AMD_ROUNDS")) {  // A/B: comma-separated check bit masks
         for (const char* p = s; *p;) {
             char* end = nullptr;
@@ -429,6 +434,7 @@ extern "C" void vgpu_ctx_destroy(vgpu_ctx* c)
     if (c->st_q) (void)hipFree(c->st_q);
     if (c->st_cnt) (void)hipFree(c->st_cnt);
     if (c->st_items) (void)hipFree(c->st_items);
+    if (c->st_list) (void)hipFree(c->st_list);
     if (c->st_host) (void)hipHostFree(c->st_host);
     if (c->knn_part) (void)hipFree(c->knn_part);
     if (c->knn_idx) (void)hipFree(c->knn_idx);
@@ -1313,6 +1319,7 @@ struct StagedOps {
     // source kinds (bit k = kind k) that run the lead pass first: where its check invalidates most
     // groups, the chained bound stage skips them (the Panda's validate heads, A/B in DESIGN.md §5d)
     unsigned lead_kinds;
+    int (*head_list)(void);  // 1: after the lead pass, validate heads run over the compacted list of live edges
     // a robot compiled as several translation units by source kind (vgpu_fetch_staged.hip VGPU_FETCH_PART):
     // by_kind[k] = the part whose exports run kind k (NULL: this table runs every kind)
     const struct StagedOps* const* by_kind = nullptr;
@@ -1324,7 +1331,7 @@ struct StagedOps {
             vgpu_##NAME##_staged_class, vgpu_##NAME##_staged_plan_bytes, vgpu_##NAME##_staged_blocks,                \
             vgpu_##NAME##_staged_bound, vgpu_##NAME##_staged_count, vgpu_##NAME##_staged_plan,                       \
             vgpu_##NAME##_staged_queue, vgpu_##NAME##_staged_children, ONE_ROUND, vgpu_##NAME##_staged_lead_check,   \
-            vgpu_##NAME##_staged_lead, LEAD                                                                          \
+            vgpu_##NAME##_staged_lead, LEAD, vgpu_##NAME##_staged_head_list                                          \
     }
 static const StagedOps kPandaParts[4] = {VGPU_STAGED_OPS(panda_p0, (1u << 3) | (1u << 4), 1u << 2),
                                          VGPU_STAGED_OPS(panda_p1, (1u << 3) | (1u << 4), 1u << 2),
@@ -1427,6 +1434,17 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const voi
     if (use_lead) {
         HIPCHK(c, ops.lead(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, valid, c->cur));
         chain = 1;
+        // validate heads: the rest of the pass runs over the edges the lead check left valid, compacted (a wave
+        // of the bound stage otherwise carries the groups it killed -- ~40 % of set B's heads -- as idle lanes)
+        if (kind == 2 && !s2 && c->head_list && ops.head_list()) {
+            const size_t sel = vgpu_compact_bytes(n);
+            const size_t list_words = (n + 63) & ~(size_t)63;
+            if ((rc = grow(c, &c->st_list, &c->st_list_cap, list_words + 64 + (sel + 3) / 4))) return rc;
+            uint32_t* const live = c->st_list + list_words;
+            HIPCHK(c, vgpu_launch_compact(valid, n, c->st_list, live, live + 64, sel, c->cur));
+            s2 = c->st_list;
+            s3 = live;
+        }
     }
     if (!masks_ready) HIPCHK(c, ops.bound(kind, s0, s1, s2, s3, first, (uint32_t)n, v, bases, chain, mask, valid, c->cur));
     uint64_t all = checks >= 64 ? ~0ull : ((1ull << checks) - 1ull);

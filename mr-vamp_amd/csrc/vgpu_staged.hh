@@ -151,6 +151,46 @@ struct SrcHeadT {  // validate head: block 0 of edge g
     __device__ __forceinline__ uint32_t out(uint32_t g) const { return g; }
 };
 
+// validate head over a compacted list: group g = block 0 of edge list[g], g < *n_live (the edges the lead pass
+// left valid, ascending -- vgpu_launch_compact).  The bound stage's grid covers every edge (the live count is
+// only on the device when it launches); groups past *n_live store an empty mask and leave.
+template <class R>
+struct SrcHeadListT {
+    static constexpr int G = 8;
+    static constexpr bool kInit = true;
+    const float* starts;
+    const float* goals;
+    const uint32_t* list;
+    const uint32_t* n_live;
+    __device__ __forceinline__ bool live(uint32_t g) const { return g < *n_live; }
+    __device__ __forceinline__ void load(uint32_t g, int lane, float v[R::D]) const
+    {
+        const uint32_t e = list[g];
+        R::head(starts + R::D * (size_t)e, goals + R::D * (size_t)e, lane, v);
+    }
+    __device__ __forceinline__ uint32_t out(uint32_t g) const { return list[g]; }
+};
+
+// R::kHeadList (optional): the robot's validate heads may run over the lead pass's compacted list
+template <class R, class = void>
+struct HeadList {
+    static constexpr bool v = false;
+};
+template <class R>
+struct HeadList<R, std::void_t<decltype(R::kHeadList)>> {
+    static constexpr bool v = R::kHeadList;
+};
+
+// groups a source leaves out (the compacted head list's tail past its device-side count)
+template <class Src, class = void>
+struct SrcLive {
+    __device__ static __forceinline__ bool of(const Src&, uint32_t) { return true; }
+};
+template <class Src>
+struct SrcLive<Src, std::void_t<decltype(&Src::live)>> {
+    __device__ static __forceinline__ bool of(const Src& s, uint32_t g) { return s.live(g); }
+};
+
 template <class R>
 struct SrcTailT {  // validate tail: item g = (edge, back-step k), result into the edge's flag
     static constexpr int G = 8;
@@ -288,6 +328,7 @@ template <class Src> struct SrcKindOf;
 template <class R> struct SrcKindOf<SrcConfigsT<R>> { static constexpr int v = 0; };
 template <class R> struct SrcKindOf<SrcSamplesT<R>> { static constexpr int v = 1; };
 template <class R> struct SrcKindOf<SrcHeadT<R>> { static constexpr int v = 2; };
+template <class R> struct SrcKindOf<SrcHeadListT<R>> { static constexpr int v = 2; };
 template <class R> struct SrcKindOf<SrcTailT<R>> { static constexpr int v = 3; };
 template <class R> struct SrcKindOf<SrcTailMaskT<R>> { static constexpr int v = 4; };
 
@@ -335,7 +376,7 @@ __global__ __launch_bounds__(kStagedBlock, (BoundWavesE<R, Src, EXT>::v)) void b
     if (g >= n_groups) return;  // group-uniform
     // a chained pass (a later pass over the same groups, e.g. the composite's arm B after arm A): a
     // group already invalid is done -- its mask stays 0 -- and the flag is not re-initialised
-    if (chain && !valid[src.out(g)]) {
+    if (!SrcLive<Src>::of(src, g) || (chain && !valid[src.out(g)])) {
         if (lane == 0) {
             mask[g] = 0;
             if constexpr (BothChunks<R>::v) mask[n_groups + g] = 0;
@@ -674,8 +715,16 @@ struct StagedHost {
         case 1:
             if constexpr ((K & 2u) != 0) return fn(SrcSamplesT<R>{first, (float*)s0, nullptr});
             break;
-        case 2:
-            if constexpr ((K & 4u) != 0) return fn(SrcHeadT<R>{(const float*)s0, (const float*)s1});
+        case 2:  // s2, s3: the compacted list and its device-side count (HeadList robots), else NULL
+            if constexpr ((K & 4u) != 0) {
+                if constexpr (HeadList<R>::v) {
+                    if (s2)
+                        return fn(SrcHeadListT<R>{(const float*)s0, (const float*)s1, (const uint32_t*)s2,
+                                                  (const uint32_t*)s3});
+                }
+                if (s2) break;
+                return fn(SrcHeadT<R>{(const float*)s0, (const float*)s1});
+            }
             break;
         case 3:
             if constexpr ((K & 8u) != 0)
@@ -716,6 +765,7 @@ struct StagedHost {
         });                                                                                                          \
     }                                                                                                                \
     int vgpu_##NAME##_staged_lead_check(void) { return vgpu::LeadCheck<R>::v; }                                   \
+    int vgpu_##NAME##_staged_head_list(void) { return vgpu::HeadList<R>::v ? 1 : 0; }                             \
     hipError_t vgpu_##NAME##_staged_lead(int kind, const void* s0, const void* s1, const void* s2, const void* s3,   \
                                          uint64_t first, uint32_t n_groups, const EnvView* env, const float* bases,  \
                                          uint8_t* valid, hipStream_t st)                                             \

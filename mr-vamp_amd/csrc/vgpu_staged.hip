@@ -29,6 +29,9 @@
 #ifndef VGPU_PANDA_MID_KINDS
 #define VGPU_PANDA_MID_KINDS ((1u << 3) | (1u << 4))
 #endif
+#ifndef VGPU_PANDA_HEAD_LIST
+#define VGPU_PANDA_HEAD_LIST 1
+#endif
 #ifndef VGPU_PANDA_CLASS0_WAVES
 #define VGPU_PANDA_CLASS0_WAVES 8
 #endif
@@ -80,6 +83,8 @@ struct PandaR {
     }
     // the lead pass (vgpu_staged.hh lead_kernel): check 8, the link-5 environment check
     static constexpr int kLeadCheck = panda_lead_check;
+    // after the lead pass, the heads' bound / children stages run over the compacted list of live edges
+    static constexpr bool kHeadList = VGPU_PANDA_HEAD_LIST;
     template <class Grp>
     __device__ static __forceinline__ bool lead(const float* v, const EnvView& env, const Bases& b)
     {
