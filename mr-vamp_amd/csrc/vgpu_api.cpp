@@ -261,6 +261,7 @@ struct vgpu_ctx {
     long one_round = -1;           // A/B: source kinds run as one round (VAMP_AMD_ONE_ROUND), -1 = the robot's
     long lead = -1;                // A/B: source kinds that run the lead pass (VAMP_AMD_LEAD), -1 = the robot's
     bool head_list = true;         // A/B: validate heads after the lead pass over its compacted list (VAMP_AMD_HEAD_LIST)
+    bool no_near = false;          // A/B: children scan every culled record, no near sets (VAMP_AMD_NEAR=0)
     uint32_t* st_list = nullptr;   // that list (edges still valid, ascending), its count word, the selection's temp
     size_t st_list_cap = 0;
     uint32_t* st_mask = nullptr;
@@ -365,6 +366,7 @@ try {
     if (const char* s = std::getenv("VAMP_AMD_ONE_ROUND")) c->one_round = std::strtol(s, nullptr, 0);
     if (const char* s = std::getenv("VAMP_AMD_LEAD")) c->lead = std::strtol(s, nullptr, 0);
     if (const char* s = std::getenv("VAMP_AMD_HEAD_LIST")) c->head_list = std::strcmp(s, "0") != 0;
+    if (const char* s = std::getenv("VAMP_AMD_NEAR")) c->no_near = std::strcmp(s, "0") == 0;
     if (const char* s = std::getenv("VAMP_AMD_ROUNDS")) {  // A/B: comma-separated check bit masks
         for (const char* p = s; *p;) {
             char* end = nullptr;
@@ -1186,6 +1188,13 @@ static EnvView make_view(const vgpu_env* e)
     v.n_pc = (int)e->pointclouds.size();
     v.att = (const VGPU_CONST float*)(e->dev + L.att_off);
     v.n_att = e->attached ? (int)e->att_spheres.size() : 0;
+    // near sets (vgpu_device.hh env_near): every primitive record has a bit
+    int total = 0;
+    for (int t = 0; t < OBS_TYPES; ++t) {
+        v.near_base[t] = total;
+        total += v.n[t];
+    }
+    v.near_ok = (total <= kNearMax && !e->ctx->no_near) ? 1 : 0;
     return v;
 }
 
@@ -1455,11 +1464,15 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const voi
     HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
     HIPCHK(c, hipMemcpy2DAsync(c->st_host, sizeof(uint32_t), offs, nb * sizeof(uint32_t), sizeof(uint32_t), checks + 1,
                                hipMemcpyDeviceToHost, c->cur));
+    if (c->stats && kind == 2 && s3)  // the compacted head list's live count (statistics only)
+        HIPCHK(c, hipMemcpyAsync(c->st_host + 127, s3, sizeof(uint32_t), hipMemcpyDeviceToHost, c->cur));
     HIPCHK(c, hipStreamSynchronize(c->cur));
     uint32_t fired[64];
     for (int k = 0; k < checks; ++k) fired[k] = c->st_host[k + 1] - c->st_host[k];
     if (c->stats) {  // VAMP_AMD_STAGED_STATS=1: the pass's bounding statistics (development)
-        std::fprintf(stderr, "staged kind=%d chain=%d groups=%zu fired:", kind, chain, n);
+        std::fprintf(stderr, "staged kind=%d chain=%d groups=%zu", kind, chain, n);
+        if (kind == 2 && s3) std::fprintf(stderr, " live=%u", c->st_host[127]);
+        std::fprintf(stderr, " fired:");
         for (int k = 0; k < checks; ++k) std::fprintf(stderr, " %u", fired[k]);
         std::fprintf(stderr, "\n");
     }

@@ -241,7 +241,12 @@ struct EnvView {
     // levels of the first point cloud's split tree staged in this workgroup's LDS by
     // capt_stage_lds (0: none -- the host-built view, and kernels that do not stage)
     int pc_lds_levels;
+    // near sets (env_near / env_bits_near): nonzero when the primitive records number at most kNearMax; record i
+    // of type t is bit near_base[t] + i
+    int near_ok;
+    int near_base[OBS_TYPES];
 };
+constexpr int kNearMax = 64;
 constexpr int kAttHdr = 8;
 constexpr int kExtHdr = 32;
 // heightfield header: x y z xs ys zs xd yd xd2 yd2 (floats) | data_off cells (uint32 bits)
@@ -857,6 +862,186 @@ template <class Grp, bool EXT = false>
 __device__ __forceinline__ bool env_lane(const EnvView& env, float x, float y, float z, float r)
 {
     return (env_bits<Grp, EXT>(env, x, y, z, r) >> 31) != 0u;
+}
+
+// ---- near sets: the records a check's children can touch ----------------------------------------------
+// A check's children are tested only after its bounding test fires, and each of them runs the full culled
+// scan of every obstacle type above -- most of the validate step's time (the Panda's lead pass: 76 us for FK and
+// the bounding test, 480 us with the 12 children's scans).  A child the reference reports hitting record O lies
+// inside S, a sphere enclosing all of the check's children with a 0.1 mm margin (tools/gen_kernels.py NEAR), so
+// O's test fires for S as well: every test value here measures a distance (sphere, capsule, orthonormal cuboid --
+// the reference's closest-point forms), and the margin is ~300x the float error of the FK centres and of the
+// test values.  env_near scans S once and keeps, per lane, the records whose S test fires (bit near_base[t] + i
+// for record i of type t); env_bits_near then runs a child's scan over those records only, with the child's own
+// cull and test -- the same records fire as in env_bits, so the sign bit is the reference's.
+// S's cull is mid_env_bits' (it bounds from above the approximate extent the reference culls any child with),
+// made infinite when S reaches the origin (a child centred there has an infinite reference extent).  Cuboids
+// whose axes are not orthonormal (bounding sphere +inf, vgpu_api.cpp obstacle_bound) are always near: their test
+// value is no distance.  Only environments of at most kNearMax primitive records (EnvView::near_ok) and without
+// heightfields / point clouds use near sets; the others run env_bits.
+struct NearSet {
+    uint64_t lane, wave;  // this lane's records (wave: unused, 0)
+};
+
+// the reference's sphere-vs-primitive test values (sign bit = collision) on one record, as in env_bits
+struct ObsTests {
+    float x, y, z, r, rsq;
+    __device__ __forceinline__ float capsule(const VGPU_CONST float* o) const  // sphere_capsule.hh:9-22
+    {
+        const float dot = dot3(x - o[1], y - o[2], z - o[3], o[4], o[5], o[6]);
+        const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
+        const float px = __builtin_fmaf(o[4], cdf, o[1]);
+        const float py = __builtin_fmaf(o[5], cdf, o[2]);
+        const float pz = __builtin_fmaf(o[6], cdf, o[3]);
+        const float xs = x - px, ys = y - py, zs = z - pz;
+        const float rs = r + o[7];
+        return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
+    }
+    __device__ __forceinline__ float zcapsule(const VGPU_CONST float* o) const  // sphere_capsule.hh:30-43
+    {
+        const float dot = (z - o[3]) * o[6];
+        const float cdf = fminf(fmaxf(dot * o[8], 0.0f), 1.0f);
+        const float pz = __builtin_fmaf(o[6], cdf, o[3]);
+        const float xs = x - o[1], ys = y - o[2], zs = z - pz;
+        const float rs = r + o[7];
+        return __builtin_fmaf(-rs, rs, dot3(xs, ys, zs, xs, ys, zs));
+    }
+    __device__ __forceinline__ float cuboid(const VGPU_CONST float* o) const  // sphere_cuboid.hh:9-27
+    {
+        const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
+        const float a1 = max0(__builtin_fabsf(dot3(o[4], o[5], o[6], xs, ys, zs)) - o[13]);
+        const float a2 = max0(__builtin_fabsf(dot3(o[7], o[8], o[9], xs, ys, zs)) - o[14]);
+        const float a3 = max0(__builtin_fabsf(dot3(o[10], o[11], o[12], xs, ys, zs)) - o[15]);
+        return dot3(a1, a2, a3, a1, a2, a3) - rsq;
+    }
+    __device__ __forceinline__ float zcuboid(const VGPU_CONST float* o) const  // sphere_cuboid.hh:35-52
+    {
+        const float xs = x - o[1], ys = y - o[2], zs = z - o[3];
+        const float a1 = max0(__builtin_fabsf(dot2(o[4], o[5], xs, ys)) - o[13]);
+        const float a2 = max0(__builtin_fabsf(dot2(o[7], o[8], xs, ys)) - o[14]);
+        const float a3 = max0(__builtin_fabsf(zs) - o[15]);
+        return dot3(a1, a2, a3, a1, a2, a3) - rsq;
+    }
+    __device__ __forceinline__ float sphere(const VGPU_CONST float* o) const  // o: md x y z r at stride 2
+    {
+        return sphere_sphere(o[2], o[4], o[6], o[8], x, y, z, r);  // sphere_sphere.hh:10-22, as scan_spheres
+    }
+};
+
+// record i of a type's section (spheres: two records per kSphereBlock-float block, fields interleaved)
+template <int TYPE>
+__device__ __forceinline__ const VGPU_CONST float* obs_record(const VGPU_CONST float* o, int i)
+{
+    if constexpr (TYPE == OBS_SPHERE) return o + kSphereBlock * (i >> 1) + (i & 1);
+    else return o + kObsStride[TYPE] * i;
+}
+
+template <int TYPE>
+__device__ __forceinline__ float obs_test(const ObsTests& t, const VGPU_CONST float* o)
+{
+    if constexpr (TYPE == OBS_SPHERE) return t.sphere(o);
+    else if constexpr (TYPE == OBS_CAPSULE) return t.capsule(o);
+    else if constexpr (TYPE == OBS_ZCAPSULE) return t.zcapsule(o);
+    else if constexpr (TYPE == OBS_CUBOID) return t.cuboid(o);
+    else return t.zcuboid(o);
+}
+
+// S's bits over one type: records in md order until no lane of the wave reaches one (the next md loaded a trip
+// ahead; the sections are sentinel-padded).  Spheres two records per trip, from their pair blocks (as scan_spheres).
+template <int TYPE>
+__device__ __forceinline__ uint64_t near_bits_type(const EnvView& env, const ObsTests& t, float emax, uint64_t lane)
+{
+    const VGPU_CONST float* o = env.obs[TYPE];
+    const int n = env.n[TYPE], base = env.near_base[TYPE];
+    if constexpr (TYPE == OBS_SPHERE) {
+        const VGPU_CONST SphereBlk* p = (const VGPU_CONST SphereBlk*)o;
+        f2v md = p->md;
+        for (int i = 0; i < n; i += 2, ++p) {
+            const bool la = md.x < emax, lb = md.y < emax;  // a pad record's md is +inf
+            if (__builtin_amdgcn_ballot_w64(la) == 0ull) break;  // sorted by md: nothing later is reached either
+            const f2v nmd = p[1].md;
+            const float va = sphere_sphere(p->x.x, p->y.x, p->z.x, p->r.x, t.x, t.y, t.z, t.r);
+            const float vb = sphere_sphere(p->x.y, p->y.y, p->z.y, p->r.y, t.x, t.y, t.z, t.r);
+            const uint64_t on = (la && !(va >= 0.0f) ? 1ull : 0ull) | (lb && !(vb >= 0.0f) ? 2ull : 0ull);  // NaN: near
+            lane |= on << (base + i);
+            md = nmd;
+        }
+    } else {
+        float md = obs_record<TYPE>(o, 0)[0];
+        for (int i = 0; i < n; ++i) {
+            const bool live = md < emax;
+            if (__builtin_amdgcn_ballot_w64(live) == 0ull) break;
+            const VGPU_CONST float* rec = obs_record<TYPE>(o, i);
+            md = obs_record<TYPE>(o, i + 1)[0];
+            const float v = obs_test<TYPE>(t, rec);
+            bool near = !(v >= 0.0f);
+            if constexpr (TYPE == OBS_CUBOID || TYPE == OBS_ZCUBOID) near = near || !(rec[kObsBound[TYPE] + 3] < __builtin_inff());
+            if (live && near) lane |= 1ull << (base + i);
+        }
+    }
+    return lane;
+}
+
+// S's near set; requires env.near_ok (the generated code branches on it: without near sets the children run
+// env_bits)
+template <class Grp>
+__device__ __forceinline__ NearSet env_near(const EnvView& env, float x, float y, float z, float r)
+{
+    const float d = dot3(x, y, z, x, y, z);
+    float me = (__builtin_sqrtf(d) + r) * 1.001f + 1e-5f;
+    if (me != me || !(d > r * r * 1.001f)) me = __builtin_inff();  // NaN, or S reaches the origin
+    const float emax = Grp::max(me);
+    const ObsTests t{x, y, z, r, r * r};
+    uint64_t b = 0ull;
+    if (env.n[OBS_SPHERE]) b = near_bits_type<OBS_SPHERE>(env, t, emax, b);
+    if (env.n[OBS_CAPSULE]) b = near_bits_type<OBS_CAPSULE>(env, t, emax, b);
+    if (env.n[OBS_ZCAPSULE]) b = near_bits_type<OBS_ZCAPSULE>(env, t, emax, b);
+    if (env.n[OBS_CUBOID]) b = near_bits_type<OBS_CUBOID>(env, t, emax, b);
+    if (env.n[OBS_ZCUBOID]) b = near_bits_type<OBS_ZCUBOID>(env, t, emax, b);
+    return NearSet{b, 0ull};
+}
+
+// a child's scan over one type's records in this lane's near set: each lane walks its OWN set (per-lane loads of
+// the records, L1-resident), so a wave needs as many trips as its fullest lane has records -- not the union over
+// the wave's 8 unrelated edges, which a scalar walk would take; the reference's cull (md < emax, the group's) and
+// test per record
+template <int TYPE>
+__device__ __forceinline__ uint32_t near_scan_type(const EnvView& env, const NearSet& ns, const ObsTests& t, float emax,
+                                                   uint32_t acc)
+{
+    const VGPU_CONST float* o = env.obs[TYPE];
+    const int n = env.n[TYPE], base = env.near_base[TYPE];
+    uint64_t m = ns.lane >> base;
+    if (n < 64) m &= (1ull << n) - 1ull;
+    if (acc >> 31) m = 0ull;  // this lane already hit
+    while (__builtin_amdgcn_ballot_w64(m != 0ull) != 0ull) {
+        if (m != 0ull) {
+            const int i = __builtin_ctzll(m);
+            m &= m - 1ull;
+            const VGPU_CONST float* rec = obs_record<TYPE>(o, i);
+            if (rec[0] < emax) acc |= __float_as_uint(obs_test<TYPE>(t, rec));
+        }
+    }
+    return acc;
+}
+
+// env_bits of a child of the check whose near set is ns (same sign bit); primitive environments with near sets
+template <class Grp>
+__device__ __forceinline__ uint32_t env_bits_near(const EnvView& env, const NearSet& ns, float x, float y, float z,
+                                                  float r, uint32_t acc)
+{
+    const float d = dot3(x, y, z, x, y, z);
+    float me = sqrt_host(d, env.lut, env.kbits) + r;  // validity.hh:55-59, as env_bits
+    const uint32_t dexp = __float_as_uint(d) & 0x7F800000u;
+    if (dexp == 0u || dexp == 0x7F800000u || me != me) me = __builtin_inff();
+    const float emax = Grp::max(me);
+    const ObsTests t{x, y, z, r, r * r};
+    if (env.n[OBS_SPHERE]) acc = near_scan_type<OBS_SPHERE>(env, ns, t, emax, acc);
+    if (env.n[OBS_CAPSULE]) acc = near_scan_type<OBS_CAPSULE>(env, ns, t, emax, acc);
+    if (env.n[OBS_ZCAPSULE]) acc = near_scan_type<OBS_ZCAPSULE>(env, ns, t, emax, acc);
+    if (env.n[OBS_CUBOID]) acc = near_scan_type<OBS_CUBOID>(env, ns, t, emax, acc);
+    if (env.n[OBS_ZCUBOID]) acc = near_scan_type<OBS_ZCUBOID>(env, ns, t, emax, acc);
+    return acc;
 }
 
 // Attachment::pose (collision/attachments.hh:75-122) at the end-effector pose p (position,

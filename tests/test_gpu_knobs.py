@@ -1,5 +1,5 @@
 """The staged pipeline's A/B knobs change only how the work is scheduled, never a result:
-the lead pass on / off / also for configurations, the heads' compacted list on / off, every source kind as one round or as rounds, explicit
+the lead pass on / off / also for configurations, the heads' compacted list on / off, the children's near sets on / off, every source kind as one round or as rounds, explicit
 rounds, and the monolithic kernels give the same validate (set A, set-B-like) and fkcc answers as the
 default schedule on the same seeded inputs.  Each setting runs in its own process (the knobs are read
 at context creation)."""
@@ -15,6 +15,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 SETTINGS = {
     "lead_off": {"VAMP_AMD_LEAD": "0"},
     "head_list_off": {"VAMP_AMD_HEAD_LIST": "0"},
+    "near_off": {"VAMP_AMD_NEAR": "0"},
     "lead_configs": {"VAMP_AMD_LEAD": "5"},
     "rounds_per_batch_everywhere": {"VAMP_AMD_ONE_ROUND": "0"},
     "one_round_everywhere": {"VAMP_AMD_ONE_ROUND": "0x1f"},
@@ -26,7 +27,7 @@ SETTINGS = {
 def run(tmp_path, name, extra):
     out = str(tmp_path / f"{name}.npz")
     env = dict(os.environ)
-    for k in ("VAMP_AMD_LEAD", "VAMP_AMD_HEAD_LIST", "VAMP_AMD_ONE_ROUND", "VAMP_AMD_ROUNDS", "VAMP_AMD_STAGED"):
+    for k in ("VAMP_AMD_LEAD", "VAMP_AMD_HEAD_LIST", "VAMP_AMD_NEAR", "VAMP_AMD_ONE_ROUND", "VAMP_AMD_ROUNDS", "VAMP_AMD_STAGED"):
         env.pop(k, None)
     env.update(extra)
     r = subprocess.run([sys.executable, os.path.join(HERE, "knob_probe.py"), out], env=env, capture_output=True,

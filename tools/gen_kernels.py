@@ -67,6 +67,13 @@ MID_SELF_CHECKS = [("panda_link1", "panda_link5"), ("panda_link2", "panda_link5"
                    ("forearm_roll_link", "torso_fixed_link"), ("elbow_flex_link", "torso_fixed_link"),
                    ("torso_lift_link", "elbow_flex_link")]
 MID_MARGIN = 1e-4
+# GPU lead pass (--no-near: off): the lead check's children after one sphere S enclosing every child with MID_MARGIN
+# is scanned against the environment (vgpu_device.hh env_near: per lane, the records S touches); each child then walks
+# only its lane's records (env_bits_near) -- a child can only hit a record its enclosing sphere touches, so the
+# results are the reference's.  Lead only: in the staged children kernels the near-set code pushed the class-0
+# kernel past its 64-VGPR budget (spills) and made them slower (A/B on MI355X).  Children spread
+# over several frames or base flags keep the full scans.
+NEAR = True
 
 # Emitted types.  The HIP kernels compute one configuration per lane in `float` with the
 # per-lane check bits in `uint32_t`; the CPU restatement (--cpu, mr-vamp_amd/csrc/cpu/) emits
@@ -415,7 +422,7 @@ class RobotGen:
         bi = links.index(e["bound"])
         return fr.bound_center(bi), m["bounding"][bi]["radius"]
 
-    def emit_children(self, E, fr, kind, ck, on_hit, early=False):
+    def emit_children(self, E, fr, kind, ck, on_hit, early=False, near_ok=False):
         """Children of a fired check; `on_hit` is the statement run when any lane's child fires.
         early: environment children leave as soon as one fires for the group (a group whose
         answer is known stops; the wave stops when all its groups have); "primitive": only in
@@ -424,14 +431,40 @@ class RobotGen:
         if kind == "env":
             E.raw(bdecl("h", "sign bit: this lane hit (a hit lane keeps no obstacle loop alive)"))
             kids = ck["children"]
-            for i, kid in enumerate(kids):
-                sp = spheres[kid["sphere"]]
-                cw = self.world(fr.center(sp["frame"], sp["offset"]), kid["base"])
-                E.raw(f"h = env_bits<Grp, EXT>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])}, h);")
-                if early == "primitive" and i + 1 < len(kids):  # staged: point-cloud queries may be deferred
-                    E.raw(f"if constexpr (!EXT) {{ if (Grp::any_bits(h)) {on_hit} }}")
-                elif early and i + 1 < len(kids):
-                    E.raw(f"if (Grp::any_bits(h)) {on_hit}")
+            frames = {spheres[k["sphere"]]["frame"] for k in kids}
+            bases = {k["base"] for k in kids}
+            near = near_ok and NEAR and not TY["cpu"] and len(frames) == 1 and len(bases) == 1 and len(kids) > 1
+
+            def kid_scans(use_near):
+                for i, kid in enumerate(kids):
+                    sp = spheres[kid["sphere"]]
+                    cw = self.world(fr.center(sp["frame"], sp["offset"]), kid["base"])
+                    if use_near:
+                        E.raw(f"h = env_bits_near<Grp>(env, ns, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])}, h);")
+                    else:
+                        E.raw(f"h = env_bits<Grp, EXT>(env, {cw[0]}, {cw[1]}, {cw[2]}, {flit(sp['radius'])}, h);")
+                    if early == "primitive" and i + 1 < len(kids):  # staged: point-cloud queries may be deferred
+                        E.raw(f"if constexpr (!EXT) {{ if (Grp::any_bits(h)) {on_hit} }}")
+                    elif early and i + 1 < len(kids):
+                        E.raw(f"if (Grp::any_bits(h)) {on_hit}")
+
+            if near:  # S: one sphere enclosing every child (env_near / env_bits_near); centres per branch
+                (off, R), = mid_spheres([spheres[k["sphere"]]["offset"] for k in kids],
+                                        [spheres[k["sphere"]]["radius"] for k in kids], 1)
+                E.raw("if (!EXT && env.near_ok) {  // primitive records only, at most kNearMax")
+                E.indent += 1
+                w = self.world(fr.center(next(iter(frames)), off), next(iter(bases)))
+                E.raw(f"const NearSet ns = env_near<Grp>(env, {w[0]}, {w[1]}, {w[2]}, {flit(R)});  "
+                      f"// the records the {len(kids)} children can touch")
+                kid_scans(True)
+                E.indent -= 1
+                E.raw("} else {")
+                E.indent += 1
+                kid_scans(False)
+                E.indent -= 1
+                E.raw("}")
+            else:
+                kid_scans(False)
             E.raw(f"if (Grp::any_bits(h)) {on_hit}")
             return
         pairs = ck["children"]
@@ -792,7 +825,7 @@ class RobotGen:
             else:
                 E.raw(f"if (Grp::any({test})) {{")
             E.indent += 1
-            self.emit_children(E, fr, kind, ck, "return false;", early)
+            self.emit_children(E, fr, kind, ck, "return false;", early, near_ok=(fname == "lead"))
             E.indent -= 1
             E.raw("}")
         E.raw("return true;")
@@ -1097,7 +1130,7 @@ def gen_radii(paths) -> str:
 
 
 def main():
-    global REMAT, TY, HOLD, GATE, MIDS, LANE_BITS
+    global REMAT, TY, HOLD, GATE, MIDS, LANE_BITS, NEAR
     if "--radii" in sys.argv:  # tools/gen_kernels.py --radii OUT model/a.json model/b.json ...
         args = [a for a in sys.argv[1:] if a != "--radii"]
         open(args[0], "w").write(gen_radii(args[1:]))
@@ -1120,6 +1153,9 @@ def main():
     if "--mids" in sys.argv:
         MIDS = True
         sys.argv.remove("--mids")
+    if "--no-near" in sys.argv:
+        NEAR = False
+        sys.argv.remove("--no-near")
     argv = [a for a in sys.argv if not a.startswith("--")]
     sys.argv[1:3] = argv[1:3]
     model = json.load(open(sys.argv[1]))
