@@ -1025,6 +1025,21 @@ __device__ __forceinline__ uint32_t near_scan_type(const EnvView& env, const Nea
     return acc;
 }
 
+// a bounding test inside a near-set cluster (tools/gen_kernels.py --cluster): the walk over the cluster sphere's near
+// records, or env_bits without near sets / with heightfields or point clouds
+template <class Grp>
+__device__ __forceinline__ uint32_t env_bits_near(const EnvView& env, const NearSet& ns, float x, float y, float z,
+                                                  float r, uint32_t acc);
+template <class Grp, bool EXT>
+__device__ __forceinline__ uint32_t env_bits_e(const EnvView& env, const NearSet& ns, float x, float y, float z, float r,
+                                               uint32_t acc = 0u, int tag = kTagDefault)
+{
+    if constexpr (!EXT) {
+        if (env.near_ok) return env_bits_near<Grp>(env, ns, x, y, z, r, acc);
+    }
+    return env_bits<Grp, EXT>(env, x, y, z, r, acc, tag);
+}
+
 // env_bits of a child of the check whose near set is ns (same sign bit); primitive environments with near sets
 template <class Grp>
 __device__ __forceinline__ uint32_t env_bits_near(const EnvView& env, const NearSet& ns, float x, float y, float z,

@@ -74,6 +74,12 @@ MID_MARGIN = 1e-4
 # kernel past its 64-VGPR budget (spills) and made them slower (A/B on MI355X).  Children spread
 # over several frames or base flags keep the full scans.
 NEAR = True
+# GPU staged bound stage (--cluster): the bounding tests of these links share one near set -- a sphere E enclosing
+# their bounding spheres, built per configuration from the centres the tests use (so it encloses them whatever the
+# base-offset quirks), scanned once (env_near), then each member's test walks only its lane's records E touches
+# (env_bits_e: env_bits_near, or env_bits without near sets / with point clouds).
+CLUSTER = {}
+CLUSTER_LINKS = {"panda": ["panda_link6", "panda_link7", "panda_hand", "panda_leftfinger", "panda_rightfinger"]}
 
 # Emitted types.  The HIP kernels compute one configuration per lane in `float` with the
 # per-lane check bits in `uint32_t`; the CPU restatement (--cpu, mr-vamp_amd/csrc/cpu/) emits
@@ -407,6 +413,8 @@ class RobotGen:
             b = links.index(ck["link"])
             bd = m["bounding"][b]
             w = self.world(fr.bound_center(b), bd["base"])
+            if ck["link"] in getattr(self, "cluster_on", ()):
+                return "env", f"env_bits_e<Grp, EXT>(env, nsE, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])})", ck
             return "env", f"env_bits<Grp, EXT>(env, {w[0]}, {w[1]}, {w[2]}, {flit(bd['radius'])})", ck
         ck = m["self_checks"][o["index"]]
         (ca, ra), (cb, rb) = self.self_ent(fr, ck["a"]), self.self_ent(fr, ck["b"])
@@ -909,7 +917,20 @@ class RobotGen:
             d0, d1 = gate["dofs"]
             E.raw(f"const uint32_t gate = Grp::or_bits({self.name}_gate(q{d0}, q{d1}));  // per group: checks that can fire")
             gated = {c: b for b, c in enumerate(gate["checks"])}
+        members = CLUSTER.get(self.name, [])
+        first = min([c for c, o in enumerate(order) if o["kind"] == "env" and
+                     m["env_checks"][o["index"]]["link"] in members], default=-1)
+        in_cluster = {c for c, o in enumerate(order) if o["kind"] == "env" and
+                      m["env_checks"][o["index"]]["link"] in members}
         for c, o in enumerate(order):
+            if c == first:  # E, then every member's bounding test at once (short live ranges of E and the centres)
+                self.emit_cluster(E, fr, members)
+                self.cluster_on = set(members)
+                for cm in sorted(in_cluster):
+                    self.emit_bound_check(E, fr, cm, order[cm], gated, one, mids_on=bool(MIDS), mt=mt)
+                self.cluster_on = set()
+            if c in in_cluster:
+                continue
             self.emit_bound_check(E, fr, c, o, gated, one, mids_on=bool(MIDS), mt=mt)
         if LANE_BITS:
             E.raw(f"return mask | {self.group_or(mt, 'lm')};")
@@ -935,6 +956,29 @@ class RobotGen:
                                   early=True)]
 
         return "\n".join(out)
+
+    def emit_cluster(self, E, fr, members):
+        """E: centred on the members' mean bounding centre, radius = the largest centre distance + radius, widened
+        for float rounding (and infinite for a NaN centre); its near set nsE (primitive environments with near sets)"""
+        m = self.m
+        links = [b["link"] for b in m["bounding"]]
+        cs = []
+        for link in members:
+            b = links.index(link)
+            bd = m["bounding"][b]
+            cs.append((self.world(fr.bound_center(b), bd["base"]), bd["radius"]))
+        k = len(cs)
+        E.raw(f"// cluster {', '.join(members)}: one near set for their bounding tests")
+        for a in range(3):
+            E.raw(f"const float e{'xyz'[a]} = (" + " + ".join(c[a] for c, _ in cs) + f") * {flit(1.0 / k)};")
+        E.raw("float eR = 0.0f, enan = 0.0f;")
+        for c, r in cs:
+            E.raw(f"{{ const float dx = {c[0]} - ex, dy = {c[1]} - ey, dz = {c[2]} - ez; "
+                  f"const float dd = __builtin_sqrtf(dx * dx + dy * dy + dz * dz) + {flit(r)}; "
+                  "eR = dd > eR ? dd : eR; enan += dd; }")
+        E.raw("eR = (eR + 2e-5f) * 1.00001f;")
+        E.raw("if (enan != enan || !(eR < __builtin_inff())) eR = __builtin_inff();")
+        E.raw("const NearSet nsE = (!EXT && env.near_ok) ? env_near<Grp>(env, ex, ey, ez, eR) : NearSet{0ull, 0ull};")
 
     @staticmethod
     def group_or(mt, v):
@@ -1130,7 +1174,7 @@ def gen_radii(paths) -> str:
 
 
 def main():
-    global REMAT, TY, HOLD, GATE, MIDS, LANE_BITS, NEAR
+    global REMAT, TY, HOLD, GATE, MIDS, LANE_BITS, NEAR, CLUSTER
     if "--radii" in sys.argv:  # tools/gen_kernels.py --radii OUT model/a.json model/b.json ...
         args = [a for a in sys.argv[1:] if a != "--radii"]
         open(args[0], "w").write(gen_radii(args[1:]))
@@ -1153,6 +1197,9 @@ def main():
     if "--mids" in sys.argv:
         MIDS = True
         sys.argv.remove("--mids")
+    if "--cluster" in sys.argv:
+        CLUSTER = CLUSTER_LINKS
+        sys.argv.remove("--cluster")
     if "--no-near" in sys.argv:
         NEAR = False
         sys.argv.remove("--no-near")
