@@ -85,10 +85,10 @@ struct PairArmR : PairRakeR {
     using Mask = panda_mask_t;
     static constexpr Mask kEnvChecks = panda_env_check_bits;
     // the Panda's children register classes (vgpu_staged.hip PandaR)
-    static constexpr int kClasses = 3;
-    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 0, 0, 2,
-                                              0, 0, 0, 1, 1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-    static constexpr int kClassWaves[kClasses] = {8, 7, 6};
+    static constexpr int kClasses = 4;
+    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 1, 1, 3, 0, 0, 0, 0, 0, 0, 2,
+                                              0, 3, 0, 1, 1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    static constexpr int kClassWaves[kClasses] = {8, 7, 6, 6};
     // validate tails run the Panda's mid-sphere tests in their bound stage, as the single Panda does
     // (vgpu_staged.hip PandaR::kMidKinds)
     static constexpr uint32_t kMidKinds = VGPU_PAIR_MID_KINDS;

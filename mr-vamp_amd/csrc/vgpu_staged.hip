@@ -1,6 +1,10 @@
 // vgpu_staged.hip -- the staged collision hierarchy (vgpu_staged.hh) instantiated for the Panda
 // (robots/panda_base.hh: 7 dof, 32 checks of panda/fk.hh:1335-6276, 32-bit check masks), plus
 // the validate head -> tail back-step counts.
+// part 0 (configurations, samples): no near-set children (their class-3 kernel as before round 6)
+#if !defined(VGPU_PANDA_PART) || VGPU_PANDA_PART == 0
+#define VGPU_NEAR_CHILDREN 0
+#endif
 #include "vgpu_panda.hh"
 #include "vgpu_staged.hh"
 
@@ -38,6 +42,9 @@
 #ifndef VGPU_PANDA_CLASS1_WAVES
 #define VGPU_PANDA_CLASS1_WAVES 7
 #endif
+#ifndef VGPU_PANDA_CLASS3_WAVES
+#define VGPU_PANDA_CLASS3_WAVES 6
+#endif
 #ifndef VGPU_PANDA_CLASS2_WAVES
 #define VGPU_PANDA_CLASS2_WAVES 6
 #endif
@@ -58,11 +65,16 @@ struct PandaR {
     static constexpr unsigned kSourceKinds = VGPU_PANDA_PART == 0 ? 0x3u : (0x4u << (VGPU_PANDA_PART - 1));
     // children register classes (ChildClasses): VGPRs per check when compiled alone (Grp8, gfx950):
     // most <= 49; 6, 7, 19, 20: 59-65; 15, 21: 90, 105
-    static constexpr int kClasses = 3;
-    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 1, 1, 0, 0, 0, 0, 0, 0, 0, 2,
-                                              0, 0, 0, 1, 1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    // class 3 (round 6): the environment checks with near-set children (link 5: 12 children, hand: 18;
+    // tools/gen_kernels.py NEAR_CHILDREN) -- their near code in the class-0 kernel spilled it at 8 waves/EU.  The
+    // table is the same in every part: PandaR's members and R-only kernels (plan_kernel<PandaR>) are shared symbols
+    // across the part TUs, so a per-part table broke the plan of the other parts (a 3-class part-0 table made the
+    // heads miss collisions in tests/test_gpu_near.py)
+    static constexpr int kClasses = 4;
+    static constexpr int kClassOf[kChecks] = {0, 0, 0, 0, 0, 0, 1, 1, 3, 0, 0, 0, 0, 0, 0, 2,
+                                              0, 3, 0, 1, 1, 2, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     static constexpr int kClassWaves[kClasses] = {VGPU_PANDA_CLASS0_WAVES, VGPU_PANDA_CLASS1_WAVES,
-                                                  VGPU_PANDA_CLASS2_WAVES};
+                                                  VGPU_PANDA_CLASS2_WAVES, VGPU_PANDA_CLASS3_WAVES};
     __device__ static __forceinline__ void sample(uint64_t k, float v[7]) { panda_sample(k, v); }
     __device__ static __forceinline__ void head(const float* s, const float* g, int lane, float v[7])
     {

@@ -74,6 +74,10 @@ MID_MARGIN = 1e-4
 # kernel past its 64-VGPR budget (spills) and made them slower (A/B on MI355X).  Children spread
 # over several frames or base flags keep the full scans.
 NEAR = True
+# GPU staged children with near sets too: {robot: least number of children} -- the checks with that many children
+# (the Panda's link 5: 12, hand: 18), which the robot's kernels run in a children class of their own (vgpu_staged.hip
+# PandaR::kClassOf): in the shared class-0 kernel the near code of every check spilled (see NEAR)
+NEAR_CHILDREN = {"panda": 8}
 # GPU staged bound stage (--cluster): the bounding tests of these links share one near set -- a sphere E enclosing
 # their bounding spheres, built per configuration from the centres the tests use (so it encloses them whatever the
 # base-offset quirks), scanned once (env_near), then each member's test walks only its lane's records E touches
@@ -430,7 +434,7 @@ class RobotGen:
         bi = links.index(e["bound"])
         return fr.bound_center(bi), m["bounding"][bi]["radius"]
 
-    def emit_children(self, E, fr, kind, ck, on_hit, early=False, near_ok=False):
+    def emit_children(self, E, fr, kind, ck, on_hit, early=False, near_ok=False, near_gate="true"):
         """Children of a fired check; `on_hit` is the statement run when any lane's child fires.
         early: environment children leave as soon as one fires for the group (a group whose
         answer is known stops; the wave stops when all its groups have); "primitive": only in
@@ -459,7 +463,7 @@ class RobotGen:
             if near:  # S: one sphere enclosing every child (env_near / env_bits_near); centres per branch
                 (off, R), = mid_spheres([spheres[k["sphere"]]["offset"] for k in kids],
                                         [spheres[k["sphere"]]["radius"] for k in kids], 1)
-                E.raw("if (!EXT && env.near_ok) {  // primitive records only, at most kNearMax")
+                E.raw(f"if (!EXT && {near_gate} && env.near_ok) {{  // primitive records only, at most kNearMax")
                 E.indent += 1
                 w = self.world(fr.center(next(iter(frames)), off), next(iter(bases)))
                 E.raw(f"const NearSet ns = env_near<Grp>(env, {w[0]}, {w[1]}, {w[2]}, {flit(R)});  "
@@ -1098,6 +1102,8 @@ class RobotGen:
         """<robot>_children(check, q..., env, base): check c's children, frames recomputed"""
         m = self.m
         body = []
+        if self.name in NEAR_CHILDREN:  # a TU may compile the near-set children out (vgpu_staged.hip part 0)
+            body += ["#ifndef VGPU_NEAR_CHILDREN", "#define VGPU_NEAR_CHILDREN 1", "#endif"]
         for c, o in enumerate(order):
             E = Emitter()
             E.indent = 2
@@ -1116,7 +1122,10 @@ class RobotGen:
                 for sa, sb in ck["children"]:
                     fr.rot(m["spheres"][sa]["frame"])
                     fr.rot(m["spheres"][sb]["frame"])
-            self.emit_children(E, fr, kind, ck, "return true;", "primitive" if self.name in EARLY_CHILDREN else False)
+            self.emit_children(E, fr, kind, ck, "return true;", "primitive" if self.name in EARLY_CHILDREN else False,
+                               near_ok=(kind == "env" and self.name in NEAR_CHILDREN and
+                                        len(ck["children"]) >= NEAR_CHILDREN[self.name]),
+                               near_gate="VGPU_NEAR_CHILDREN")
             body += [f"    case {c}: {{  // {kind}: {label} ({len(ck['children'])} children)"] + E.lines + \
                     ["        return false;", "    }"]
         out = self.signature("bool", "children", "int check, ")
