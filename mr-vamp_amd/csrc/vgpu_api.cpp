@@ -49,7 +49,7 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
     int vgpu_##NAME##_staged_checks(void);                                                                           \
     uint64_t vgpu_##NAME##_staged_env_checks(void);                                                                  \
     int vgpu_##NAME##_staged_mask_bytes(void);                                                                       \
-    int vgpu_##NAME##_staged_class(int c);                                                                           \
+    int vgpu_##NAME##_staged_class(int c, int ext);                                                                  \
     size_t vgpu_##NAME##_staged_plan_bytes(void);                                                                    \
     uint32_t vgpu_##NAME##_staged_blocks(int kind, uint32_t n_groups);                                               \
     hipError_t vgpu_##NAME##_staged_bound(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
@@ -59,7 +59,7 @@ hipError_t vgpu_launch_total64(const uint32_t* cnt, size_t n, unsigned long long
                                           const void* mask, uint32_t n_groups, uint64_t set, const uint8_t* valid,   \
                                           uint32_t* counts, hipStream_t st);                                         \
     hipError_t vgpu_##NAME##_staged_plan(const uint32_t* offs, uint32_t nb, uint32_t W, uint64_t set,                \
-                                         uint32_t n_groups, void* plan, hipStream_t st);                             \
+                                         uint32_t n_groups, void* plan, int ext, hipStream_t st);                    \
     hipError_t vgpu_##NAME##_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           const void* mask, uint32_t n_groups, uint64_t set, const void* plan,       \
                                           const uint8_t* valid, const uint32_t* offs, uint32_t* items,               \
@@ -1303,14 +1303,14 @@ struct StagedOps {
     int (*checks)(void);
     uint64_t (*env_checks)(void);
     int (*mask_bytes)(void);
-    int (*child_class)(int);
+    int (*child_class)(int, int);  // (check, point-cloud / heightfield environment)
     size_t (*plan_bytes)(void);
     uint32_t (*blocks)(int, uint32_t);
     hipError_t (*bound)(int, const void*, const void*, const void*, const void*, uint64_t, uint32_t, const EnvView*,
                         const float*, int, void*, uint8_t*, hipStream_t);
     hipError_t (*count)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
                         const uint8_t*, uint32_t*, hipStream_t);
-    hipError_t (*plan)(const uint32_t*, uint32_t, uint32_t, uint64_t, uint32_t, void*, hipStream_t);
+    hipError_t (*plan)(const uint32_t*, uint32_t, uint32_t, uint64_t, uint32_t, void*, int, hipStream_t);
     hipError_t (*queue)(int, const void*, const void*, const void*, const void*, const void*, uint32_t, uint64_t,
                         const void*, const uint8_t*, const uint32_t*, uint32_t*, const void*, hipStream_t);
     hipError_t (*children)(int, const void*, const void*, const void*, const void*, uint64_t, const void*,
@@ -1459,6 +1459,7 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const voi
     uint64_t all = checks >= 64 ? ~0ull : ((1ull << checks) - 1ull);
     if (use_lead) all &= ~(1ull << lead);  // decided by the lead pass
     const uint64_t env_bits = ops.env_checks();
+    const int ext = (v->n_hf > 0 || v->n_pc > 0) ? 1 : 0;  // the children kernels' EXT instantiation (class table)
     // every check's fired groups (groups still valid): segment boundaries offs[k * nb], k = 0..checks
     HIPCHK(c, ops.count(kind, s0, s1, s2, s3, mask, (uint32_t)n, all, valid, counts, c->cur));
     HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
@@ -1504,14 +1505,14 @@ static int staged_pass(vgpu_ctx* c, const StagedOps& ops_in, int kind, const voi
         set &= all;
         uint32_t ub[4] = {0, 0, 0, 0};  // per children class, from the first round's counts
         for (int k = 0; k < checks; ++k)
-            if ((set >> k) & 1u) ub[ops.child_class(k)] += (fired[k] + W - 1) / W * W;
+            if ((set >> k) & 1u) ub[ops.child_class(k, ext)] += (fired[k] + W - 1) / W * W;
         if (!(ub[0] | ub[1] | ub[2] | ub[3])) continue;
         if (!first_round) {
             HIPCHK(c, ops.count(kind, s0, s1, s2, s3, mask, (uint32_t)n, set, valid, counts, c->cur));
             HIPCHK(c, vgpu_launch_scan(counts, offs, cells, tmp, scan_bytes, c->cur));
         }
         first_round = false;
-        HIPCHK(c, ops.plan(offs, (uint32_t)nb, W, set, (uint32_t)n, plan, c->cur));
+        HIPCHK(c, ops.plan(offs, (uint32_t)nb, W, set, (uint32_t)n, plan, ext, c->cur));
         HIPCHK(c, ops.queue(kind, s0, s1, s2, s3, mask, (uint32_t)n, set, plan, valid, offs, c->st_items, v->base,
                             c->cur));
         HIPCHK(c, ops.children(kind, s0, s1, s2, s3, first, plan, ub, c->st_items, v, bases, valid, c->cur));

@@ -68,6 +68,21 @@ struct ChildClasses<R, std::void_t<decltype(R::kClassOf)>> {
     __host__ __device__ static constexpr int waves(int k) { return R::kClassWaves[k]; }
 };
 
+// R::kExtClassOf / kExtClasses (optional): the class table of the point-cloud (EXT) instantiations -- their
+// environment children run the CAPT queries, not near sets, so a robot may keep fewer classes there (the Panda's
+// near-set class 3 is folded back into class 0 with a point cloud).  The host asks for the table of the pass's
+// environment (vgpu_<name>_staged_class(c, ext)); plan and children kernels take it from their EXT parameter.
+template <class R, bool EXT, class = void>
+struct ChildClassesE : ChildClasses<R> {
+};
+template <class R>
+struct ChildClassesE<R, true, std::void_t<decltype(R::kExtClassOf)>> {
+    static_assert(R::kExtClasses <= kPlanMaxClasses, "too many children classes");
+    static constexpr int n = R::kExtClasses;
+    __host__ __device__ static constexpr int of(int c) { return R::kExtClassOf[c]; }
+    __host__ __device__ static constexpr int waves(int k) { return R::kClassWaves[k]; }
+};
+
 // waves/EU of a children kernel: with a point cloud (EXT) at most VGPU_EXT_CHILD_WAVES -- the deferred
 // queries' queue bookkeeping adds live registers: at 7 waves (72 VGPRs) the Panda / pair-arm class-0 kernels
 // spilled 16-23 VGPRs (48-72 B scratch per lane); at 5 (96) none do (tests/test_kernel_resources.py).  A/B on
@@ -86,7 +101,7 @@ struct ExtClassWaves<R, std::void_t<decltype(R::kExtClassWaves)>> {
 };
 template <class R, int K, bool EXT>
 struct ChildWaves {
-    static constexpr int w = ChildClasses<R>::waves(K);
+    static constexpr int w = ChildClassesE<R, EXT>::waves(K);
     static constexpr int cap = ExtClassWaves<R>::of(K);
     static constexpr int v = (EXT && w > cap) ? cap : w;
 };
@@ -464,11 +479,11 @@ __global__ __launch_bounds__(kStagedBlock) void count_kernel(Src src, const type
 
 // After a round's count + scan: fired[c] = offs[(c+1)*nb] - offs[c*nb]; the round's segments,
 // class-major.  One lane per check computes its fired count, lane 0 lays them out.
-template <class R>
+template <class R, bool EXT>
 __global__ __launch_bounds__(64) void plan_kernel(const uint32_t* __restrict__ offs, uint32_t nb, uint32_t W,
                                                   uint64_t set, uint32_t n_groups, StagedPlan* __restrict__ plan)
 {
-    using CC = ChildClasses<R>;
+    using CC = ChildClassesE<R, EXT>;
     __shared__ uint32_t fired[R::kChecks];
     for (int k = threadIdx.x; k < R::kChecks; k += 64)
         fired[k] = offs[(size_t)(k + 1) * nb] - offs[(size_t)k * nb];
@@ -551,7 +566,7 @@ __device__ __forceinline__ int children_of_class(uint32_t item0, const StagedPla
     if constexpr (C == R::kChecks) {
         return -1;
     } else {
-        if constexpr (ChildClasses<R>::of(C) == K) {
+        if constexpr (ChildClassesE<R, EXT>::of(C) == K) {
             if (item0 >= plan->start[C] && item0 < plan->end[C])
                 return R::template children<Grp, EXT>(C, v, env, bs) ? 1 : 0;
         }
@@ -579,7 +594,7 @@ __global__ __launch_bounds__(kStagedBlock, (ChildWaves<R, K, EXT>::v)) void chil
     uint32_t fill = 0;
 #pragma unroll
     for (int k = 0; k < R::kChecks; ++k)
-        if (ChildClasses<R>::of(k) == K && item0 >= plan->start[k] && item0 < plan->end[k]) fill = plan->fill[k];
+        if (ChildClassesE<R, EXT>::of(k) == K && item0 >= plan->start[k] && item0 < plan->end[k]) fill = plan->fill[k];
     if (item >= fill) return;  // segment padding (group-uniform)
     const uint32_t g = VGPU_DCLAMP(env.base, items[item], plan->n_groups, DBG_CHILD_GROUP);
     float v[R::D];
@@ -669,7 +684,7 @@ struct StagedHost {
                                        const uint32_t* items, const EnvView* env, const Bases& bs,
                                        uint8_t* valid, hipStream_t st)
     {
-        if constexpr (K == ChildClasses<R>::n) {
+        if constexpr (K == ChildClassesE<R, EXT>::n) {
             return hipSuccess;
         } else {
             const size_t threads = (size_t)ub[K] * Src::G;
@@ -694,9 +709,12 @@ struct StagedHost {
     }
 
     static hipError_t plan(const uint32_t* offs, uint32_t nb, uint32_t W, M set, uint32_t n_groups, StagedPlan* plan,
-                           hipStream_t st)
+                           int ext, hipStream_t st)
     {
-        hipLaunchKernelGGL((plan_kernel<R>), dim3(1), dim3(64), 0, st, offs, nb, W, (uint64_t)set, n_groups, plan);
+        if (ext)
+            hipLaunchKernelGGL((plan_kernel<R, true>), dim3(1), dim3(64), 0, st, offs, nb, W, (uint64_t)set, n_groups, plan);
+        else
+            hipLaunchKernelGGL((plan_kernel<R, false>), dim3(1), dim3(64), 0, st, offs, nb, W, (uint64_t)set, n_groups, plan);
         return hipGetLastError();
     }
 
@@ -748,7 +766,10 @@ struct StagedHost {
     int vgpu_##NAME##_staged_checks(void) { return R::kChecks; }                                                     \
     uint64_t vgpu_##NAME##_staged_env_checks(void) { return (uint64_t)R::kEnvChecks; }                             \
     int vgpu_##NAME##_staged_mask_bytes(void) { return (int)sizeof(typename R::Mask) * (vgpu::BothChunks<R>::v ? 2 : 1); } \
-    int vgpu_##NAME##_staged_class(int c) { return vgpu::ChildClasses<R>::of(c); }                                   \
+    int vgpu_##NAME##_staged_class(int c, int ext)                                                                   \
+    {                                                                                                                \
+        return ext ? vgpu::ChildClassesE<R, true>::of(c) : vgpu::ChildClassesE<R, false>::of(c);                    \
+    }                                                                                                                \
     size_t vgpu_##NAME##_staged_plan_bytes(void) { return sizeof(vgpu::StagedPlan); }                               \
     uint32_t vgpu_##NAME##_staged_blocks(int, uint32_t n_groups)                                                     \
     {                                                                                                                \
@@ -786,9 +807,10 @@ struct StagedHost {
         });                                                                                                          \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_plan(const uint32_t* offs, uint32_t nb, uint32_t W, uint64_t set,                \
-                                         uint32_t n_groups, void* plan, hipStream_t st)                              \
+                                         uint32_t n_groups, void* plan, int ext, hipStream_t st)                     \
     {                                                                                                                \
-        return vgpu::StagedHost<R>::plan(offs, nb, W, (typename R::Mask)set, n_groups, (vgpu::StagedPlan*)plan, st); \
+        return vgpu::StagedHost<R>::plan(offs, nb, W, (typename R::Mask)set, n_groups, (vgpu::StagedPlan*)plan, ext, \
+                                         st);                                                                        \
     }                                                                                                                \
     hipError_t vgpu_##NAME##_staged_queue(int kind, const void* s0, const void* s1, const void* s2, const void* s3,  \
                                           const void* mask, uint32_t n_groups, uint64_t set, const void* plan,       \
