@@ -435,8 +435,18 @@ struct LeadCheck<R, std::void_t<decltype(R::kLeadCheck)>> {
     static constexpr int v = R::kLeadCheck;
 };
 
+// waves/EU of the lead kernel: R::kLeadWaves, else the bound stage's
+template <class R, class Src, class = void>
+struct LeadWaves {
+    static constexpr int v = BoundWaves<R, Src>::v;
+};
 template <class R, class Src>
-__global__ __launch_bounds__(kStagedBlock, (BoundWaves<R, Src>::v)) void lead_kernel(Src src, uint32_t n_groups,
+struct LeadWaves<R, Src, std::void_t<decltype(R::kLeadWaves)>> {
+    static constexpr int v = R::kLeadWaves;
+};
+
+template <class R, class Src>
+__global__ __launch_bounds__(kStagedBlock, (LeadWaves<R, Src>::v)) void lead_kernel(Src src, uint32_t n_groups,
                                                                                 EnvView env, Bases bs,
                                                                                 uint8_t* __restrict__ valid)
 {

@@ -33,6 +33,9 @@
 #ifndef VGPU_PANDA_MID_KINDS
 #define VGPU_PANDA_MID_KINDS ((1u << 3) | (1u << 4))
 #endif
+#ifndef VGPU_PANDA_LEAD_WAVES
+#define VGPU_PANDA_LEAD_WAVES 8  // 64 VGPRs, no spill (5, the bound stage budget: 67 VGPRs = 7 waves/EU; A/B set B 1.93-1.94 -> 1.90-1.91 ms)
+#endif
 #ifndef VGPU_PANDA_HEAD_LIST
 #define VGPU_PANDA_HEAD_LIST 1
 #endif
@@ -100,6 +103,7 @@ struct PandaR {
     }
     // the lead pass (vgpu_staged.hh lead_kernel): check 8, the link-5 environment check
     static constexpr int kLeadCheck = panda_lead_check;
+    static constexpr int kLeadWaves = VGPU_PANDA_LEAD_WAVES;
     // after the lead pass, the heads' bound / children stages run over the compacted list of live edges
     static constexpr bool kHeadList = VGPU_PANDA_HEAD_LIST;
     template <class Grp>
